@@ -1,0 +1,304 @@
+"""ctypes mirror of include/compton2d.h and numpy builders for its structs.
+
+The C-ABI takes every per-zone table as (pointer, strides); the builders
+here keep dense numpy arrays in the layouts the reference COMMON blocks
+would hand over (src/commonblock.f:53-70) and describe them with strides,
+so the same structs drive the HIP library and the test oracle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+N_VOL = 400
+NUM_NT = 200
+NPHFIELD = 400
+NPHOMAX = 128
+NPHLCMAX = 10
+NMUMAX = 32
+NFMAX = 500
+MAXZONE = 99
+EVENT_WORDS = 7
+NCOUNTERS = 16
+
+COMTOT_EXACT = 0
+COMTOT_TABLE = 1
+
+CNT_STEPS, CNT_ESCAPES, CNT_CENSUS, CNT_COLLIDE, CNT_KILLED, CNT_SOURCES, \
+    CNT_COMPB, CNT_EVENTS, CNT_GENS = range(9)
+
+ERRORS = {
+    0: "C2D_OK", -1: "C2D_E_ARG", -2: "C2D_E_HIP", -3: "C2D_E_CENSUS_OVERFLOW",
+    -4: "C2D_E_EVENT_OVERFLOW", -5: "C2D_E_QUEUE_OVERFLOW", -6: "C2D_E_NOMEM",
+    -7: "C2D_E_STATE",
+}
+
+PD = C.POINTER(C.c_double)
+PI32 = C.POINTER(C.c_int32)
+
+
+class Array3(C.Structure):
+    _fields_ = [("data", PD), ("s_i", C.c_int64), ("s_j", C.c_int64), ("s_k", C.c_int64)]
+
+
+class Array2(C.Structure):
+    _fields_ = [("data", PD), ("s_j", C.c_int64), ("s_k", C.c_int64)]
+
+
+class IArray2(C.Structure):
+    _fields_ = [("data", PI32), ("s_j", C.c_int64), ("s_k", C.c_int64)]
+
+
+class Spectrum(C.Structure):
+    _fields_ = [("nfile", C.c_int32), ("E_file", PD), ("a1", PD), ("I_file", PD),
+                ("F_file", PD), ("P_file", PD)]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("nz", C.c_int32), ("nr", C.c_int32), ("rmin", C.c_double), ("zmin", C.c_double),
+        ("z", PD), ("r", PD), ("E_ph", PD), ("E_field", PD), ("gnt", PD),
+        ("nphtotal", C.c_int32), ("hu", PD), ("nph_lc", C.c_int32), ("Elcmin", PD),
+        ("Elcmax", PD), ("nmu", C.c_int32), ("mu", PD),
+        ("split1", C.c_int32), ("split2", C.c_int32), ("split3", C.c_int32),
+        ("spl3_trg", C.c_int32), ("spec_switch", C.c_int32), ("cr_sent", C.c_int32),
+        ("pair_switch", C.c_int32), ("kappa_lag", C.c_int32), ("comtot_mode", C.c_int32),
+        ("device", C.c_int32), ("seed", C.c_uint64), ("rank", C.c_int32), ("world", C.c_int32),
+        ("census_capacity", C.c_int64), ("event_capacity", C.c_int64),
+        ("queue_capacity", C.c_int64),
+    ]
+
+
+class StepIn(C.Structure):
+    _fields_ = [
+        ("ncycle", C.c_int32), ("time", C.c_double), ("dt", C.c_double),
+        ("kappa_tot", Array3), ("eps_tot", Array3), ("eps_th", Array3),
+        ("f_nt", Array3), ("Pnt", Array3),
+        ("n_e", Array2), ("Eloss_th", Array2), ("Eloss_tot", Array2), ("zsurf", Array2),
+        ("ewsv", Array2), ("nsv", IArray2),
+        ("nsurfi", PI32), ("nsurfo", PI32), ("ewsurfi", PD), ("ewsurfo", PD),
+        ("nsurfu", PI32), ("nsurfl", PI32), ("ewsurfu", PD), ("ewsurfl", PD),
+        ("tbbi", PD), ("tbbo", PD), ("tbbu", PD), ("tbbl", PD),
+        ("spec_i", PI32), ("spec_o", PI32), ("spec_u", PI32), ("spec_l", PI32),
+        ("n_spectra", C.c_int32), ("spectra", C.POINTER(Spectrum)),
+    ]
+
+
+class TallyLayout(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in (
+        "edep", "prdep", "ecens", "npcen", "n_field", "E_IC", "nelectron", "fout", "edout",
+        "erlki", "erlko", "erlku", "erlkl", "Ed_in", "counters", "total")]
+
+
+class FpIn(C.Structure):
+    _fields_ = [("ncell", C.c_int32), ("a", PD), ("b", PD), ("c", PD), ("r", PD),
+                ("nt", C.c_int32)]
+
+
+def tally_layout(nz: int, nr: int, nmu: int) -> dict:
+    """Python restatement of c2d_tally_layout_for (include/compton2d.h)."""
+    nc = nz * nr
+    sizes = [("edep", nc), ("prdep", nc), ("ecens", nc), ("npcen", nc),
+             ("n_field", nc * NPHFIELD), ("E_IC", NUM_NT + 2), ("nelectron", NUM_NT + 2),
+             ("fout", nmu * NPHOMAX), ("edout", nmu * NPHLCMAX), ("erlki", nz), ("erlko", nz),
+             ("erlku", nr), ("erlkl", nr), ("Ed_in", nr), ("counters", NCOUNTERS)]
+    out, o = {}, 0
+    for name, n in sizes:
+        out[name] = (o, n)
+        o += n
+    out["total"] = (o, 0)
+    return out
+
+
+def split_tallies(buf: np.ndarray, nz: int, nr: int, nmu: int) -> dict:
+    """View a fused tally buffer as named arrays (reference shapes, 0-based)."""
+    L = tally_layout(nz, nr, nmu)
+    t = {}
+    for name, (o, n) in L.items():
+        if name == "total":
+            continue
+        t[name] = buf[o:o + n]
+    t["edep"] = t["edep"].reshape(nz, nr)
+    t["prdep"] = t["prdep"].reshape(nz, nr)
+    t["ecens"] = t["ecens"].reshape(nz, nr)
+    t["npcen"] = t["npcen"].reshape(nz, nr)
+    t["n_field"] = t["n_field"].reshape(nz, nr, NPHFIELD)
+    t["fout"] = t["fout"].reshape(nmu, NPHOMAX)
+    t["edout"] = t["edout"].reshape(nmu, NPHLCMAX)
+    return t
+
+
+def _pd(a: np.ndarray):
+    return a.ctypes.data_as(PD)
+
+
+def _pi(a: np.ndarray):
+    return a.ctypes.data_as(PI32)
+
+
+@dataclass
+class GridConfig:
+    """Run-constant set-up: what src/setup2d.f leaves in COMMON."""
+    nz: int
+    nr: int
+    rmin: float
+    zmin: float
+    z: np.ndarray            # [nz]
+    r: np.ndarray            # [nr]
+    E_ph: np.ndarray         # [N_VOL]
+    E_field: np.ndarray      # [NPHFIELD]
+    gnt: np.ndarray          # [NUM_NT]
+    hu: np.ndarray           # [nphtotal+1]
+    Elcmin: np.ndarray
+    Elcmax: np.ndarray
+    mu: np.ndarray
+    split1: int = 10
+    split2: int = 10
+    split3: int = 3
+    spl3_trg: int = 10
+    spec_switch: int = 0
+    cr_sent: int = 0
+    pair_switch: int = 0
+    kappa_lag: int = 1
+    comtot_mode: int = COMTOT_EXACT
+    device: int = 0
+    seed: int = 0x5EEDC2D
+    rank: int = 0
+    world: int = 1
+    census_capacity: int = 1 << 20
+    event_capacity: int = 1 << 20
+    queue_capacity: int = 1 << 18
+
+    def to_ctypes(self) -> Config:
+        self._keep = [np.ascontiguousarray(a, dtype=np.float64) for a in (
+            self.z, self.r, self.E_ph, self.E_field, self.gnt, self.hu, self.Elcmin,
+            self.Elcmax, self.mu)]
+        z, r, eph, efield, gnt, hu, elmin, elmax, mu = self._keep
+        assert eph.size == N_VOL and efield.size == NPHFIELD and gnt.size == NUM_NT
+        return Config(
+            nz=self.nz, nr=self.nr, rmin=self.rmin, zmin=self.zmin, z=_pd(z), r=_pd(r),
+            E_ph=_pd(eph), E_field=_pd(efield), gnt=_pd(gnt), nphtotal=hu.size - 1, hu=_pd(hu),
+            nph_lc=elmin.size, Elcmin=_pd(elmin), Elcmax=_pd(elmax), nmu=mu.size, mu=_pd(mu),
+            split1=self.split1, split2=self.split2, split3=self.split3, spl3_trg=self.spl3_trg,
+            spec_switch=self.spec_switch, cr_sent=self.cr_sent, pair_switch=self.pair_switch,
+            kappa_lag=self.kappa_lag, comtot_mode=self.comtot_mode, device=self.device,
+            seed=self.seed, rank=self.rank, world=self.world,
+            census_capacity=self.census_capacity, event_capacity=self.event_capacity,
+            queue_capacity=self.queue_capacity)
+
+
+@dataclass
+class SpectrumTable:
+    """file_sp output (src/imcsurf2d_para.f:544-685)."""
+    E_file: np.ndarray
+    a1: np.ndarray
+    I_file: np.ndarray
+    F_file: np.ndarray
+    P_file: np.ndarray
+
+
+@dataclass
+class StepInputs:
+    """Per-step transport inputs (what imcgen2d/volume_em/file_sp leave in COMMON).
+
+    Dense C-order layouts: kappa_tot/eps_tot/eps_th [nz,nr,N_VOL],
+    f_nt/Pnt [nz,nr,NUM_NT], zone scalars [nz,nr], z-surface arrays [nz],
+    r-surface arrays [nr].
+    """
+    ncycle: int
+    time: float
+    dt: float
+    kappa_tot: np.ndarray
+    eps_tot: np.ndarray
+    eps_th: np.ndarray
+    f_nt: np.ndarray
+    Pnt: np.ndarray
+    n_e: np.ndarray
+    Eloss_th: np.ndarray
+    Eloss_tot: np.ndarray
+    zsurf: np.ndarray
+    ewsv: np.ndarray
+    nsv: np.ndarray
+    nsurfi: np.ndarray
+    nsurfo: np.ndarray
+    ewsurfi: np.ndarray
+    ewsurfo: np.ndarray
+    nsurfu: np.ndarray
+    nsurfl: np.ndarray
+    ewsurfu: np.ndarray
+    ewsurfl: np.ndarray
+    tbbi: np.ndarray
+    tbbo: np.ndarray
+    tbbu: np.ndarray
+    tbbl: np.ndarray
+    spectra: List[SpectrumTable] = field(default_factory=list)
+    spec_i: Optional[np.ndarray] = None
+    spec_o: Optional[np.ndarray] = None
+    spec_u: Optional[np.ndarray] = None
+    spec_l: Optional[np.ndarray] = None
+
+    def to_ctypes(self) -> StepIn:
+        nz, nr = self.n_e.shape
+        keep = []
+
+        def d(a):
+            a = np.ascontiguousarray(a, dtype=np.float64)
+            keep.append(a)
+            return a
+
+        def i(a):
+            a = np.ascontiguousarray(a, dtype=np.int32)
+            keep.append(a)
+            return a
+
+        def a3(a, n):
+            a = d(a)
+            assert a.shape == (nz, nr, n), (a.shape, (nz, nr, n))
+            return Array3(_pd(a), 1, nr * n, n)
+
+        def a2(a):
+            a = d(a)
+            assert a.shape == (nz, nr)
+            return Array2(_pd(a), nr, 1)
+
+        nsv = i(self.nsv)
+        s = StepIn()
+        s.ncycle = int(self.ncycle)
+        s.time = float(self.time)
+        s.dt = float(self.dt)
+        s.kappa_tot = a3(self.kappa_tot, N_VOL)
+        s.eps_tot = a3(self.eps_tot, N_VOL)
+        s.eps_th = a3(self.eps_th, N_VOL)
+        s.f_nt = a3(self.f_nt, NUM_NT)
+        s.Pnt = a3(self.Pnt, NUM_NT)
+        s.n_e = a2(self.n_e)
+        s.Eloss_th = a2(self.Eloss_th)
+        s.Eloss_tot = a2(self.Eloss_tot)
+        s.zsurf = a2(self.zsurf)
+        s.ewsv = a2(self.ewsv)
+        s.nsv = IArray2(_pi(nsv), nr, 1)
+        s.nsurfi, s.nsurfo = _pi(i(self.nsurfi)), _pi(i(self.nsurfo))
+        s.ewsurfi, s.ewsurfo = _pd(d(self.ewsurfi)), _pd(d(self.ewsurfo))
+        s.nsurfu, s.nsurfl = _pi(i(self.nsurfu)), _pi(i(self.nsurfl))
+        s.ewsurfu, s.ewsurfl = _pd(d(self.ewsurfu)), _pd(d(self.ewsurfl))
+        s.tbbi, s.tbbo = _pd(d(self.tbbi)), _pd(d(self.tbbo))
+        s.tbbu, s.tbbl = _pd(d(self.tbbu)), _pd(d(self.tbbl))
+        spec_default_z = np.zeros(nz, np.int32) if self.spectra else np.full(nz, -1, np.int32)
+        spec_default_r = np.zeros(nr, np.int32) if self.spectra else np.full(nr, -1, np.int32)
+        s.spec_i = _pi(i(self.spec_i if self.spec_i is not None else spec_default_z))
+        s.spec_o = _pi(i(self.spec_o if self.spec_o is not None else spec_default_z))
+        s.spec_u = _pi(i(self.spec_u if self.spec_u is not None else spec_default_r))
+        s.spec_l = _pi(i(self.spec_l if self.spec_l is not None else spec_default_r))
+        nsp = len(self.spectra)
+        arr = (Spectrum * max(nsp, 1))()
+        for m, sp in enumerate(self.spectra):
+            e, a1, ii, f, p = (d(x) for x in (sp.E_file, sp.a1, sp.I_file, sp.F_file, sp.P_file))
+            arr[m] = Spectrum(e.size, _pd(e), _pd(a1), _pd(ii), _pd(f), _pd(p))
+        keep.append(arr)
+        s.n_spectra = nsp
+        s.spectra = C.cast(arr, C.POINTER(Spectrum))
+        s._keep = keep
+        return s

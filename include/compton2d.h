@@ -1,0 +1,247 @@
+/*
+ * compton2d.h — C-ABI of the MI355X-native Compton2d IMC engine.
+ *
+ * Drop-in boundary for the reference's per-step transport entry points
+ * (all argument-less Fortran subroutines that talk through COMMON blocks):
+ *
+ *   reference entry point                         replaced by
+ *   -------------------------------------------   --------------------------------------
+ *   src/imcfield2d.f:5   imcfield2d (census)       c2d_transport_step  (census phase)
+ *   src/imcvol2d_para.f:1 imcvol2d (volume src)    c2d_transport_step  (volume phase)
+ *   src/imcsurf2d_para.f:1 imcsurf2d (surface src) c2d_transport_step  (surface phase)
+ *   src/imcredist.f:5    imcredist (census bal.)   not needed: census stays on its GPU
+ *   src/xec2d.f:325/371  xec_add/graphics_collect  c2d_tally_device_ptr + one all-reduce
+ *   src/update2d.f:1929  cens_add_up (REDUCE)      c2d_tally_device_ptr + one all-reduce
+ *   src/imcleak2d.f:171  event-file writes         c2d_events
+ *   src/census2d.f:1-76  write_cens/read_cens      c2d_census_export / c2d_census_import
+ *   src/update2d.f:337   FP_calc + tridag          c2d_fp_step
+ *
+ * Every array argument is (pointer, strides) so Fortran COMMON arrays with
+ * their fixed leading extents (general.pa: n_vol=400, jmax=kmax=99,
+ * num_nt=200) are passed without copies; the library gathers only the
+ * [1:nz,1:nr] sub-block.  Indices below are 0-based: element (i,j,k) of a
+ * c2d_array3 lives at data[i*s_i + j*s_j + k*s_k] with j=0..nz-1 (z zone),
+ * k=0..nr-1 (r zone).  For kappa_tot(n_vol,jmax,kmax) pass s_i=1,
+ * s_j=n_vol, s_k=n_vol*jmax; for f_nt(jmax,kmax,num_nt) pass s_j=1,
+ * s_k=jmax, s_i=jmax*kmax.
+ *
+ * Errors: every call returns 0 or a negative C2D_E_* code; the message is
+ * in c2d_last_error().  Nothing calls exit() (the reference `stop`s at
+ * src/imctrk2d.f:573-577, src/imcfield2d.f:84-87).
+ * Threading: all calls on one context from one host thread; calls are
+ * synchronous on return unless documented otherwise.
+ */
+#ifndef COMPTON2D_H
+#define COMPTON2D_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Compile-time extents of the reference (src/general.pa:7-30). */
+#define C2D_N_VOL     400   /* photon energy grid of kappa_tot/eps_tot (n_vol)  */
+#define C2D_NUM_NT    200   /* electron Lorentz-factor grid (num_nt)            */
+#define C2D_NPHFIELD  400   /* internal photon-field grid n_field (nphfield)    */
+#define C2D_NPHOMAX   128   /* spectrum bins (nphomax)                          */
+#define C2D_NPHLCMAX  10    /* light-curve bands (nphlcmax)                     */
+#define C2D_NMUMAX    32    /* angular bins (nmumax)                            */
+#define C2D_NFMAX     500   /* external seed spectrum table (nfmax)             */
+#define C2D_MAXZONE   99    /* jmax = kmax                                      */
+
+/* Error codes. */
+#define C2D_OK                  0
+#define C2D_E_ARG              -1   /* bad argument / unsupported option          */
+#define C2D_E_HIP              -2   /* HIP runtime error                          */
+#define C2D_E_CENSUS_OVERFLOW  -3   /* replaces `stop 'too many photons'`         */
+#define C2D_E_EVENT_OVERFLOW   -4   /* escape-event buffer full                   */
+#define C2D_E_QUEUE_OVERFLOW   -5   /* scatter-secondary queue full               */
+#define C2D_E_NOMEM            -6
+#define C2D_E_STATE            -7   /* call order violated                        */
+
+/* comtot (src/comtot2d.f:1-334, icoms=6) evaluation mode. */
+#define C2D_COMTOT_EXACT  0   /* 199-term electron-spectrum sum per call (reference)   */
+#define C2D_COMTOT_TABLE  1   /* per-cell cubic table in log(xnu), rebuilt every step  */
+
+typedef struct c2d_array3 { const double* data; int64_t s_i, s_j, s_k; } c2d_array3;
+typedef struct c2d_array2 { const double* data; int64_t s_j, s_k; } c2d_array2;
+typedef struct c2d_iarray2 { const int32_t* data; int64_t s_j, s_k; } c2d_iarray2;
+
+/* Seed spectrum for a surface with tbb <= 0: the normalised table that
+ * file_sp (src/imcsurf2d_para.f:544-685, host-side) leaves in COMMON /insp/
+ * and file_sample (:694-788) draws from. */
+typedef struct c2d_spectrum {
+  int32_t nfile;
+  const double* E_file;   /* [nfile]   */
+  const double* a1;       /* [nfile-1] */
+  const double* I_file;   /* [nfile-1] */
+  const double* F_file;   /* [nfile]   */
+  const double* P_file;   /* [nfile-1] cumulative, normalised */
+} c2d_spectrum;
+
+/* Run-constant set-up (src/setup2d.f:47-222, src/reader.f). */
+typedef struct c2d_config {
+  int32_t nz, nr;                 /* zones (reference nz, nr <= 99)           */
+  double  rmin, zmin;             /* inner radius, lower z (zmin = 0 in ref)  */
+  const double* z;                /* [nz] upper z boundary of zone j          */
+  const double* r;                /* [nr] outer r boundary of zone k          */
+  const double* E_ph;             /* [C2D_N_VOL] energy grid of kappa/eps     */
+  const double* E_field;          /* [C2D_NPHFIELD] grid of n_field           */
+  const double* gnt;              /* [C2D_NUM_NT] gamma-1 grid                */
+  int32_t nphtotal;               /* spectrum bins; hu has nphtotal+1 edges   */
+  const double* hu;
+  int32_t nph_lc;                 /* light-curve bands                        */
+  const double* Elcmin;
+  const double* Elcmax;
+  int32_t nmu;                    /* angular bins                             */
+  const double* mu;               /* [nmu] upper bin edges                    */
+  int32_t split1, split2, split3, spl3_trg;  /* variance reduction (COMMON /split/) */
+  int32_t spec_switch;            /* 0: escaping spectrum into fout            */
+  int32_t cr_sent;                /* Compton reflection; only 0 supported      */
+  int32_t pair_switch;            /* gamma-gamma; inert in the MPI reference (H6) */
+  int32_t kappa_lag;              /* 1: census+volume use previous step's kappa_tot (H3) */
+  int32_t comtot_mode;            /* C2D_COMTOT_EXACT | C2D_COMTOT_TABLE       */
+  int32_t device;                 /* HIP device ordinal                        */
+  uint64_t seed;                  /* lineage RNG seed (replaces rseed)        */
+  int32_t rank, world;            /* source sharding: this context tracks sources with
+                                     (global source index % world) == rank       */
+  int64_t census_capacity;        /* packets (per context)                     */
+  int64_t event_capacity;         /* escape events per step                    */
+  int64_t queue_capacity;         /* scatter records per generation            */
+} c2d_config;
+
+/* Per-step inputs (what imcgen2d/volume_em/file_sp leave in COMMON). */
+typedef struct c2d_step_in {
+  int32_t ncycle;                 /* step counter (events only for ncycle > 0) */
+  double  time, dt;               /* time, dt(1)                              */
+  c2d_array3 kappa_tot;           /* (i<400, j, k) absorption [1/cm]          */
+  c2d_array3 eps_tot;             /* (i<400, j, k) volume emission CDF        */
+  c2d_array3 eps_th;              /* (i<400, j, k) thermal-surface CDF        */
+  c2d_array3 f_nt;                /* (i<200, j, k) electron spectrum          */
+  c2d_array3 Pnt;                 /* (i<200, j, k) electron CDF               */
+  c2d_array2 n_e;                 /* electron density                         */
+  c2d_array2 Eloss_th, Eloss_tot; /* thermal / total emitted energy           */
+  c2d_array2 zsurf;               /* zone surface area                        */
+  c2d_array2 ewsv;                /* volume packet weight                     */
+  c2d_iarray2 nsv;                /* volume packets per zone                  */
+  const int32_t* nsurfi; const int32_t* nsurfo;  /* [nz] inner/outer z-surface packets */
+  const double*  ewsurfi; const double*  ewsurfo; /* [nz] weights                       */
+  const int32_t* nsurfu; const int32_t* nsurfl;  /* [nr] upper/lower r-surface packets */
+  const double*  ewsurfu; const double*  ewsurfl; /* [nr]                                */
+  const double*  tbbi; const double* tbbo;        /* [nz] boundary temps at time index ti */
+  const double*  tbbu; const double* tbbl;        /* [nr]                                 */
+  const int32_t* spec_i; const int32_t* spec_o;   /* [nz] spectrum index for tbb<=0       */
+  const int32_t* spec_u; const int32_t* spec_l;   /* [nr]                                  */
+  int32_t n_spectra;
+  const c2d_spectrum* spectra;
+} c2d_step_in;
+
+/* Fused per-step tally buffer (f64).  One all-reduce over this buffer
+ * replaces xec_add, graphics_collect, cens_add_up and E_add_up's scalar
+ * MPI_REDUCE loops.  Offsets are in doubles. */
+typedef struct c2d_tally_layout {
+  int64_t edep, prdep, ecens, npcen;  /* [ncell] each, cell = j*nr + k        */
+  int64_t n_field;                    /* [ncell][C2D_NPHFIELD]                */
+  int64_t E_IC, nelectron;            /* [C2D_NUM_NT+2] (reference index i)   */
+  int64_t fout;                       /* [nmu][C2D_NPHOMAX]: fout(mu,jgpsp)   */
+  int64_t edout;                      /* [nmu][C2D_NPHLCMAX]                  */
+  int64_t erlki, erlko;               /* [nz]                                 */
+  int64_t erlku, erlkl, Ed_in;        /* [nr]                                 */
+  int64_t counters;                   /* [C2D_NCOUNTERS]                      */
+  int64_t total;
+} c2d_tally_layout;
+
+/* counters[] entries (exact integers stored as f64). */
+#define C2D_CNT_STEPS      0   /* packet-steps: passes through imctrk2d.f:228-485 */
+#define C2D_CNT_ESCAPES    1   /* packets leaving the system (imcleak)           */
+#define C2D_CNT_CENSUS     2   /* packets written to census                       */
+#define C2D_CNT_COLLIDE    3   /* Compton collisions (ikind=3)                    */
+#define C2D_CNT_KILLED     4   /* weight kills (ewnew <= wtmin)                   */
+#define C2D_CNT_SOURCES    5   /* source packets started (census+volume+surface)  */
+#define C2D_CNT_COMPB      6   /* compb2d calls                                    */
+#define C2D_CNT_EVENTS     7   /* event-file records written                      */
+#define C2D_CNT_GENS       8   /* scatter generations launched                    */
+#define C2D_NCOUNTERS      16
+
+static inline void c2d_tally_layout_for(int32_t nz, int32_t nr, int32_t nmu,
+                                        c2d_tally_layout* L) {
+  int64_t nc = (int64_t)nz * nr, o = 0;
+  L->edep = o; o += nc;
+  L->prdep = o; o += nc;
+  L->ecens = o; o += nc;
+  L->npcen = o; o += nc;
+  L->n_field = o; o += nc * C2D_NPHFIELD;
+  L->E_IC = o; o += C2D_NUM_NT + 2;
+  L->nelectron = o; o += C2D_NUM_NT + 2;
+  L->fout = o; o += (int64_t)nmu * C2D_NPHOMAX;
+  L->edout = o; o += (int64_t)nmu * C2D_NPHLCMAX;
+  L->erlki = o; o += nz;
+  L->erlko = o; o += nz;
+  L->erlku = o; o += nr;
+  L->erlkl = o; o += nr;
+  L->Ed_in = o; o += nr;
+  L->counters = o; o += C2D_NCOUNTERS;
+  L->total = o;
+}
+
+/* Escape event = one line of p###_evb.dat (src/imcleak2d.f:171,181):
+ * t_bound, xnu [keV], ew [erg], rpre, zpre [cm], wmu, phi. */
+#define C2D_EVENT_WORDS 7
+
+/* Census record (src/imctrk2d.f:558-572; census2d.f 6e14.7 / 6i5):
+ * d6 = rpre, zpre, wmu, phi, ew, xnu; i5 = jgpsp, jgplc, jgpmu, jph, kph
+ * (1-based as in the reference); key = lineage RNG key (replaces the
+ * per-packet fibran seed, hazard H5). */
+
+typedef struct c2d_ctx c2d_ctx;
+
+/* Fokker-Planck per-zone solve (src/update2d.f:337-1739, tridag :2476-2518). */
+typedef struct c2d_fp_in {
+  int32_t ncell;                  /* zones solved in this call                  */
+  const double* a;                /* [ncell][nt] sub-diagonal                   */
+  const double* b;                /* [ncell][nt] diagonal                       */
+  const double* c;                /* [ncell][nt] super-diagonal                 */
+  const double* r;                /* [ncell][nt] right-hand side                */
+  int32_t nt;                     /* unknowns per zone (num_nt-1 = 199 in ref)  */
+} c2d_fp_in;
+
+const char* c2d_version(void);
+int  c2d_init(const c2d_config* cfg, c2d_ctx** out);
+void c2d_finalize(c2d_ctx* ctx);
+const char* c2d_last_error(c2d_ctx* ctx);
+
+/* One MC time step: census + volume + surface transport, all scatter
+ * generations, tallies into the fused device buffer.  Synchronous. */
+int  c2d_transport_step(c2d_ctx* ctx, const c2d_step_in* in);
+
+int  c2d_tally_layout_get(c2d_ctx* ctx, c2d_tally_layout* out);
+/* Device pointer of the fused tally buffer (layout above), valid until the
+ * next step; callers may all-reduce it in place (RCCL) before reading. */
+double* c2d_tally_device_ptr(c2d_ctx* ctx);
+/* Copy the fused tally buffer to host memory (total doubles). */
+int  c2d_tally_download(c2d_ctx* ctx, double* host, int64_t n);
+
+/* Escape events of the last step: copies min(cap, n) records. */
+int  c2d_events(c2d_ctx* ctx, double* buf, int64_t cap, int64_t* n);
+
+/* Census held on the device for the next step. */
+int  c2d_census_count(c2d_ctx* ctx, int64_t* n);
+int  c2d_census_export(c2d_ctx* ctx, double* d6, int32_t* i5, uint64_t* keys,
+                       int64_t cap, int64_t* n);
+int  c2d_census_import(c2d_ctx* ctx, const double* d6, const int32_t* i5,
+                       const uint64_t* keys, int64_t n);
+
+/* Batched tridiagonal (Thomas with the reference's clipping) solve: one
+ * zone per wavefront.  x is [ncell][nt] on the host. */
+int  c2d_fp_tridag(c2d_ctx* ctx, const c2d_fp_in* in, double* x);
+
+/* Device timing of the last step's dominant kernel (transport generation 0):
+ * milliseconds and launches, measured with HIP events on the library's
+ * own stream. */
+int  c2d_last_kernel_ms(c2d_ctx* ctx, double* gen0_ms, double* all_ms, int32_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COMPTON2D_H */

@@ -1,0 +1,51 @@
+#!/usr/bin/env bash
+# oracle/ref/build_ref.sh — TEST INFRASTRUCTURE ONLY.
+#
+# Builds the reference Fortran (bbw7561135/Compton2d, src/ snapshot) from
+# its sources where they lie under /root/reference/src, with the image's
+# own toolchain (AMD flang 22 + MPICH from /opt/conda),
+# plus the serial driver oracle/ref/c2d_refdrv.f.  Outputs go ONLY to
+# oracle/_ref/ (git-ignored).  Nothing here is needed on the GPU box: the
+# tests there use the committed fixtures in tests/golden/.
+#
+# Object list = src/Makefile:39-68 minus the MPI main program compton2d.o.
+set -euo pipefail
+HERE="$(cd "$(dirname "$0")" && pwd)"
+OUT="$HERE/../_ref"
+SRC="${C2D_REFERENCE_SRC:-/root/reference/src}"
+FC="${FC:-/opt/rocm/lib/llvm/bin/flang}"
+MPI_INC="${MPI_INC:-/opt/conda/include}"
+MPI_LIB="${MPI_LIB:-/opt/conda/lib}"
+FFLAGS="${FFLAGS:--O2}"
+
+if [ ! -d "$SRC" ]; then
+  echo "build_ref: reference sources not found at $SRC" >&2
+  exit 2
+fi
+mkdir -p "$OUT/obj" "$OUT/mod"
+
+OBJS="reader setup2d xec2d imcgen2d volume2d gamma1_2d nontherm2d imcsurf2d_para
+      planck2d pp2d imctrk2d census2d compb_2d comtot2d imcdate2d ref_matrix
+      imcleak2d graphics2d imcvol2d_para imcfield2d imcredist icloss2d update2d
+      rand fp_mpi surf_mpi vol_mpi write_record read_record"
+
+pids=()
+for f in $OBJS; do
+  o="$OUT/obj/$f.o"
+  if [ ! -f "$o" ] || [ "$SRC/$f.f" -nt "$o" ]; then
+    "$FC" -c $FFLAGS -I"$MPI_INC" -I"$SRC" -module-dir "$OUT/mod" \
+      "$SRC/$f.f" -o "$o" &
+    pids+=($!)
+    if [ ${#pids[@]} -ge 8 ]; then wait "${pids[0]}"; pids=("${pids[@]:1}"); fi
+  fi
+done
+for p in "${pids[@]}"; do wait "$p"; done
+
+"$FC" -c $FFLAGS -I"$MPI_INC" -I"$SRC" -module-dir "$OUT/mod" \
+  "$HERE/c2d_refdrv.f" -o "$OUT/obj/c2d_refdrv.o"
+
+objs=""
+for f in $OBJS; do objs="$objs $OUT/obj/$f.o"; done
+"$FC" -o "$OUT/c2d_refdrv" "$OUT/obj/c2d_refdrv.o" $objs \
+  -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
+echo "build_ref: $OUT/c2d_refdrv"

@@ -1,0 +1,185 @@
+c     c2d_refdrv.f -- TEST INFRASTRUCTURE ONLY (oracle/ref).
+c
+c     Serial driver for the REFERENCE Fortran (built from
+c     /root/reference/src by oracle/ref/build_ref.sh into
+c     oracle/_ref/).  It runs, in one process, the same per-step
+c     sequence a master + worker pair runs under MPI
+c     (src/xec2d.f:41-110 master, :141-193 worker):
+c        imcgen2d (master part)              src/imcgen2d.f:1-553
+c        worker tally reset                  src/imcgen2d.f:557-601
+c        field_calc (census)                 src/imcfield2d.f:57
+c        vol_calc for every zone             src/imcvol2d_para.f:90
+c        z_surf_calc / r_surf_calc           src/imcsurf2d_para.f:228,353
+c     emulating the worker's lagged kappa_tot (hazard H3: workers
+c     receive kappa_tot only in z_surf_bcast, src/surf_mpi.f:97) and
+c     restoring the master's seeds after field_calc overwrites them
+c     (src/imcfield2d.f:115; volume jobs carry the master's seed,
+c     src/vol_mpi.f:107).  After every step it dumps the transport
+c     inputs and the worker tallies in full precision (stream files)
+c     so tests can compare the C oracle against the reference itself.
+c
+c     usage: c2d_refdrv NSTEPS KLAG    (run inside a prepared case
+c            directory holding input/input.dat + input/input_JJ_KK.dat)
+c
+      program c2d_refdrv
+      implicit none
+      include 'mpif.h'
+      include 'general.pa'
+      include 'commonblock.f'
+c
+      integer nsteps, klag, n, j, k, zone, js, ks, u
+      integer seeds_sv(jmax,kmax)
+      double precision kap_cur(n_vol,jmax,kmax)
+      double precision kap_prev(n_vol,jmax,kmax)
+      double precision t_average
+      character*32 arg
+      character*40 fn
+      save kap_cur, kap_prev, seeds_sv
+c
+      call MPI_INIT(ierr)
+      call MPI_COMM_RANK(MPI_COMM_WORLD, myid, ierr)
+      call MPI_COMM_SIZE(MPI_COMM_WORLD, numprocs, ierr)
+      master = 0
+      call getarg(1, arg)
+      read(arg, *) nsteps
+      call getarg(2, arg)
+      read(arg, *) klag
+c
+      open(unit=4, file='log.txt')
+      call reader
+      call setup
+c
+      nunit_evt = 1001
+      kap_prev = 0.d0
+      ndxout = 0
+      u = 31
+c
+c     static configuration (after setup)
+      open(unit=u, file='config.bin', access='stream',
+     1     form='unformatted', status='replace')
+      write(u) nz, nr, nphtotal, nph_lc, nmu
+      write(u) split1, split2, split3, spl3_trg
+      write(u) spec_switch, cr_sent, pair_switch, rand_switch
+      write(u) rseed, T_const, ntime
+      write(u) rmin, zmin
+      write(u) (z(j), j=1,nz)
+      write(u) (r(k), k=1,nr)
+      write(u) (E_field(j), j=1,nphfield)
+      write(u) (gnt(j), j=1,num_nt)
+      write(u) (hu(j), j=1,nphtotal+1)
+      write(u) (Elcmin(j), j=1,nph_lc)
+      write(u) (Elcmax(j), j=1,nph_lc)
+      write(u) (mu(j), j=1,nmu)
+      close(u)
+c
+      do 500 n = 0, nsteps-1
+c        master part of the step
+         call imcgen2d
+c        worker-side resets (src/imcgen2d.f:559-601)
+         do 10 j = 1, nz
+            erlko(j) = 0.d0
+            erlki(j) = 0.d0
+ 10      continue
+         do 12 k = 1, nr
+            erlku(k) = 0.d0
+            erlkl(k) = 0.d0
+ 12      continue
+         do 14 j = 1, num_nt
+            nelectron(j) = 0
+ 14      continue
+c        time-window index (src/imcsurf2d_para.f:55-64)
+         if (ncycle.eq.0) then
+            ti = 1
+         else
+            t_average = time + 5.d-1*dt(1)
+            do 20 ti = 1, ntime
+               if (t1(ti).gt.t_average) goto 21
+ 20         continue
+ 21         continue
+         endif
+c        transport inputs of this step
+         write(fn, '(a,i3.3,a)') 'in_', n, '.bin'
+         open(unit=u, file=fn, access='stream',
+     1        form='unformatted', status='replace')
+         write(u) ncycle, ti
+         write(u) time, dt(1)
+         write(u) (E_ph(j), j=1,n_vol)
+         write(u) (((kappa_tot(j,js,ks), j=1,n_vol), ks=1,nr),
+     1             js=1,nz)
+         write(u) (((eps_tot(j,js,ks), j=1,n_vol), ks=1,nr), js=1,nz)
+         write(u) (((eps_th(j,js,ks), j=1,n_vol), ks=1,nr), js=1,nz)
+         write(u) (((f_nt(js,ks,j), j=1,num_nt), ks=1,nr), js=1,nz)
+         write(u) (((Pnt(js,ks,j), j=1,num_nt), ks=1,nr), js=1,nz)
+         write(u) ((n_e(js,ks), ks=1,nr), js=1,nz)
+         write(u) ((Eloss_th(js,ks), ks=1,nr), js=1,nz)
+         write(u) ((Eloss_tot(js,ks), ks=1,nr), js=1,nz)
+         write(u) ((zsurf(js,ks), ks=1,nr), js=1,nz)
+         write(u) ((ewsv(js,ks), ks=1,nr), js=1,nz)
+         write(u) ((nsv(js,ks), ks=1,nr), js=1,nz)
+         write(u) (nsurfi(j), j=1,nz), (nsurfo(j), j=1,nz)
+         write(u) (ewsurfi(j), j=1,nz), (ewsurfo(j), j=1,nz)
+         write(u) (nsurfu(k), k=1,nr), (nsurfl(k), k=1,nr)
+         write(u) (ewsurfu(k), k=1,nr), (ewsurfl(k), k=1,nr)
+         write(u) (tbbi(j,ti), j=1,nz), (tbbo(j,ti), j=1,nz)
+         write(u) (tbbu(k,ti), k=1,nr), (tbbl(k,ti), k=1,nr)
+         write(u) rseed
+         close(u)
+c
+c        per-step event file (the reference appends to p###_evb.dat)
+         write(fn, '(a,i3.3,a)') 'ev_', n, '.dat'
+         open(unit=nunit_evt, file=fn, status='replace')
+c        census transport with the worker's previous kappa_tot (H3)
+         seeds_sv = seeds
+         kap_cur = kappa_tot
+         if (klag.eq.1) kappa_tot = kap_prev
+         call field_calc
+         seeds = seeds_sv
+         do 30 zone = 1, nz*nr
+            call vol_calc(zone)
+ 30      continue
+         kappa_tot = kap_cur
+         do 40 js = 1, nz
+            call z_surf_calc(js)
+ 40      continue
+         do 50 ks = 1, nr
+            call r_surf_calc(ks)
+ 50      continue
+         kap_prev = kap_cur
+c
+c        worker tallies of this step
+         write(fn, '(a,i3.3,a)') 'out_', n, '.bin'
+         open(unit=u, file=fn, access='stream',
+     1        form='unformatted', status='replace')
+         write(u) ((edep(js,ks), ks=1,nr), js=1,nz)
+         write(u) ((prdep(js,ks), ks=1,nr), js=1,nz)
+         write(u) ((ecens(js,ks), ks=1,nr), js=1,nz)
+         write(u) ((npcen(js,ks), ks=1,nr), js=1,nz)
+         write(u) (((n_field(j,js,ks), j=1,nphfield), ks=1,nr),
+     1             js=1,nz)
+         write(u) (E_IC(j), j=1,num_nt)
+         write(u) (nelectron(j), j=1,num_nt)
+         write(u) ((fout(js,ks), ks=1,nphomax), js=1,nmu)
+         write(u) ((edout(js,ks), ks=1,nphlcmax), js=1,nmu)
+         write(u) (erlki(j), j=1,nz), (erlko(j), j=1,nz)
+         write(u) (erlku(k), k=1,nr), (erlkl(k), k=1,nr)
+         write(u) (Ed_in(k), k=1,nr)
+         write(u) ndxout
+         write(u) (dbufout(j), j=1,6*ndxout)
+         write(u) (ibufout(j), j=1,6*ndxout)
+         write(u) nfile
+         write(u) (E_file(j), j=1,nfmax), (a1(j), j=1,nfmax)
+         write(u) (I_file(j), j=1,nfmax), (F_file(j), j=1,nfmax)
+         write(u) (P_file(j), j=1,nfmax)
+         close(u)
+         close(nunit_evt)
+c
+c        advance in time (src/xec2d.f:100-107)
+         dt(2) = dt(1)
+         if (ncycle.gt.0) then
+            time = time + dt(1)
+         endif
+         ncycle = ncycle + 1
+ 500  continue
+      close(4)
+      call MPI_FINALIZE(ierr)
+      end

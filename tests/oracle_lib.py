@@ -1,0 +1,140 @@
+"""ctypes front-end of the C oracle (oracle/c2d_oracle.c) — TEST INFRASTRUCTURE.
+
+Builds oracle/_build/liboracle_{ref,det}.so on demand (gcc is available here
+and on the GPU box) and wraps them.  Used only by tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+from compton2d_amd import abi
+
+ROOT = Path(__file__).resolve().parents[1]
+ORACLE_DIR = ROOT / "oracle"
+
+RNG_FIB, RNG_RAN1, RNG_LINEAGE = 1, 2, 3
+
+_libs = {}
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
+
+
+def load(flavor: str = "ref") -> C.CDLL:
+    """flavor 'ref' = glibc libm (reference parity); 'det' = c2d_math (GPU parity)."""
+    if flavor in _libs:
+        return _libs[flavor]
+    path = ORACLE_DIR / "_build" / ("liboracle_%s.so" % flavor)
+    src = ORACLE_DIR / "c2d_oracle.c"
+    if not path.exists() or path.stat().st_mtime < src.stat().st_mtime:
+        build()
+    lib = C.CDLL(str(path))
+    lib.c2o_create.restype = C.c_void_p
+    lib.c2o_create.argtypes = [C.POINTER(abi.Config), C.c_int, C.c_int, C.c_int32, C.c_int]
+    lib.c2o_destroy.argtypes = [C.c_void_p]
+    lib.c2o_step.restype = C.c_int
+    lib.c2o_step.argtypes = [C.c_void_p, C.POINTER(abi.StepIn)]
+    lib.c2o_tallies.restype = C.POINTER(C.c_double)
+    lib.c2o_tallies.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
+    lib.c2o_event_count.restype = C.c_int64
+    lib.c2o_event_count.argtypes = [C.c_void_p]
+    lib.c2o_events.restype = C.c_int64
+    lib.c2o_events.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int64]
+    lib.c2o_census_count.restype = C.c_int64
+    lib.c2o_census_count.argtypes = [C.c_void_p]
+    lib.c2o_census_export.restype = C.c_int64
+    lib.c2o_census_export.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32),
+                                      C.POINTER(C.c_uint64), C.c_int64]
+    lib.c2o_census_import.restype = C.c_int
+    lib.c2o_census_import.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32),
+                                      C.POINTER(C.c_uint64), C.c_int64]
+    lib.c2o_rseed.restype = C.c_int32
+    lib.c2o_rseed.argtypes = [C.c_void_p]
+    lib.c2o_unit_fib_init.argtypes = [C.c_int32]
+    lib.c2o_unit_fib_draw.argtypes = [C.c_int64, C.POINTER(C.c_double)]
+    lib.c2o_unit_seed_zone.argtypes = [C.POINTER(C.c_int32), C.c_int, C.c_int,
+                                       C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                       C.POINTER(C.c_int32)]
+    lib.c2o_unit_ran1.argtypes = [C.POINTER(C.c_int32), C.c_int64, C.POINTER(C.c_double)]
+    lib.c2o_unit_dilog.restype = C.c_double
+    lib.c2o_unit_dilog.argtypes = [C.c_double]
+    lib.c2o_unit_intg_v.restype = C.c_double
+    lib.c2o_unit_intg_v.argtypes = [C.c_double]
+    lib.c2o_unit_comtot.restype = C.c_double
+    lib.c2o_unit_comtot.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double]
+    lib.c2o_unit_set_tables.argtypes = [C.c_void_p, C.POINTER(abi.StepIn)]
+    lib.c2o_unit_compb2d.restype = C.c_int
+    lib.c2o_unit_compb2d.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32),
+                                     C.c_int, C.c_uint64, C.POINTER(C.c_uint32)]
+    lib.c2o_unit_planck.restype = C.c_double
+    lib.c2o_unit_planck.argtypes = [C.c_void_p, C.c_double, C.c_double, C.POINTER(C.c_int32)]
+    lib.c2o_unit_philox_draw.restype = C.c_double
+    lib.c2o_unit_philox_draw.argtypes = [C.c_uint64, C.c_uint32]
+    lib.c2o_unit_derive.restype = C.c_uint64
+    lib.c2o_unit_derive.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
+    lib.c2o_is_detmath.restype = C.c_int
+    _libs[flavor] = lib
+    return lib
+
+
+class Oracle:
+    """One oracle context = the reference's worker state for one run."""
+
+    def __init__(self, grid: abi.GridConfig, rng_mode: int = RNG_LINEAGE, flavor: str = "det",
+                 rand_switch: int = 1, rseed: int = 9857, h4_stale: int = 0):
+        self.lib = load(flavor)
+        self.grid = grid
+        self._cfg = grid.to_ctypes()
+        self.ctx = self.lib.c2o_create(C.byref(self._cfg), rng_mode, rand_switch, rseed, h4_stale)
+        if not self.ctx:
+            raise ValueError("c2o_create rejected the configuration")
+        self.nz, self.nr, self.nmu = grid.nz, grid.nr, grid.mu.size
+
+    def close(self):
+        if self.ctx:
+            self.lib.c2o_destroy(self.ctx)
+            self.ctx = None
+
+    __del__ = close
+
+    def step(self, si: abi.StepInputs) -> int:
+        self._si = si.to_ctypes()
+        return self.lib.c2o_step(self.ctx, C.byref(self._si))
+
+    def tallies(self) -> np.ndarray:
+        n = C.c_int64()
+        p = self.lib.c2o_tallies(self.ctx, C.byref(n))
+        return np.ctypeslib.as_array(p, shape=(n.value,)).copy()
+
+    def split(self) -> dict:
+        return abi.split_tallies(self.tallies(), self.nz, self.nr, self.nmu)
+
+    def events(self) -> np.ndarray:
+        n = self.lib.c2o_event_count(self.ctx)
+        out = np.zeros((max(n, 1), abi.EVENT_WORDS))
+        self.lib.c2o_events(self.ctx, out.ctypes.data_as(C.POINTER(C.c_double)), n)
+        return out[:n]
+
+    def census(self):
+        n = self.lib.c2o_census_count(self.ctx)
+        d6 = np.zeros((max(n, 1), 6))
+        i5 = np.zeros((max(n, 1), 5), np.int32)
+        keys = np.zeros(max(n, 1), np.uint64)
+        self.lib.c2o_census_export(self.ctx, d6.ctypes.data_as(C.POINTER(C.c_double)),
+                                   i5.ctypes.data_as(C.POINTER(C.c_int32)),
+                                   keys.ctypes.data_as(C.POINTER(C.c_uint64)), n)
+        return d6[:n], i5[:n], keys[:n]
+
+    def import_census(self, d6, i5, keys) -> int:
+        d6 = np.ascontiguousarray(d6, np.float64)
+        i5 = np.ascontiguousarray(i5, np.int32)
+        keys = np.ascontiguousarray(keys, np.uint64)
+        return self.lib.c2o_census_import(self.ctx, d6.ctypes.data_as(C.POINTER(C.c_double)),
+                                          i5.ctypes.data_as(C.POINTER(C.c_int32)),
+                                          keys.ctypes.data_as(C.POINTER(C.c_uint64)), len(keys))

@@ -1,0 +1,251 @@
+"""Reference-case helpers — TEST INFRASTRUCTURE.
+
+* write an input deck in the reference's fixed-column format
+  (label in columns 1-80, value from column 81; field order of
+  src/reader.f:157-657),
+* run the reference driver built by oracle/ref/build_ref.sh
+  (oracle/_ref/c2d_refdrv, this container only),
+* parse its full-precision dumps (config.bin, in_NNN.bin, out_NNN.bin,
+  ev_NNN.dat) into compton2d_amd.abi structures / numpy arrays.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+from compton2d_amd import abi
+
+ROOT = Path(__file__).resolve().parents[1]
+REFDRV = ROOT / "oracle" / "_ref" / "c2d_refdrv"
+REFERENCE = Path(os.environ.get("C2D_REFERENCE", "/root/reference"))
+
+BASE_CASE = dict(
+    nz=2, nr=2, zmax=1.0e16, rmin=0.0, rmax=7.5e15, tstop=1.0e7, mcdt=1.0,
+    t0=0.0, t1=1.0e30, tbbu=0.0, tbbl=0.0, spec_file="blackbody_20110929.in",
+    spec_switch=0,
+    regions=((1.0e-7, 1.0e-3, 10), (1.0e-3, 1.0e2, 49), (1.0e2, 1.0e11, 69)),
+    nmu=1, lc=((1e-7, 1e-3), (1e-3, 1e0), (1e0, 1e2), (1e2, 1e5), (1e5, 1e9)),
+    nst=2000, rseed=9857, rand_switch=1, cr_sent=0, pair_switch=0, T_const=1,
+    g_bulk=33.0, split1=10, split2=10, split3=3, spl3_trg=10,
+    # zone medium (src_20121026/inputm.dat:1-11)
+    tea=100.0, tna=100.0, n_e=80.0, B=0.13, amxwl=0.0, gmin=1.0e2, gmax=1.0e5, p_nth=2.3,
+)
+
+
+def _line(label: str, value) -> str:
+    if isinstance(value, float):
+        v = "%.7E" % value
+    else:
+        v = str(value)
+    return label[:80].ljust(80) + v + "\n"
+
+
+def write_input_deck(case_dir: Path, case: dict) -> None:
+    c = dict(BASE_CASE)
+    c.update(case)
+    d = Path(case_dir)
+    (d / "input").mkdir(parents=True, exist_ok=True)
+    for sub in ("output", "rates", "temp"):
+        (d / sub).mkdir(exist_ok=True)
+    L = []
+    L.append(_line("nz", c["nz"]))
+    L.append(_line("nr", c["nr"]))
+    L.append(_line("z(nz)", float(c["zmax"])))
+    L.append(_line("rmin", float(c["rmin"])))
+    L.append(_line("r(nr)", float(c["rmax"])))
+    L.append(_line("star_switch", 0))
+    L.append(_line("tstop", float(c["tstop"])))
+    L.append(_line("mcdt", float(c["mcdt"])))
+    L.append(_line("ntime", 1))
+    L.append(_line("t0(1)", float(c["t0"])))
+    L.append(_line("t1(1)", float(c["t1"])))
+    tbbu = c["tbbu"] if isinstance(c["tbbu"], (list, tuple)) else [c["tbbu"]] * c["nr"]
+    tbbl = c["tbbl"] if isinstance(c["tbbl"], (list, tuple)) else [c["tbbl"]] * c["nr"]
+    for k in range(c["nr"]):
+        L.append(_line("tbbu", float(tbbu[k])))
+        L.append(_line("u_fname", c["spec_file"]))
+        L.append(_line("tbbl", float(tbbl[k])))
+        L.append(_line("l_fname", c["spec_file"]))
+    L.append(_line("spec_switch", c["spec_switch"]))
+    L.append(_line("nphreg", len(c["regions"])))
+    for lo, hi, nb in c["regions"]:
+        L.append(_line("Ephmin", float(lo)))
+        L.append(_line("Ephmax", float(hi)))
+        L.append(_line("nphbins", nb))
+    L.append(_line("nmu", c["nmu"]))
+    L.append(_line("nph_lc", len(c["lc"])))
+    for lo, hi in c["lc"]:
+        L.append(_line("Elcmin", float(lo)))
+        L.append(_line("Elcmax", float(hi)))
+    for nm in ("output/spb.dat", "output/phb.dat", "output/lcb_01.dat", "evb.dat",
+               "output/temp_b.dat"):
+        L.append(_line("file", nm))
+    L.append(_line("nst", c["nst"]))
+    L.append(_line("rseed", c["rseed"]))
+    L.append(_line("rand_switch", c["rand_switch"]))
+    L.append(_line("cr_sent", c["cr_sent"]))
+    L.append(_line("upper_sent", 0))
+    L.append(_line("dh_sentinel", 0))
+    L.append(_line("pair_switch", c["pair_switch"]))
+    L.append(_line("T_const", c["T_const"]))
+    L.append(_line("cf_sentinel", 0))
+    for nm in ("r_flare", "z_flare", "t_flare", "sigma_r", "sigma_z", "sigma_t", "flare_amp"):
+        L.append(_line(nm, 0.0 if nm in ("r_flare", "z_flare", "flare_amp") else 1.0e6))
+    L.append(_line("r_esc", 0.3))
+    L.append(_line("r_acc", 1.0))
+    for nm, v in (("inj_switch", 0), ("inj_dis", 2), ("g2var_switch", 0), ("pick_sw", 0)):
+        L.append(_line(nm, v))
+    for nm, v in (("inj_g1", 1e2), ("inj_g2", 3e4), ("inj_p", 1.0), ("inj_t", 1.2e6),
+                  ("inj_L", 5e40), ("pick_rate", 0.8e-3), ("inj_gg", 1e2), ("inj_sigma", 1e1),
+                  ("g_bulk", float(c["g_bulk"]))):
+        L.append(_line(nm, float(v)))
+    for nm, v in (("R_blr", 2.18e38), ("fr_blr", 0.1), ("R_ir", 0.78e19), ("fr_ir", 0.5),
+                  ("R_disk", 1e17), ("d_jet", 0.5e17)):
+        L.append(_line(nm, float(v)))
+    for nm in ("split1", "split2", "split3", "spl3_trg"):
+        L.append(_line(nm, c[nm]))
+    (d / "input" / "input.dat").write_text("".join(L))
+    for j in range(1, c["nz"] + 1):
+        for k in range(1, c["nr"] + 1):
+            Z = []
+            for nm, v in (("tea", c["tea"]), ("tna", c["tna"]), ("n_e", c["n_e"])):
+                Z.append(_line(nm, float(v)))
+            Z.append(_line("ep_switch", 0))
+            for nm, v in (("B_field", c["B"]), ("amxwl", c["amxwl"]), ("gmin", c["gmin"]),
+                          ("gmax", c["gmax"]), ("p_nth", c["p_nth"]), ("q_turb", 1.666667),
+                          ("turb_lev", 1.0e-20)):
+                Z.append(_line(nm, float(v)))
+            (d / "input" / ("input_%02d_%02d.dat" % (j, k))).write_text("".join(Z))
+    src = REFERENCE / "disk" / c["spec_file"]
+    if src.exists():
+        shutil.copy(src, d / c["spec_file"])
+
+
+def run_reference(case_dir: Path, nsteps: int, klag: int = 1, timeout: int = 600) -> None:
+    if not REFDRV.exists():
+        raise FileNotFoundError("reference driver not built: run oracle/ref/build_ref.sh")
+    subprocess.run([str(REFDRV), str(nsteps), str(klag)], cwd=str(case_dir), check=True,
+                   timeout=timeout, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+
+
+class _Reader:
+    def __init__(self, path: Path):
+        self.b = Path(path).read_bytes()
+        self.o = 0
+
+    def i4(self, n=1):
+        a = np.frombuffer(self.b, dtype="<i4", count=n, offset=self.o)
+        self.o += 4 * n
+        return a.copy()
+
+    def f8(self, n=1):
+        a = np.frombuffer(self.b, dtype="<f8", count=n, offset=self.o)
+        self.o += 8 * n
+        return a.copy()
+
+
+def read_config(case_dir: Path) -> dict:
+    R = _Reader(Path(case_dir) / "config.bin")
+    nz, nr, nphtotal, nph_lc, nmu = R.i4(5)
+    split1, split2, split3, spl3_trg = R.i4(4)
+    spec_switch, cr_sent, pair_switch, rand_switch = R.i4(4)
+    rseed, T_const, ntime = R.i4(3)
+    rmin, zmin = R.f8(2)
+    cfg = dict(nz=int(nz), nr=int(nr), nphtotal=int(nphtotal), nph_lc=int(nph_lc), nmu=int(nmu),
+               split1=int(split1), split2=int(split2), split3=int(split3),
+               spl3_trg=int(spl3_trg), spec_switch=int(spec_switch), cr_sent=int(cr_sent),
+               pair_switch=int(pair_switch), rand_switch=int(rand_switch), rseed=int(rseed),
+               T_const=int(T_const), ntime=int(ntime), rmin=float(rmin), zmin=float(zmin))
+    cfg["z"] = R.f8(nz)
+    cfg["r"] = R.f8(nr)
+    cfg["E_field"] = R.f8(abi.NPHFIELD)
+    cfg["gnt"] = R.f8(abi.NUM_NT)
+    cfg["hu"] = R.f8(nphtotal + 1)
+    cfg["Elcmin"] = R.f8(nph_lc)
+    cfg["Elcmax"] = R.f8(nph_lc)
+    cfg["mu"] = R.f8(nmu)
+    return cfg
+
+
+def read_step_in(case_dir: Path, n: int, cfg: dict) -> dict:
+    nz, nr = cfg["nz"], cfg["nr"]
+    R = _Reader(Path(case_dir) / ("in_%03d.bin" % n))
+    d = {}
+    d["ncycle"], d["ti"] = (int(x) for x in R.i4(2))
+    d["time"], d["dt"] = (float(x) for x in R.f8(2))
+    d["E_ph"] = R.f8(abi.N_VOL)
+    for nm in ("kappa_tot", "eps_tot", "eps_th"):
+        d[nm] = R.f8(nz * nr * abi.N_VOL).reshape(nz, nr, abi.N_VOL)
+    for nm in ("f_nt", "Pnt"):
+        d[nm] = R.f8(nz * nr * abi.NUM_NT).reshape(nz, nr, abi.NUM_NT)
+    for nm in ("n_e", "Eloss_th", "Eloss_tot", "zsurf", "ewsv"):
+        d[nm] = R.f8(nz * nr).reshape(nz, nr)
+    d["nsv"] = R.i4(nz * nr).reshape(nz, nr)
+    d["nsurfi"], d["nsurfo"] = R.i4(nz), R.i4(nz)
+    d["ewsurfi"], d["ewsurfo"] = R.f8(nz), R.f8(nz)
+    d["nsurfu"], d["nsurfl"] = R.i4(nr), R.i4(nr)
+    d["ewsurfu"], d["ewsurfl"] = R.f8(nr), R.f8(nr)
+    d["tbbi"], d["tbbo"] = R.f8(nz), R.f8(nz)
+    d["tbbu"], d["tbbl"] = R.f8(nr), R.f8(nr)
+    d["rseed_after"] = int(R.i4(1)[0])
+    return d
+
+
+def read_step_out(case_dir: Path, n: int, cfg: dict) -> dict:
+    nz, nr, nmu = cfg["nz"], cfg["nr"], cfg["nmu"]
+    R = _Reader(Path(case_dir) / ("out_%03d.bin" % n))
+    o = {}
+    for nm in ("edep", "prdep", "ecens"):
+        o[nm] = R.f8(nz * nr).reshape(nz, nr)
+    o["npcen"] = R.i4(nz * nr).reshape(nz, nr)
+    o["n_field"] = R.f8(nz * nr * abi.NPHFIELD).reshape(nz, nr, abi.NPHFIELD)
+    o["E_IC"] = R.f8(abi.NUM_NT)
+    o["nelectron"] = R.i4(abi.NUM_NT)
+    o["fout"] = R.f8(nmu * abi.NPHOMAX).reshape(nmu, abi.NPHOMAX)
+    o["edout"] = R.f8(nmu * abi.NPHLCMAX).reshape(nmu, abi.NPHLCMAX)
+    o["erlki"], o["erlko"] = R.f8(nz), R.f8(nz)
+    o["erlku"], o["erlkl"] = R.f8(nr), R.f8(nr)
+    o["Ed_in"] = R.f8(nr)
+    nd = int(R.i4(1)[0])
+    o["census_d"] = R.f8(6 * nd).reshape(nd, 6)
+    o["census_i"] = R.i4(6 * nd).reshape(nd, 6)
+    o["nfile"] = int(R.i4(1)[0])
+    o["E_file"], o["a1"] = R.f8(abi.NFMAX), R.f8(abi.NFMAX)
+    o["I_file"], o["F_file"] = R.f8(abi.NFMAX), R.f8(abi.NFMAX)
+    o["P_file"] = R.f8(abi.NFMAX)
+    ev = Path(case_dir) / ("ev_%03d.dat" % n)
+    txt = ev.read_text().split() if ev.exists() else []
+    o["events"] = (np.array([float(x.replace("D", "E")) for x in txt]).reshape(-1, 7)
+                   if txt else np.zeros((0, 7)))
+    return o
+
+
+def grid_config(cfg: dict, E_ph: np.ndarray, **over) -> abi.GridConfig:
+    g = abi.GridConfig(
+        nz=cfg["nz"], nr=cfg["nr"], rmin=cfg["rmin"], zmin=cfg["zmin"], z=cfg["z"], r=cfg["r"],
+        E_ph=E_ph, E_field=cfg["E_field"], gnt=cfg["gnt"], hu=cfg["hu"], Elcmin=cfg["Elcmin"],
+        Elcmax=cfg["Elcmax"], mu=cfg["mu"], split1=cfg["split1"], split2=cfg["split2"],
+        split3=cfg["split3"], spl3_trg=cfg["spl3_trg"], spec_switch=cfg["spec_switch"],
+        cr_sent=cfg["cr_sent"], pair_switch=cfg["pair_switch"])
+    for k, v in over.items():
+        setattr(g, k, v)
+    return g
+
+
+def step_inputs(d: dict, spectrum: dict | None = None) -> abi.StepInputs:
+    spectra = []
+    if spectrum is not None and spectrum["nfile"] >= 2:
+        nf = spectrum["nfile"]
+        spectra.append(abi.SpectrumTable(
+            E_file=spectrum["E_file"][:nf].copy(), a1=spectrum["a1"][:nf].copy(),
+            I_file=spectrum["I_file"][:nf].copy(), F_file=spectrum["F_file"][:nf].copy(),
+            P_file=spectrum["P_file"][:nf].copy()))
+    keys = ("kappa_tot", "eps_tot", "eps_th", "f_nt", "Pnt", "n_e", "Eloss_th", "Eloss_tot",
+            "zsurf", "ewsv", "nsv", "nsurfi", "nsurfo", "ewsurfi", "ewsurfo", "nsurfu", "nsurfl",
+            "ewsurfu", "ewsurfl", "tbbi", "tbbo", "tbbu", "tbbl")
+    return abi.StepInputs(ncycle=d["ncycle"], time=d["time"], dt=d["dt"],
+                          spectra=spectra, **{k: d[k] for k in keys})
