@@ -28,7 +28,7 @@ COMTOT_EXACT = 0
 COMTOT_TABLE = 1
 
 CNT_STEPS, CNT_ESCAPES, CNT_CENSUS, CNT_COLLIDE, CNT_KILLED, CNT_SOURCES, \
-    CNT_COMPB, CNT_EVENTS, CNT_GENS = range(9)
+    CNT_COMPB, CNT_EVENTS, CNT_GENS, CNT_ABORTED = range(10)
 
 ERRORS = {
     0: "C2D_OK", -1: "C2D_E_ARG", -2: "C2D_E_HIP", -3: "C2D_E_CENSUS_OVERFLOW",

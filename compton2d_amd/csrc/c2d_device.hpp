@@ -1,0 +1,124 @@
+/*
+ * c2d_device.hpp — data layout shared by the host C-ABI (capi.cpp) and the
+ * transport kernels (transport.hip).
+ */
+#ifndef C2D_DEVICE_HPP
+#define C2D_DEVICE_HPP
+
+#include <stdint.h>
+#include "../../include/compton2d.h"
+
+namespace c2d {
+
+/* Run-constant grids, 1-based like the reference COMMON arrays. */
+struct Geo {
+  double z[C2D_MAXZONE + 1];          /* z[0] = zmin, z[1..nz]           */
+  double r[C2D_MAXZONE + 1];          /* r[0] = rmin, r[1..nr]           */
+  double E_ph[C2D_N_VOL + 1];         /* E_ph[1..400]                    */
+  double E_field[C2D_NPHFIELD + 1];   /* E_field[1..400]                 */
+  double hu[C2D_NPHOMAX + 2];         /* hu[1..nphtotal+1]               */
+  double Elcmin[C2D_NPHLCMAX + 1];
+  double Elcmax[C2D_NPHLCMAX + 1];
+  double mu[C2D_NMUMAX + 1];
+};
+/* LDS image of Geo (everything but nothing else). */
+constexpr int GEO_DOUBLES = (int)(sizeof(Geo) / sizeof(double));
+
+struct SpecDev {             /* file_sp table (imcsurf2d_para.f:544-685) */
+  int32_t nfile;
+  const double* E_file;
+  const double* a1;
+  const double* I_file;
+  const double* F_file;
+  const double* P_file;
+};
+
+/* Census packet store, SoA (record of imctrk2d.f:558-572 + lineage key). */
+struct CensusSoA {
+  double* rpre; double* zpre; double* wmu; double* phi; double* ew; double* xnu;
+  uint32_t* jk;      /* jph << 16 | kph (1-based)                  */
+  uint32_t* bins;    /* jgpsp | jgplc << 8 | jgpmu << 16            */
+  uint64_t* key;
+};
+
+/* Collision record: packet state after the move to the collision point
+ * (imctrk2d.f:593-604 "csv" copy) plus the RNG point of the split. */
+struct ScatRec {
+  double rpre, zpre, wmu, phi, ew, xnu, dcen;
+  uint32_t jk;
+  uint32_t ctr;      /* RNG counter of the parent (SCAT2) / child (SCAT3) */
+  uint64_t key;      /* parent key (SCAT2) / child key (SCAT3)            */
+  uint32_t kap;      /* 0: census/volume phase kappa (H3), 1: surface phase */
+  uint32_t pad;
+};
+
+struct TallyOff {
+  int64_t edep, prdep, ecens, npcen, n_field, E_IC, nelectron, fout, edout;
+  int64_t erlki, erlko, erlku, erlkl, Ed_in, counters;
+};
+
+#define C2D_COMTAB_N 2048
+/* comtot table: x grid in u = ln(xnu/keV) */
+#define C2D_COMTAB_U0 (-27.631021115928547)   /* ln(1e-12) */
+#define C2D_COMTAB_U1 (29.933606208922594)    /* ln(1e13)  */
+
+enum : int32_t {
+  ERR_CENSUS = 1, ERR_EVENT = 2, ERR_QUEUE = 4, ERR_SPEC = 8
+};
+
+struct KParams {
+  int32_t nz, nr, ncell, nphtotal, nph_lc, nmu;
+  int32_t split1, split2, split3, spl3_trg, spec_switch;
+  int32_t rank, world, ncycle, gen, eps_linear;
+  double time, dt, rmin, zmin, cdt;
+  uint64_t step_key;
+  const Geo* geo;
+  const double* gnt;        /* [200] */
+  const double* kappa_cv;   /* [ncell][400] census + volume phase (H3) */
+  const double* kappa_s;    /* [ncell][400] surface phase               */
+  const double* eps_tot;    /* [ncell][400] */
+  const double* eps_th;
+  const double* f_nt;       /* [ncell][200] */
+  const double* Pnt;
+  const double* n_e;        /* [ncell] */
+  const double* vfrac;      /* [ncell][4] f_thermal, f_inn, f_outer, f_upper */
+  const double* ewsv;       /* [ncell] */
+  const int64_t* vol_prefix;    /* [ncell+1] global volume-source prefix */
+  const int64_t* surf_prefix;   /* [nslot+1] global surface-source prefix */
+  const double* surf_ew;        /* [nslot] */
+  const double* surf_tbb;       /* [nslot] */
+  const int32_t* surf_spec;     /* [nslot] */
+  const double* tbbl;           /* [nr]  lower-surface temperature (imcleak) */
+  const SpecDev* spectra;
+  int32_t n_spectra, nslot;
+  const double* comtab;         /* [ncell][C2D_COMTAB_N] cosig on the u grid */
+  double comtab_du_inv;
+  /* census */
+  CensusSoA cin, cout;
+  int64_t n_cin, cap_cout;
+  unsigned long long* n_cout;
+  /* events */
+  double* ev;
+  int64_t cap_ev;
+  unsigned long long* n_ev;
+  /* scatter queues: in (this generation) / out (next) */
+  const ScatRec* q2_in; const ScatRec* q3_in;
+  int64_t n2_in, n3_in;
+  ScatRec* q2_out; ScatRec* q3_out;
+  unsigned long long* n2_out; unsigned long long* n3_out;
+  int64_t cap_q;
+  /* work items of this launch */
+  int64_t n_items, n_cens_items, n_vol_items, n_surf_items;
+  int64_t n_vol_global, n_surf_global;
+  unsigned long long* work_counter;
+  /* tallies */
+  double* T;
+  TallyOff off;
+  unsigned long long* cnt;  /* [C2D_NCOUNTERS] */
+  int32_t* err;
+  int32_t lds_cells;        /* 1: cell tallies privatised in LDS */
+};
+
+}  // namespace c2d
+
+#endif

@@ -1,0 +1,700 @@
+/*
+ * capi.cpp — C-ABI implementation (include/compton2d.h) over the gfx950
+ * transport kernels.  Host-side work is limited to gathering the
+ * [1:nz,1:nr] sub-blocks of the caller's (strided, COMMON-layout) tables,
+ * tiny per-step prefix sums, and the generation loop.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/compton2d.h"
+#include "c2d_device.hpp"
+#include "c2d_rng.h"
+
+using namespace c2d;
+
+extern "C" int c2d_launch_transport_exact(const KParams* P, int grid, size_t lds, hipStream_t s);
+extern "C" int c2d_launch_transport_fast(const KParams* P, int grid, size_t lds, hipStream_t s);
+extern "C" int c2d_transport_attrs_exact(int* block, int* max_lds);
+extern "C" int c2d_transport_attrs_fast(int* block, int* max_lds);
+extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t s);
+extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
+                                      double* tab, int ncell, hipStream_t s);
+extern "C" int c2d_launch_tridag(const double* a, const double* b, const double* c,
+                                 const double* r, double* x, int ncell, int nt, hipStream_t s);
+
+namespace {
+
+enum { CTL_WORK = 0, CTL_NCOUT = 1, CTL_NEV = 2, CTL_N2 = 3, CTL_N3 = 4, CTL_CNT = 8,
+       CTL_WORDS = 8 + C2D_NCOUNTERS };
+
+struct DevCensus {
+  double* d[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint32_t* jk = nullptr;
+  uint32_t* bins = nullptr;
+  uint64_t* key = nullptr;
+  CensusSoA soa() const {
+    CensusSoA s;
+    s.rpre = d[0]; s.zpre = d[1]; s.wmu = d[2]; s.phi = d[3]; s.ew = d[4]; s.xnu = d[5];
+    s.jk = jk; s.bins = bins; s.key = key;
+    return s;
+  }
+};
+
+}  // namespace
+
+struct c2d_ctx {
+  c2d_config cfg;
+  int nz = 0, nr = 0, ncell = 0, nmu = 0, nslot = 0;
+  std::string err;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_g0a = nullptr, ev_g0b = nullptr, ev_end = nullptr;
+  int n_cu = 0, max_grid = 0, lds_cells = 0;
+  size_t lds_bytes = 0;
+  c2d_tally_layout L;
+  /* device buffers */
+  Geo* geo = nullptr;
+  double *gnt = nullptr, *kappa_cur = nullptr, *kappa_prev = nullptr, *eps_tot = nullptr,
+         *eps_th = nullptr, *f_nt = nullptr, *Pnt = nullptr, *n_e = nullptr, *vfrac = nullptr,
+         *ewsv = nullptr, *surf_ew = nullptr, *surf_tbb = nullptr, *tbbl = nullptr;
+  int64_t *vol_prefix = nullptr, *surf_prefix = nullptr;
+  int32_t* surf_spec = nullptr;
+  SpecDev* spectra = nullptr;
+  std::vector<double*> spec_bufs;
+  int n_spectra = 0;
+  double *comtab = nullptr, *comS = nullptr;
+  DevCensus cens[2];
+  int cur_out = 0;           /* census buffer written by the last step */
+  int64_t n_census = 0;      /* packets in cens[cur_out] */
+  double* ev = nullptr;
+  int64_t n_ev = 0;
+  ScatRec *q2[2] = {nullptr, nullptr}, *q3[2] = {nullptr, nullptr};
+  double* T = nullptr;
+  double* T_own = nullptr;
+  unsigned long long* ctl = nullptr;
+  int32_t* derr = nullptr;
+  KParams* dP = nullptr;
+  /* host state of the current step */
+  KParams P;
+  bool have_step = false;
+  int64_t n_vol_global = 0, n_surf_global = 0;
+  int eps_linear = 0;
+  std::vector<double> h_stage;
+  double last_g0_ms = 0.0, last_all_ms = 0.0;
+  int last_launches = 0;
+};
+
+static int fail(c2d_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(c, x)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess)                                                              \
+      return fail((c), C2D_E_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #x,              \
+                  hipGetErrorString(e_));                                              \
+  } while (0)
+
+template <class T>
+static hipError_t dalloc(T** p, size_t n) {
+  if (n == 0) n = 1;
+  return hipMalloc((void**)p, n * sizeof(T));
+}
+
+extern "C" const char* c2d_version(void) { return "compton2d_amd 0.1.0 (gfx950)"; }
+
+extern "C" const char* c2d_last_error(c2d_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
+  if (!cfg || !out) return C2D_E_ARG;
+  *out = nullptr;
+  if (cfg->nz < 1 || cfg->nr < 1 || cfg->nz > C2D_MAXZONE || cfg->nr > C2D_MAXZONE)
+    return C2D_E_ARG;
+  if (cfg->nphtotal < 1 || cfg->nphtotal > C2D_NPHOMAX || cfg->nph_lc < 0 ||
+      cfg->nph_lc > C2D_NPHLCMAX || cfg->nmu < 1 || cfg->nmu > C2D_NMUMAX)
+    return C2D_E_ARG;
+  if (cfg->cr_sent != 0) return C2D_E_ARG;   /* Compton reflection not supported */
+  if (cfg->split1 < 1 || cfg->split2 < 1 || cfg->split3 < 1 || cfg->world < 1 ||
+      cfg->rank < 0 || cfg->rank >= cfg->world)
+    return C2D_E_ARG;
+  c2d_ctx* c = new c2d_ctx();
+  c->cfg = *cfg;
+  c->nz = cfg->nz;
+  c->nr = cfg->nr;
+  c->ncell = cfg->nz * cfg->nr;
+  c->nmu = cfg->nmu;
+  c->nslot = 2 * cfg->nz + 2 * cfg->nr;
+  c2d_tally_layout_for(c->nz, c->nr, c->nmu, &c->L);
+  *out = c;
+
+  HIPCHK(c, hipSetDevice(cfg->device));
+  HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(c, hipEventCreate(&c->ev_g0a));
+  HIPCHK(c, hipEventCreate(&c->ev_g0b));
+  HIPCHK(c, hipEventCreate(&c->ev_end));
+  hipDeviceProp_t prop;
+  HIPCHK(c, hipGetDeviceProperties(&prop, cfg->device));
+  c->n_cu = prop.multiProcessorCount;
+
+  /* grids (1-based like the reference COMMON) */
+  Geo g;
+  memset(&g, 0, sizeof g);
+  g.z[0] = cfg->zmin;
+  g.r[0] = cfg->rmin;
+  for (int j = 0; j < c->nz; j++) g.z[j + 1] = cfg->z[j];
+  for (int k = 0; k < c->nr; k++) g.r[k + 1] = cfg->r[k];
+  for (int i = 0; i < C2D_N_VOL; i++) g.E_ph[i + 1] = cfg->E_ph[i];
+  for (int i = 0; i < C2D_NPHFIELD; i++) g.E_field[i + 1] = cfg->E_field[i];
+  for (int i = 0; i <= cfg->nphtotal; i++) g.hu[i + 1] = cfg->hu[i];
+  for (int m = 0; m < cfg->nph_lc; m++) {
+    g.Elcmin[m + 1] = cfg->Elcmin[m];
+    g.Elcmax[m + 1] = cfg->Elcmax[m];
+  }
+  for (int n = 0; n < cfg->nmu; n++) g.mu[n + 1] = cfg->mu[n];
+  HIPCHK(c, dalloc(&c->geo, 1));
+  HIPCHK(c, hipMemcpy(c->geo, &g, sizeof g, hipMemcpyHostToDevice));
+  HIPCHK(c, dalloc(&c->gnt, C2D_NUM_NT));
+  HIPCHK(c, hipMemcpy(c->gnt, cfg->gnt, sizeof(double) * C2D_NUM_NT, hipMemcpyHostToDevice));
+
+  const size_t nc = (size_t)c->ncell;
+  HIPCHK(c, dalloc(&c->kappa_cur, nc * C2D_N_VOL));
+  HIPCHK(c, dalloc(&c->kappa_prev, nc * C2D_N_VOL));
+  HIPCHK(c, hipMemset(c->kappa_prev, 0, nc * C2D_N_VOL * sizeof(double)));
+  HIPCHK(c, dalloc(&c->eps_tot, nc * C2D_N_VOL));
+  HIPCHK(c, dalloc(&c->eps_th, nc * C2D_N_VOL));
+  HIPCHK(c, dalloc(&c->f_nt, nc * C2D_NUM_NT));
+  HIPCHK(c, dalloc(&c->Pnt, nc * C2D_NUM_NT));
+  HIPCHK(c, dalloc(&c->n_e, nc));
+  HIPCHK(c, dalloc(&c->ewsv, nc));
+  HIPCHK(c, dalloc(&c->vfrac, nc * 4));
+  HIPCHK(c, dalloc(&c->vol_prefix, nc + 1));
+  HIPCHK(c, dalloc(&c->surf_prefix, (size_t)c->nslot + 1));
+  HIPCHK(c, dalloc(&c->surf_ew, (size_t)c->nslot));
+  HIPCHK(c, dalloc(&c->surf_tbb, (size_t)c->nslot));
+  HIPCHK(c, dalloc(&c->surf_spec, (size_t)c->nslot));
+  HIPCHK(c, dalloc(&c->tbbl, (size_t)c->nr));
+  if (cfg->comtot_mode == C2D_COMTOT_TABLE) {
+    HIPCHK(c, dalloc(&c->comtab, nc * C2D_COMTAB_N));
+    HIPCHK(c, dalloc(&c->comS, (size_t)C2D_COMTAB_N * C2D_NUM_NT));
+    int rc = c2d_launch_comtab_sigma(c->gnt, c->comS, c->stream);
+    if (rc) return fail(c, C2D_E_HIP, "comtab_sigma launch: %d", rc);
+  }
+  const int64_t ccap = std::max<int64_t>(cfg->census_capacity, 1);
+  for (int b = 0; b < 2; b++) {
+    for (int f = 0; f < 6; f++) HIPCHK(c, dalloc(&c->cens[b].d[f], ccap));
+    HIPCHK(c, dalloc(&c->cens[b].jk, ccap));
+    HIPCHK(c, dalloc(&c->cens[b].bins, ccap));
+    HIPCHK(c, dalloc(&c->cens[b].key, ccap));
+  }
+  HIPCHK(c, dalloc(&c->ev, (size_t)std::max<int64_t>(cfg->event_capacity, 1) * C2D_EVENT_WORDS));
+  const int64_t qcap = std::max<int64_t>(cfg->queue_capacity, 1);
+  for (int b = 0; b < 2; b++) {
+    HIPCHK(c, dalloc(&c->q2[b], qcap));
+    HIPCHK(c, dalloc(&c->q3[b], qcap));
+  }
+  HIPCHK(c, dalloc(&c->T_own, (size_t)c->L.total));
+  HIPCHK(c, hipMemset(c->T_own, 0, sizeof(double) * c->L.total));
+  c->T = c->T_own;
+  HIPCHK(c, dalloc(&c->ctl, CTL_WORDS));
+  HIPCHK(c, dalloc(&c->derr, 1));
+  HIPCHK(c, dalloc(&c->dP, 1));
+
+  /* LDS plan: Geo image + (cell tallies if they fit) + escape tallies */
+  const size_t esc = (size_t)c->nmu * (C2D_NPHOMAX + C2D_NPHLCMAX) + 2 * c->nz + 2 * c->nr;
+  c->lds_cells = (4 * nc * sizeof(double) <= 48 * 1024) ? 1 : 0;
+  c->lds_bytes = sizeof(double) * (GEO_DOUBLES + (c->lds_cells ? 4 * nc : 0) + esc);
+  int blocks_per_cu = 0;
+  const void* kfn = nullptr;
+  (void)kfn;
+  int block = 512, max_lds = 0;
+  if (cfg->comtot_mode == C2D_COMTOT_TABLE)
+    c2d_transport_attrs_fast(&block, &max_lds);
+  else
+    c2d_transport_attrs_exact(&block, &max_lds);
+  /* occupancy: VGPR-limited to 2 waves/SIMD today (8 waves = 1 block/CU); LDS
+   * allows 160 KiB / lds_bytes blocks.  Persistent grid = CUs x blocks. */
+  blocks_per_cu = std::max(1, std::min<int>(2, (int)((160 * 1024) / c->lds_bytes)));
+  c->max_grid = c->n_cu * blocks_per_cu;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return C2D_OK;
+}
+
+extern "C" void c2d_finalize(c2d_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->cfg.device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* ptrs[] = {c->geo, c->gnt, c->kappa_cur, c->kappa_prev, c->eps_tot, c->eps_th, c->f_nt,
+                  c->Pnt, c->n_e, c->vfrac, c->ewsv, c->surf_ew, c->surf_tbb, c->tbbl,
+                  c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comS,
+                  c->ev, c->q2[0], c->q2[1], c->q3[0], c->q3[1], c->T_own, c->ctl, c->derr, c->dP};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  for (int b = 0; b < 2; b++) {
+    for (int f = 0; f < 6; f++)
+      if (c->cens[b].d[f]) (void)hipFree(c->cens[b].d[f]);
+    if (c->cens[b].jk) (void)hipFree(c->cens[b].jk);
+    if (c->cens[b].bins) (void)hipFree(c->cens[b].bins);
+    if (c->cens[b].key) (void)hipFree(c->cens[b].key);
+  }
+  for (double* p : c->spec_bufs) (void)hipFree(p);
+  if (c->ev_g0a) (void)hipEventDestroy(c->ev_g0a);
+  if (c->ev_g0b) (void)hipEventDestroy(c->ev_g0b);
+  if (c->ev_end) (void)hipEventDestroy(c->ev_end);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+/* gather (i, j, k) of a strided table into dense [cell][n] */
+static void gather3(const c2d_ctx* c, const c2d_array3& a, int n, double* out) {
+  for (int j = 0; j < c->nz; j++)
+    for (int k = 0; k < c->nr; k++) {
+      double* o = out + (size_t)(j * c->nr + k) * n;
+      if (!a.data) {
+        std::fill(o, o + n, 0.0);
+        continue;
+      }
+      const double* base = a.data + j * a.s_j + k * a.s_k;
+      if (a.s_i == 1)
+        memcpy(o, base, sizeof(double) * n);
+      else
+        for (int i = 0; i < n; i++) o[i] = base[i * a.s_i];
+    }
+}
+static double at2(const c2d_array2& a, int j, int k) {
+  return a.data ? a.data[j * a.s_j + k * a.s_k] : 0.0;
+}
+
+extern "C" int c2d_set_clock(c2d_ctx* c, int32_t ncycle, double time, double dt) {
+  if (!c) return C2D_E_ARG;
+  c->P.ncycle = ncycle;
+  c->P.time = time;
+  c->P.dt = dt;
+  c->P.cdt = 2.9979245620e10 * dt;                 /* dcen = c_light*dt(1), imcfield2d.f:117 */
+  c->P.step_key = c2d_step_key(c->cfg.seed, ncycle);
+  return C2D_OK;
+}
+
+extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
+  if (!c || !in) return C2D_E_ARG;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const int nz = c->nz, nr = c->nr, nc = c->ncell;
+  const size_t nvol = (size_t)nc * C2D_N_VOL, nnt = (size_t)nc * C2D_NUM_NT;
+  std::vector<double>& h = c->h_stage;
+  h.resize(nvol);
+  gather3(c, in->kappa_tot, C2D_N_VOL, h.data());
+  HIPCHK(c, hipMemcpy(c->kappa_cur, h.data(), nvol * sizeof(double), hipMemcpyHostToDevice));
+  gather3(c, in->eps_tot, C2D_N_VOL, h.data());
+  int nonmono = 0;
+  for (int cc = 0; cc < nc && !nonmono; cc++)
+    for (int i = 1; i < C2D_N_VOL; i++)
+      if (!(h[(size_t)cc * C2D_N_VOL + i] >= h[(size_t)cc * C2D_N_VOL + i - 1])) { nonmono = 1; break; }
+  HIPCHK(c, hipMemcpy(c->eps_tot, h.data(), nvol * sizeof(double), hipMemcpyHostToDevice));
+  gather3(c, in->eps_th, C2D_N_VOL, h.data());
+  for (int cc = 0; cc < nc && !nonmono; cc++)
+    for (int i = 1; i < C2D_N_VOL; i++)
+      if (!(h[(size_t)cc * C2D_N_VOL + i] >= h[(size_t)cc * C2D_N_VOL + i - 1])) { nonmono = 1; break; }
+  HIPCHK(c, hipMemcpy(c->eps_th, h.data(), nvol * sizeof(double), hipMemcpyHostToDevice));
+  c->eps_linear = nonmono;
+  std::vector<double> hn(nnt);
+  gather3(c, in->f_nt, C2D_NUM_NT, hn.data());
+  HIPCHK(c, hipMemcpy(c->f_nt, hn.data(), nnt * sizeof(double), hipMemcpyHostToDevice));
+  gather3(c, in->Pnt, C2D_NUM_NT, hn.data());
+  HIPCHK(c, hipMemcpy(c->Pnt, hn.data(), nnt * sizeof(double), hipMemcpyHostToDevice));
+
+  /* zone scalars, volume fractions (imcvol2d_para.f:119-149), volume prefix */
+  std::vector<double> ne(nc), ew(nc), vf(4 * (size_t)nc);
+  std::vector<int64_t> vp(nc + 1);
+  vp[0] = 0;
+  for (int j = 0; j < nz; j++)
+    for (int k = 0; k < nr; k++) {
+      const int cell = j * nr + k;
+      ne[cell] = at2(in->n_e, j, k);
+      ew[cell] = at2(in->ewsv, j, k);
+      const int jv = j + 1, kv = k + 1;
+      const double zj = c->cfg.z[j], zjm = (jv == 1) ? 0.0 : c->cfg.z[j - 1];
+      const double delz = (jv == 1) ? c->cfg.z[0] : zj - zjm;
+      const double zs = at2(in->zsurf, j, k);
+      const double rlow = (kv == 1) ? c->cfg.rmin : c->cfg.r[k - 1];
+      const double rk = c->cfg.r[k];
+      const double fi = (4.4e1 / 7.0 * rlow * delz) / zs;
+      const double fo = (4.4e1 / 7.0 * rk * delz) / zs;
+      const double fu = (2.2e1 / 7.0 * (rk * rk - rlow * rlow)) / zs;
+      vf[4 * cell + 0] = at2(in->Eloss_th, j, k) / at2(in->Eloss_tot, j, k);
+      vf[4 * cell + 1] = fi;
+      vf[4 * cell + 2] = fi + fo;
+      vf[4 * cell + 3] = (fi + fo) + fu;
+      const int32_t nsv = in->nsv.data ? in->nsv.data[j * in->nsv.s_j + k * in->nsv.s_k] : 0;
+      vp[cell + 1] = vp[cell] + (nsv > 0 ? nsv : 0);
+    }
+  c->n_vol_global = vp[nc];
+  HIPCHK(c, hipMemcpy(c->n_e, ne.data(), nc * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->ewsv, ew.data(), nc * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->vfrac, vf.data(), vf.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->vol_prefix, vp.data(), vp.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+
+  /* surface slots: (inner js, outer js) for js=1..nz, then (upper ks, lower ks) */
+  const int ns = c->nslot;
+  std::vector<int64_t> sp(ns + 1);
+  std::vector<double> sew(ns), stb(ns);
+  std::vector<int32_t> ssp(ns);
+  sp[0] = 0;
+  for (int s = 0; s < ns; s++) {
+    int32_t cnt = 0, spec = -1;
+    double w = 0.0, tb = 0.0;
+    if (s < 2 * nz) {
+      const int j = s / 2, side = s & 1;
+      const int32_t* n = side ? in->nsurfo : in->nsurfi;
+      const double* e = side ? in->ewsurfo : in->ewsurfi;
+      const double* t = side ? in->tbbo : in->tbbi;
+      const int32_t* sx = side ? in->spec_o : in->spec_i;
+      cnt = n ? n[j] : 0;
+      w = e ? e[j] : 0.0;
+      tb = t ? t[j] : 0.0;
+      spec = sx ? sx[j] : -1;
+    } else {
+      const int k = (s - 2 * nz) / 2, side = (s - 2 * nz) & 1;
+      const int32_t* n = side ? in->nsurfl : in->nsurfu;
+      const double* e = side ? in->ewsurfl : in->ewsurfu;
+      const double* t = side ? in->tbbl : in->tbbu;
+      const int32_t* sx = side ? in->spec_l : in->spec_u;
+      cnt = n ? n[k] : 0;
+      w = e ? e[k] : 0.0;
+      tb = t ? t[k] : 0.0;
+      spec = sx ? sx[k] : -1;
+    }
+    if (cnt > 0 && !(tb > 0.0) && (spec < 0 || spec >= in->n_spectra))
+      return fail(c, C2D_E_ARG, "surface slot %d emits %d packets but has no spectrum", s, cnt);
+    sp[s + 1] = sp[s] + (cnt > 0 ? cnt : 0);
+    sew[s] = w;
+    stb[s] = tb;
+    ssp[s] = spec;
+  }
+  c->n_surf_global = sp[ns];
+  HIPCHK(c, hipMemcpy(c->surf_prefix, sp.data(), sp.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->surf_ew, sew.data(), ns * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->surf_tbb, stb.data(), ns * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->surf_spec, ssp.data(), ns * sizeof(int32_t), hipMemcpyHostToDevice));
+  std::vector<double> tl(nr, 0.0);
+  for (int k = 0; k < nr; k++) tl[k] = in->tbbl ? in->tbbl[k] : 0.0;
+  HIPCHK(c, hipMemcpy(c->tbbl, tl.data(), nr * sizeof(double), hipMemcpyHostToDevice));
+
+  /* seed spectra (file_sp output) */
+  for (double* p : c->spec_bufs) (void)hipFree(p);
+  c->spec_bufs.clear();
+  if (c->spectra) (void)hipFree(c->spectra);
+  c->spectra = nullptr;
+  c->n_spectra = in->n_spectra;
+  if (in->n_spectra > 0) {
+    std::vector<SpecDev> hs(in->n_spectra);
+    for (int m = 0; m < in->n_spectra; m++) {
+      const c2d_spectrum& s = in->spectra[m];
+      if (s.nfile < 2 || s.nfile > C2D_NFMAX) return fail(c, C2D_E_ARG, "spectrum %d: nfile %d", m, s.nfile);
+      const double* src[5] = {s.E_file, s.a1, s.I_file, s.F_file, s.P_file};
+      const int len[5] = {s.nfile, s.nfile - 1, s.nfile - 1, s.nfile, s.nfile - 1};
+      double* dst[5];
+      for (int f = 0; f < 5; f++) {
+        HIPCHK(c, dalloc(&dst[f], (size_t)len[f]));
+        HIPCHK(c, hipMemcpy(dst[f], src[f], len[f] * sizeof(double), hipMemcpyHostToDevice));
+        c->spec_bufs.push_back(dst[f]);
+      }
+      hs[m].nfile = s.nfile;
+      hs[m].E_file = dst[0]; hs[m].a1 = dst[1]; hs[m].I_file = dst[2]; hs[m].F_file = dst[3];
+      hs[m].P_file = dst[4];
+    }
+    HIPCHK(c, dalloc(&c->spectra, (size_t)in->n_spectra));
+    HIPCHK(c, hipMemcpy(c->spectra, hs.data(), hs.size() * sizeof(SpecDev), hipMemcpyHostToDevice));
+  }
+
+  if (c->cfg.comtot_mode == C2D_COMTOT_TABLE) {
+    int rc = c2d_launch_comtab_gemm(c->f_nt, c->gnt, c->comS, c->comtab, nc, c->stream);
+    if (rc) return fail(c, C2D_E_HIP, "comtab_gemm launch: %d", rc);
+  }
+  c2d_set_clock(c, in->ncycle, in->time, in->dt);
+  c->have_step = true;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return C2D_OK;
+}
+
+extern "C" int c2d_run_step(c2d_ctx* c) {
+  if (!c) return C2D_E_ARG;
+  if (!c->have_step) return fail(c, C2D_E_STATE, "c2d_set_step must precede c2d_run_step");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const c2d_config& cfg = c->cfg;
+  KParams& P = c->P;
+  P.nz = c->nz; P.nr = c->nr; P.ncell = c->ncell; P.nphtotal = cfg.nphtotal;
+  P.nph_lc = cfg.nph_lc; P.nmu = cfg.nmu;
+  P.split1 = cfg.split1; P.split2 = cfg.split2; P.split3 = cfg.split3; P.spl3_trg = cfg.spl3_trg;
+  P.spec_switch = cfg.spec_switch; P.rank = cfg.rank; P.world = cfg.world;
+  P.eps_linear = c->eps_linear;
+  P.rmin = cfg.rmin; P.zmin = cfg.zmin;
+  P.geo = c->geo; P.gnt = c->gnt;
+  P.kappa_cv = cfg.kappa_lag ? c->kappa_prev : c->kappa_cur;
+  P.kappa_s = c->kappa_cur;
+  P.eps_tot = c->eps_tot; P.eps_th = c->eps_th; P.f_nt = c->f_nt; P.Pnt = c->Pnt;
+  P.n_e = c->n_e; P.vfrac = c->vfrac; P.ewsv = c->ewsv;
+  P.vol_prefix = c->vol_prefix; P.surf_prefix = c->surf_prefix; P.surf_ew = c->surf_ew;
+  P.surf_tbb = c->surf_tbb; P.surf_spec = c->surf_spec; P.tbbl = c->tbbl;
+  P.spectra = c->spectra; P.n_spectra = c->n_spectra; P.nslot = c->nslot;
+  P.comtab = c->comtab;
+  P.comtab_du_inv = (double)(C2D_COMTAB_N - 1) / (C2D_COMTAB_U1 - C2D_COMTAB_U0);
+  const int in_buf = c->cur_out, out_buf = 1 - c->cur_out;
+  P.cin = c->cens[in_buf].soa();
+  P.cout = c->cens[out_buf].soa();
+  P.n_cin = c->n_census;
+  P.cap_cout = cfg.census_capacity;
+  P.n_cout = c->ctl + CTL_NCOUT;
+  P.ev = c->ev; P.cap_ev = cfg.event_capacity; P.n_ev = c->ctl + CTL_NEV;
+  P.cap_q = cfg.queue_capacity;
+  P.work_counter = c->ctl + CTL_WORK;
+  P.n2_out = c->ctl + CTL_N2; P.n3_out = c->ctl + CTL_N3;
+  P.T = c->T;
+  P.off.edep = c->L.edep; P.off.prdep = c->L.prdep; P.off.ecens = c->L.ecens;
+  P.off.npcen = c->L.npcen; P.off.n_field = c->L.n_field; P.off.E_IC = c->L.E_IC;
+  P.off.nelectron = c->L.nelectron; P.off.fout = c->L.fout; P.off.edout = c->L.edout;
+  P.off.erlki = c->L.erlki; P.off.erlko = c->L.erlko; P.off.erlku = c->L.erlku;
+  P.off.erlkl = c->L.erlkl; P.off.Ed_in = c->L.Ed_in; P.off.counters = c->L.counters;
+  P.cnt = c->ctl + CTL_CNT;
+  P.err = c->derr;
+  P.lds_cells = c->lds_cells;
+  P.n_vol_global = c->n_vol_global;
+  P.n_surf_global = c->n_surf_global;
+  /* this rank's share of the global source index space (lineage-sharded) */
+  auto share = [&](int64_t n) -> int64_t {
+    return n > cfg.rank ? (n - cfg.rank + cfg.world - 1) / cfg.world : 0;
+  };
+  P.n_cens_items = c->n_census;
+  P.n_vol_items = share(c->n_vol_global);
+  P.n_surf_items = share(c->n_surf_global);
+
+  HIPCHK(c, hipMemsetAsync(c->T, 0, sizeof(double) * c->L.total, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->ctl, 0, sizeof(unsigned long long) * CTL_WORDS, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->derr, 0, sizeof(int32_t), c->stream));
+
+  auto launch = cfg.comtot_mode == C2D_COMTOT_TABLE ? c2d_launch_transport_fast
+                                                    : c2d_launch_transport_exact;
+  int gen = 0, qin = 0;
+  int64_t n2 = 0, n3 = 0;
+  int launches = 0;
+  for (;;) {
+    P.gen = gen;
+    if (gen == 0) {
+      P.n_items = P.n_cens_items + P.n_vol_items + P.n_surf_items;
+      P.q2_in = nullptr; P.q3_in = nullptr; P.n2_in = 0; P.n3_in = 0;
+    } else {
+      P.n2_in = n2; P.n3_in = n3;
+      P.q2_in = c->q2[qin]; P.q3_in = c->q3[qin];
+      P.n_items = n2 * cfg.split2 + n3 * cfg.split3;
+    }
+    P.q2_out = c->q2[1 - qin];
+    P.q3_out = c->q3[1 - qin];
+    if (P.n_items <= 0) break;
+    HIPCHK(c, hipMemcpyAsync(c->dP, &P, sizeof(KParams), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->ctl + CTL_WORK, 0, sizeof(unsigned long long), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->ctl + CTL_N2, 0, 2 * sizeof(unsigned long long), c->stream));
+    const int64_t waves = (P.n_items + 63) / 64;
+    const int64_t blocks = (waves + 7) / 8;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->max_grid, blocks));
+    if (gen == 0) HIPCHK(c, hipEventRecord(c->ev_g0a, c->stream));
+    int rc = launch(c->dP, grid, c->lds_bytes, c->stream);
+    if (rc) return fail(c, C2D_E_HIP, "transport launch (gen %d): %s", gen,
+                        hipGetErrorString((hipError_t)rc));
+    launches++;
+    if (gen == 0) HIPCHK(c, hipEventRecord(c->ev_g0b, c->stream));
+    unsigned long long nq[2];
+    HIPCHK(c, hipMemcpyAsync(nq, c->ctl + CTL_N2, sizeof nq, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((int64_t)nq[0] > cfg.queue_capacity || (int64_t)nq[1] > cfg.queue_capacity)
+      return fail(c, C2D_E_QUEUE_OVERFLOW, "scatter queue overflow in generation %d (%llu, %llu > %lld)",
+                  gen, nq[0], nq[1], (long long)cfg.queue_capacity);
+    n2 = (int64_t)nq[0];
+    n3 = (int64_t)nq[1];
+    qin = 1 - qin;
+    gen++;
+  }
+  HIPCHK(c, hipEventRecord(c->ev_end, c->stream));
+  unsigned long long ctl[CTL_WORDS];
+  int32_t herr = 0;
+  HIPCHK(c, hipMemcpyAsync(ctl, c->ctl, sizeof ctl, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&herr, c->derr, sizeof herr, hipMemcpyDeviceToHost, c->stream));
+  /* census + volume kappa of the next step = this step's (H3) */
+  HIPCHK(c, hipMemcpyAsync(c->kappa_prev, c->kappa_cur, sizeof(double) * c->ncell * C2D_N_VOL,
+                           hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  float ms0 = 0.f, msall = 0.f;
+  if (launches > 0) {
+    (void)hipEventElapsedTime(&ms0, c->ev_g0a, c->ev_g0b);
+    (void)hipEventElapsedTime(&msall, c->ev_g0a, c->ev_end);
+  }
+  c->last_g0_ms = ms0;
+  c->last_all_ms = msall;
+  c->last_launches = launches;
+  /* counters into the fused buffer (exact integers as f64) */
+  double hc[C2D_NCOUNTERS];
+  for (int i = 0; i < C2D_NCOUNTERS; i++) hc[i] = (double)ctl[CTL_CNT + i];
+  hc[C2D_CNT_GENS] = (double)gen;
+  HIPCHK(c, hipMemcpyAsync(c->T + c->L.counters, hc, sizeof hc, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int64_t ncout = (int64_t)ctl[CTL_NCOUT];
+  c->n_ev = std::min<int64_t>((int64_t)ctl[CTL_NEV], cfg.event_capacity);
+  c->cur_out = out_buf;
+  c->n_census = std::min<int64_t>(ncout, cfg.census_capacity);
+  if (herr & ERR_CENSUS)
+    return fail(c, C2D_E_CENSUS_OVERFLOW, "too many photons: census %lld > capacity %lld",
+                (long long)ncout, (long long)cfg.census_capacity);
+  if (herr & ERR_EVENT)
+    return fail(c, C2D_E_EVENT_OVERFLOW, "event buffer overflow: %llu > %lld",
+                ctl[CTL_NEV], (long long)cfg.event_capacity);
+  if (herr & ERR_QUEUE) return fail(c, C2D_E_QUEUE_OVERFLOW, "scatter queue overflow");
+  if (herr & ERR_SPEC) return fail(c, C2D_E_ARG, "surface packet without a seed spectrum");
+  return C2D_OK;
+}
+
+extern "C" int c2d_transport_step(c2d_ctx* c, const c2d_step_in* in) {
+  int rc = c2d_set_step(c, in);
+  if (rc) return rc;
+  return c2d_run_step(c);
+}
+
+extern "C" int c2d_tally_layout_get(c2d_ctx* c, c2d_tally_layout* out) {
+  if (!c || !out) return C2D_E_ARG;
+  *out = c->L;
+  return C2D_OK;
+}
+
+extern "C" double* c2d_tally_device_ptr(c2d_ctx* c) { return c ? c->T : nullptr; }
+
+extern "C" int c2d_set_tally_buffer(c2d_ctx* c, double* device_ptr) {
+  if (!c) return C2D_E_ARG;
+  c->T = device_ptr ? device_ptr : c->T_own;
+  return C2D_OK;
+}
+
+extern "C" int c2d_tally_download(c2d_ctx* c, double* host, int64_t n) {
+  if (!c || !host || n < c->L.total) return C2D_E_ARG;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, hipMemcpy(host, c->T, sizeof(double) * c->L.total, hipMemcpyDeviceToHost));
+  return C2D_OK;
+}
+
+extern "C" int c2d_events(c2d_ctx* c, double* buf, int64_t cap, int64_t* n) {
+  if (!c || !n) return C2D_E_ARG;
+  *n = c->n_ev;
+  const int64_t m = std::min(cap, c->n_ev);
+  if (m > 0 && buf) {
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipMemcpy(buf, c->ev, sizeof(double) * C2D_EVENT_WORDS * m, hipMemcpyDeviceToHost));
+  }
+  return C2D_OK;
+}
+
+extern "C" int c2d_census_count(c2d_ctx* c, int64_t* n) {
+  if (!c || !n) return C2D_E_ARG;
+  *n = c->n_census;
+  return C2D_OK;
+}
+
+extern "C" int c2d_census_export(c2d_ctx* c, double* d6, int32_t* i5, uint64_t* keys, int64_t cap,
+                                 int64_t* n) {
+  if (!c || !n) return C2D_E_ARG;
+  *n = c->n_census;
+  const int64_t m = std::min(cap, c->n_census);
+  if (m <= 0) return C2D_OK;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const DevCensus& d = c->cens[c->cur_out];
+  std::vector<double> col(m);
+  for (int f = 0; f < 6; f++) {
+    HIPCHK(c, hipMemcpy(col.data(), d.d[f], m * sizeof(double), hipMemcpyDeviceToHost));
+    if (d6)
+      for (int64_t i = 0; i < m; i++) d6[6 * i + f] = col[i];
+  }
+  std::vector<uint32_t> jk(m), bins(m);
+  HIPCHK(c, hipMemcpy(jk.data(), d.jk, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(bins.data(), d.bins, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (i5)
+    for (int64_t i = 0; i < m; i++) {
+      i5[5 * i + 0] = (int32_t)(bins[i] & 0xff);
+      i5[5 * i + 1] = (int32_t)((bins[i] >> 8) & 0xff);
+      i5[5 * i + 2] = (int32_t)((bins[i] >> 16) & 0xff);
+      i5[5 * i + 3] = (int32_t)(jk[i] >> 16);
+      i5[5 * i + 4] = (int32_t)(jk[i] & 0xffff);
+    }
+  if (keys) HIPCHK(c, hipMemcpy(keys, d.key, m * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return C2D_OK;
+}
+
+extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5,
+                                 const uint64_t* keys, int64_t n) {
+  if (!c || n < 0 || (n > 0 && (!d6 || !i5 || !keys))) return C2D_E_ARG;
+  if (n > c->cfg.census_capacity)
+    return fail(c, C2D_E_CENSUS_OVERFLOW, "census import %lld > capacity", (long long)n);
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const DevCensus& d = c->cens[c->cur_out];
+  std::vector<double> col(n);
+  for (int f = 0; f < 6; f++) {
+    for (int64_t i = 0; i < n; i++) col[i] = d6[6 * i + f];
+    if (n) HIPCHK(c, hipMemcpy(d.d[f], col.data(), n * sizeof(double), hipMemcpyHostToDevice));
+  }
+  std::vector<uint32_t> jk(n), bins(n);
+  for (int64_t i = 0; i < n; i++) {
+    const int32_t* q = i5 + 5 * i;
+    if (q[3] < 1 || q[3] > c->nz || q[4] < 1 || q[4] > c->nr || q[0] < 0 || q[0] > 255 ||
+        q[1] < 0 || q[1] > 255 || q[2] < 0 || q[2] > 255)
+      return fail(c, C2D_E_ARG, "census record %lld out of range", (long long)i);
+    bins[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16);
+    jk[i] = ((uint32_t)q[3] << 16) | (uint32_t)q[4];
+  }
+  if (n) {
+    HIPCHK(c, hipMemcpy(d.jk, jk.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(d.bins, bins.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(d.key, keys, n * sizeof(uint64_t), hipMemcpyHostToDevice));
+  }
+  c->n_census = n;
+  return C2D_OK;
+}
+
+extern "C" int c2d_fp_tridag(c2d_ctx* c, const c2d_fp_in* in, double* x) {
+  if (!c || !in || !x || in->ncell < 0 || in->nt < 1) return C2D_E_ARG;
+  if (in->ncell == 0) return C2D_OK;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const size_t n = (size_t)in->ncell * in->nt;
+  double *a, *b, *cc, *r, *xd;
+  HIPCHK(c, dalloc(&a, n));
+  HIPCHK(c, dalloc(&b, n));
+  HIPCHK(c, dalloc(&cc, n));
+  HIPCHK(c, dalloc(&r, n));
+  HIPCHK(c, dalloc(&xd, n));
+  HIPCHK(c, hipMemcpy(a, in->a, n * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(b, in->b, n * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(cc, in->c, n * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(r, in->r, n * sizeof(double), hipMemcpyHostToDevice));
+  /* |b(1)| <= 1e-100 leaves the previous solution untouched (update2d.f:2490-2493) */
+  HIPCHK(c, hipMemcpy(xd, x, n * sizeof(double), hipMemcpyHostToDevice));
+  int rc = c2d_launch_tridag(a, b, cc, r, xd, in->ncell, in->nt, c->stream);
+  if (rc) return fail(c, C2D_E_HIP, "tridag launch: %d", rc);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(x, xd, n * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(a); (void)hipFree(b); (void)hipFree(cc); (void)hipFree(r); (void)hipFree(xd);
+  return C2D_OK;
+}
+
+extern "C" int c2d_last_kernel_ms(c2d_ctx* c, double* gen0_ms, double* all_ms, int32_t* launches) {
+  if (!c) return C2D_E_ARG;
+  if (gen0_ms) *gen0_ms = c->last_g0_ms;
+  if (all_ms) *all_ms = c->last_all_ms;
+  if (launches) *launches = c->last_launches;
+  return C2D_OK;
+}

@@ -1,0 +1,1259 @@
+/*
+ * transport.hip — MI355X (gfx950) photon-packet transport kernels.
+ *
+ * One launch tracks every packet of one "generation" of a Monte-Carlo time
+ * step.  Generation 0 = the step's sources: census packets of the previous
+ * step (src/imcfield2d.f:57-144), volume packets (src/imcvol2d_para.f:90-414)
+ * and surface packets (src/imcsurf2d_para.f:228-534); generation g+1 = the
+ * split2/split3 scatter secondaries created by collisions in generation g
+ * (src/imctrk2d.f:580-684).  The reference's recursive depth-first tracker
+ * (src/imctrk2d.f:8-708) becomes a persistent per-lane state machine:
+ *
+ *   lane idle -> fetch a work item (wave-aggregated, chunked atomic) ->
+ *   sample the source into registers -> split1 probe copies, one packet-step
+ *   per loop iteration -> recombined unscattered copy (imctrk2d(0)) ->
+ *   next work item.
+ *
+ * Packet state never leaves registers between packet-steps; HBM sees only
+ * the source records, the census/event/scatter appends (wave-ballot
+ * compaction: one atomic per wave) and the tally flush.  Cell tallies
+ * (edep, prdep, ecens, npcen) and escape tallies (fout, edout, erlk*) are
+ * privatised per workgroup in LDS and flushed once with atomics.  Every
+ * packet draws from its own Philox stream keyed by lineage (c2d_rng.h), so
+ * a history does not depend on which lane/GPU/generation tracks it.
+ *
+ * Built twice (see Makefile): C2D_VARIANT=0 "exact" (comtot by the full
+ * 199-term sum, -ffp-contract=off: bit-identical to the oracle's lineage
+ * mode) and C2D_VARIANT=1 "fast" (comtot from the per-step cubic table).
+ */
+#include <hip/hip_runtime.h>
+
+#include "c2d_device.hpp"
+#include "c2d_math.h"
+#include "c2d_rng.h"
+
+#ifndef C2D_VARIANT
+#define C2D_VARIANT 0
+#endif
+#if C2D_VARIANT == 0
+#define C2D_SFX(x) x##_exact
+#define C2D_TABLE_COMTOT 0
+#else
+#define C2D_SFX(x) x##_fast
+#define C2D_TABLE_COMTOT 1
+#endif
+
+namespace c2d {
+namespace {
+
+constexpr double PI_REF = 3.1415926536;        /* general.pa:24 */
+constexpr double C_LIGHT = 2.9979245620e10;    /* general.pa:25 */
+constexpr double RAD_CP = 3.333564097e-11;     /* general.pa:23 */
+constexpr double EMASSKEV = 5.11e2;
+constexpr double SIGTHOM = 6.6516e-25;
+constexpr int WAVE = 64;
+constexpr int BLOCK = 512;
+constexpr long long CHUNK = 64;
+
+/* Fortran REAL literals promoted to double (src/imcvol2d_para.f:204,221,247,268,336) */
+#define F32(x) ((double)(float)(x))
+
+enum : int32_t { ST_IDLE = 0, ST_PROBE = 1, ST_TRACK = 2 };
+enum : int32_t { FL_CONT = 0, FL_END = 1, FL_COLLIDE = 2 };
+
+struct Pkt {
+  double xnu, wmu, phi, rpre, zpre, dcen, ew, wtmin;
+  int32_t jph, kph, jgpsp, jgplc, jgpmu, mode, kap;
+  uint64_t key;
+  uint32_t ctr;
+  uint32_t nflight;   /* safety cap: a history that stops progressing is aborted */
+};
+
+/* Safety caps (never reached by a valid history; they keep a malformed input
+ * from hanging the GPU).  Hitting one counts C2D_CNT_ABORTED. */
+constexpr uint32_t MAX_FLIGHTS = 1u << 20;
+constexpr int MAX_REJECT = 1 << 20;
+
+/* per-thread counters, reduced once per wave at the end */
+struct LaneCnt {
+  uint32_t steps, escapes, census, collide, killed, sources, compb, events, aborted;
+};
+
+/* Tally views.  Cell tallies edep|prdep|ecens|npcen (stride ncell) and
+ * escape tallies fout|edout|erlki|erlko|erlku|erlkl have the same layout in
+ * LDS and in the fused global buffer, so three base pointers suffice. */
+struct Tal {
+  const Geo* g;      /* LDS image of the grids */
+  double* cells;     /* LDS (privatised) or global */
+  double* esc;       /* LDS */
+};
+#define T_EDEP(P, T) ((T).cells)
+#define T_PRDEP(P, T) ((T).cells + (P).ncell)
+#define T_ECENS(P, T) ((T).cells + 2 * (P).ncell)
+#define T_NPCEN(P, T) ((T).cells + 3 * (P).ncell)
+#define T_FOUT(P, T) ((T).esc)
+#define T_EDOUT(P, T) ((T).esc + (P).nmu * C2D_NPHOMAX)
+#define T_ERLKI(P, T) ((T).esc + (P).nmu * (C2D_NPHOMAX + C2D_NPHLCMAX))
+#define T_ERLKO(P, T) (T_ERLKI(P, T) + (P).nz)
+#define T_ERLKU(P, T) (T_ERLKI(P, T) + 2 * (P).nz)
+#define T_ERLKL(P, T) (T_ERLKI(P, T) + 2 * (P).nz + (P).nr)
+
+__device__ __forceinline__ double U(Pkt& p) { return c2d_draw(p.key, p.ctr++); }
+
+__device__ __forceinline__ double clampd(double v, double lim) {
+  if (v > lim) v = lim;
+  if (v < -lim) v = -lim;
+  return v;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+/* Wave-ballot compaction: the lanes executing this call reserve consecutive
+ * slots of *counter with a single atomic. */
+__device__ __forceinline__ unsigned long long wave_reserve(unsigned long long* counter) {
+  unsigned long long mask = __ballot(1);
+  uint32_t leader = (uint32_t)(__ffsll((long long)mask) - 1);
+  uint32_t lane = lane_id();
+  unsigned long long lt = (lane == 0) ? 0ull : (mask & ((~0ull) >> (64 - lane)));
+  uint32_t rank = (uint32_t)__popcll(lt);
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(mask));
+  uint32_t lo = __builtin_amdgcn_readlane((uint32_t)base, leader);
+  uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(base >> 32), leader);
+  return (((unsigned long long)hi << 32) | lo) + rank;
+}
+
+/* ------------------------------------------------------------------ */
+/* comtot (src/comtot2d.f:1-334, icoms=6 :219-247), intg_v :337, dilog :356 */
+/* ------------------------------------------------------------------ */
+__device__ double dilog(double x) {
+  const double C[21] = {0,
+      0.42996693560813697, 0.40975987533077105, -0.01858843665014592,
+      0.00145751084062268, -0.00014304184442340, 0.1588415541880e-4,
+      -0.190784959387e-5, 0.024195180854e-5, -0.003193341274e-5,
+      0.000434545063e-5, -0.000060578480e-5, 0.000008612098e-5,
+      -0.000001244332e-5, 0.000000182256e-5, -0.000000027007e-5,
+      0.000000004042e-5, -0.000000000610e-5, 0.000000000093e-5,
+      -0.000000000014e-5, 0.000000000002e-5};
+  const double HF = 0.5, PI2 = PI_REF * PI_REF, PI3 = PI2 / 3, PI6 = PI2 / 6,
+               PI12 = PI2 / 12;
+  double T, H, Y, S, A, ALFA, B1, B2, B0 = 0.0;
+  if (x == 1) {
+    H = PI6;
+  } else if (x == -1) {
+    H = -PI12;
+  } else {
+    T = -x;
+    if (T <= -2) {
+      Y = -1 / (1 + T);
+      S = 1;
+      B1 = c2d_log(-T);
+      B2 = c2d_log(1 + 1 / T);
+      A = -PI3 + HF * (B1 * B1 - B2 * B2);
+    } else if (T < -1) {
+      Y = -1 - T;
+      S = -1;
+      A = c2d_log(-T);
+      A = -PI6 + A * (A + c2d_log(1 + 1 / T));
+    } else if (T <= -0.5) {
+      Y = -(1 + T) / T;
+      S = 1;
+      A = c2d_log(-T);
+      A = -PI6 + A * (-HF * A + c2d_log(1 + T));
+    } else if (T < 0) {
+      Y = -T / (1 + T);
+      S = -1;
+      B1 = c2d_log(1 + T);
+      A = HF * B1 * B1;
+    } else if (T <= 1) {
+      Y = T;
+      S = 1;
+      A = 0;
+    } else {
+      Y = 1 / T;
+      S = -1;
+      B1 = c2d_log(T);
+      A = PI6 + HF * B1 * B1;
+    }
+    H = Y + Y - 1;
+    ALFA = H + H;
+    B1 = 0;
+    B2 = 0;
+#pragma unroll
+    for (int i = 20; i >= 1; i--) {
+      B0 = C[i] + ALFA * B1 - B2;
+      B2 = B1;
+      B1 = B0;
+    }
+    H = -(S * (B0 - H * B2) + A);
+  }
+  return H;
+}
+
+__device__ __forceinline__ double intg_v(double x) {
+  double i1 = -x / 2.0 + 0.5 / (1.0 + x);
+  double i2 = 4.0 * dilog(-x);
+  double i3 = (9.0 + x + 8.0 / x) * c2d_log(1.0 + x);
+  return i1 + i2 + i3;
+}
+
+/* cross section for one Lorentz-factor bin i (1-based): sigma_E(i, x) */
+__device__ __forceinline__ double sigma_E_bin(double gnti, double x) {
+  double gamma0 = gnti + 1.0;
+  double betta = __builtin_sqrt(1.0 - 1.0 / (gamma0 * gamma0));
+  if (x * gamma0 * (1 + betta) < 1.0e-2) return SIGTHOM * (1.0 - 2.0 * x * gamma0);
+  return 9.375e-2 * SIGTHOM / (gamma0 * gamma0) / betta / (x * x) *
+         (intg_v(2 * gamma0 * (1 + betta) * x) - intg_v(2 * gamma0 * (1 - betta) * x));
+}
+
+__device__ __noinline__ double comtot_exact(const KParams& P, int cell, double xnuc) {
+  const double* fnt = P.f_nt + (int64_t)cell * C2D_NUM_NT;
+  double cosig = 0.0, x = xnuc / EMASSKEV;
+  for (int i = 1; i <= C2D_NUM_NT - 1; i++) {
+    double gi = P.gnt[i - 1], gi1 = P.gnt[i];
+    double sE = sigma_E_bin(gi, x);
+    cosig = cosig + sE * fnt[i - 1] * (gi1 - gi);
+  }
+  if (cosig < 1.0e-40) return 1.0e-40;
+  return P.n_e[cell] * cosig;
+}
+
+#if C2D_TABLE_COMTOT
+/* cubic Lagrange interpolation of the per-step table in u = ln(xnu) */
+__device__ __forceinline__ double comtot_table(const KParams& P, int cell, double xnu) {
+  double u = c2d_log(xnu);
+  double s = (u - C2D_COMTAB_U0) * P.comtab_du_inv;
+  if (!(s >= 1.0 && s < (double)(C2D_COMTAB_N - 3))) return comtot_exact(P, cell, xnu);
+  int g = (int)s;
+  double t = s - (double)g;
+  const double* tb = P.comtab + (int64_t)cell * C2D_COMTAB_N + (g - 1);
+  double y0 = tb[0], y1 = tb[1], y2 = tb[2], y3 = tb[3];
+  double tm1 = t - 1.0, tm2 = t - 2.0, tp1 = t + 1.0;
+  double cosig = -(t * tm1 * tm2) * (1.0 / 6.0) * y0 + (tp1 * tm1 * tm2) * 0.5 * y1 -
+                 (tp1 * t * tm2) * 0.5 * y2 + (tp1 * t * tm1) * (1.0 / 6.0) * y3;
+  if (cosig < 1.0e-40) return 1.0e-40;
+  return P.n_e[cell] * cosig;
+}
+#endif
+
+/* ------------------------------------------------------------------ */
+/* binning (src/compb_2d.f:249-302, src/imcleak2d.f:329-405)            */
+/* ------------------------------------------------------------------ */
+__device__ __forceinline__ int bin_sp(const Geo* g, int nphtotal, double xnu, double fbot,
+                                      double ftop, int top_value) {
+  int jbot = 1, jtop = nphtotal + 1, jmid;
+  double hubot = fbot * g->hu[1];
+  double hutop = ftop * g->hu[jtop];
+  if (xnu >= hutop) return top_value;
+  if (xnu <= hubot) return 0;
+  for (;;) {
+    jmid = (jbot + jtop) / 2;
+    if (jmid == jbot) break;
+    if (xnu == g->hu[jmid]) break;
+    if (xnu < g->hu[jmid]) jtop = jmid;
+    else jbot = jmid;
+  }
+  return jmid;
+}
+__device__ __forceinline__ int bin_lc(const Geo* g, int nph_lc, double xnu) {
+  for (int m = 1; m <= nph_lc; m++)
+    if (xnu > g->Elcmin[m] && xnu <= g->Elcmax[m]) return m;
+  return 0;
+}
+__device__ __forceinline__ int bin_mu(const Geo* g, int nmu, double wmu) {
+  for (int n = 1; n <= nmu; n++)
+    if (wmu <= g->mu[n]) return n;
+  return nmu;
+}
+/* first i in 1..n-1 with x < E[i+1], else n (the reference's linear scans
+ * imctrk2d.f:382-384 and :547-549), by bisection on a monotone grid */
+__device__ __forceinline__ int grid_index(const double* E, int n, double x) {
+  int lo = 1, hi = n;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (x < E[mid + 1]) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+/* `i=0; do i=i+1 while (cdf(i) < rnum .and. i < n)` (imcvol2d_para.f:170-172) */
+__device__ __forceinline__ int cdf_index(const double* cdf /*0-based*/, int n, double rnum,
+                                         int linear) {
+  if (linear) {
+    int i = 0;
+    do { i = i + 1; } while (cdf[i - 1] < rnum && i < n);
+    return i;
+  }
+  int lo = 1, hi = n;   /* smallest i with cdf(i) >= rnum, capped at n */
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (cdf[mid - 1] < rnum) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+/* ------------------------------------------------------------------ */
+/* nth2d (src/nontherm2d.f:159-183) + compb2d (src/compb_2d.f:1-318)    */
+/* ------------------------------------------------------------------ */
+__device__ __noinline__ int compb2d(const KParams& P, const Tal T, Pkt& p, LaneCnt& lc) {
+  const double fuzz = 1.0e-10, lim = 9.9999999e-1;
+  const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
+  const double* Pc = P.Pnt + (int64_t)cell * C2D_NUM_NT;
+  double znu = p.xnu / EMASSKEV;
+  double gamm, betb, omeg, tl, tr, znue, betz, xknot;
+  double sz, games, phat, znues, wa, wb, swa;
+  int i_gam;
+  int guard = 0;
+  lc.compb++;
+  for (;;) {
+    if (++guard > MAX_REJECT) { lc.aborted++; break; }
+    /* nth2d */
+    double rnum = U(p);
+    rnum = (double)(int32_t)(rnum * 1.0e6) / 1.0e6 + 1.0e-6 * U(p);
+    int i = 2;
+    {   /* first i in 2..200 with Pnt(i) > rnum, else 201 (bisection on the CDF) */
+      int lo = 2, hi = C2D_NUM_NT + 1;
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (Pc[mid - 1] > rnum) hi = mid;
+        else lo = mid + 1;
+      }
+      i = lo > C2D_NUM_NT ? C2D_NUM_NT : lo;   /* Pnt(200) = 1 > rnum in valid input */
+    }
+    gamm = __builtin_sqrt(P.gnt[i - 1] * P.gnt[i - 2]) + 1.0;
+    betb = __builtin_sqrt(1.0 - 1.0 / (gamm * gamm));
+    atomicAdd(&P.T[P.off.nelectron + i], 1.0);
+    i_gam = i;
+    omeg = 2.0 * U(p) - 1.0;
+    omeg = clampd(omeg, lim);
+    tl = U(p);
+    tr = 0.5 * (1.0 - betb * omeg);
+    if (tl > tr) omeg = -omeg;
+    omeg = clampd(omeg, lim);
+    znue = (1.0 - betb * omeg) * znu * gamm;
+    if (znue < 1.0e-10) continue;
+    if (znue <= 1.0e-2) {
+      xknot = 1.0 - znue * (2.0 - znue * (5.2 - znue * (13.3 - 1.144e3 * znue / 3.5e1)));
+    } else {
+      double znue3 = znue * znue * znue;
+      betz = 1.0 + 2.0 * znue;
+      double gamz = znue * (znue - 2.0) - 2.0;
+      double xxx = 4.0 * znue + 2.0 * znue3 * (1.0 + znue) / (betz * betz) + gamz * c2d_log(betz);
+      xknot = 3.75e-1 * xxx / znue3;
+    }
+    if (U(p) > xknot) continue;
+    break;
+  }
+  betz = 1.0 + 2.0 * znue;
+  for (;;) {
+    if (++guard > 2 * MAX_REJECT) { lc.aborted++; break; }
+    sz = (1.0 + 2.0 * znue * U(p)) / betz;
+    games = 1.0 + (1.0 - 1.0 / sz) / znue;
+    if ((1.0 - games * games) < 0.0) continue;
+    tr = games * games - 1.0 + sz + 1.0 / sz;
+    phat = betz + 1.0 / betz;
+    if (U(p) * phat > tr) continue;
+    break;
+  }
+  znues = znue * sz;
+  for (;;) {
+    if (++guard > 3 * MAX_REJECT) { lc.aborted++; break; }
+    wa = U(p);
+    wb = 2.0 * U(p) - 1.0;
+    swa = wa * wa + wb * wb;
+    if (swa >= 1.0 || swa <= 1.0e-20) continue;
+    break;
+  }
+  double cazes = (wa * wa - wb * wb) / swa;
+  double omege = clampd((omeg - betb) / (1.0 - betb * omeg), lim);
+  double omeges = games * omege +
+                  cazes * __builtin_sqrt((1.0 - omege * omege + fuzz) * (1.0 - games * games));
+  omeges = clampd(omeges, lim);
+  double znus = (1.0 + betb * omeges) * gamm * znues;
+  double gams = clampd(1.0 - (znue - znues) / (znu * znus), lim);
+  for (;;) {
+    if (++guard > 4 * MAX_REJECT) { lc.aborted++; break; }
+    wa = U(p);
+    wb = 2.0 * U(p) - 1.0;
+    swa = wa * wa + wb * wb;
+    if (swa >= 1.0 || swa <= 1.0e-20) continue;
+    break;
+  }
+  double cazs = clampd((wa * wa - wb * wb) / swa, lim);
+  double wmus = p.wmu * gams +
+                cazs * __builtin_sqrt((1.0 - gams * gams) * (1.0 - p.wmu * p.wmu + fuzz));
+  wmus = clampd(wmus, lim);
+  double xnus = znus * EMASSKEV;
+  double cosdphi = clampd((gams - p.wmu * wmus) /
+                              __builtin_sqrt((1.0 - p.wmu * p.wmu) * (1.0 - wmus * wmus)),
+                          lim);
+  double dphi = c2d_acos(cosdphi);
+  double phis = p.phi + dphi;
+  p.jgpsp = bin_sp(T.g, P.nphtotal, xnus, 1.000001, 0.999999, 0);
+  p.jgplc = bin_lc(T.g, P.nph_lc, xnus);
+  p.jgpmu = bin_mu(T.g, P.nmu, wmus);
+  p.ew = p.ew * xnus / p.xnu;
+  p.xnu = xnus;
+  p.wmu = wmus;
+  p.phi = phis;
+  return i_gam;
+}
+
+/* ------------------------------------------------------------------ */
+/* escapes (src/imcleak2d.f:2-320, cr_sent = 0)                          */
+/* ------------------------------------------------------------------ */
+__device__ __forceinline__ void push_event(const KParams& P, double tb, const Pkt& p, LaneCnt& lc) {
+  unsigned long long slot = wave_reserve(P.n_ev);
+  if (slot < (unsigned long long)P.cap_ev) {
+    double* e = P.ev + slot * C2D_EVENT_WORDS;
+    e[0] = tb; e[1] = p.xnu; e[2] = p.ew; e[3] = p.rpre; e[4] = p.zpre; e[5] = p.wmu; e[6] = p.phi;
+  } else {
+    atomicOr(P.err, ERR_EVENT);
+  }
+  lc.events++;
+}
+
+__device__ __forceinline__ void escape_tally(const KParams& P, const Tal& T, const Pkt& p) {
+  if (p.jgplc > 0) atomicAdd(&T_EDOUT(P, T)[(p.jgpmu - 1) * C2D_NPHLCMAX + (p.jgplc - 1)], p.ew / P.dt);
+  if (p.jgpsp > 0 && P.spec_switch == 0)
+    atomicAdd(&T_FOUT(P, T)[(p.jgpmu - 1) * C2D_NPHOMAX + (p.jgpsp - 1)], p.ew);
+}
+
+/* returns idead: 1 = left the system, 0 = continue (axis pass-through) */
+__device__ __forceinline__ int imcleak(const KParams& P, const Tal& T, Pkt& p, LaneCnt& lc) {
+  if (p.kph == 0) {
+    if (P.rmin > 1.0e-10) {
+      atomicAdd(&T_ERLKI(P, T)[p.jph - 1], p.ew);
+      lc.escapes++;
+      return 1;
+    }
+    p.phi = 1.0e-6;
+    p.kph = 1;
+    return 0;
+  }
+  lc.escapes++;
+  const double tb = P.time + P.dt - RAD_CP * p.dcen;   /* H4: fresh t_bound everywhere */
+  if (p.jph <= 0) {
+    if (P.tbbl[p.kph - 1] > 0.0) {
+      atomicAdd(&P.T[P.off.Ed_in + p.kph - 1], p.ew);
+      atomicAdd(&T_ERLKL(P, T)[p.kph - 1], p.ew);
+    }
+    if (P.ncycle > 0) {
+      push_event(P, tb, p, lc);
+      escape_tally(P, T, p);
+    }
+    return 1;
+  }
+  if (p.jph != P.nz + 1) {
+    atomicAdd(&T_ERLKO(P, T)[p.jph - 1], p.ew);
+    if (P.ncycle > 0) {
+      push_event(P, tb, p, lc);
+      escape_tally(P, T, p);
+    }
+    return 1;
+  }
+  atomicAdd(&T_ERLKU(P, T)[p.kph - 1], p.ew);
+  if (P.ncycle > 0 && p.wmu < F32(0.98)) {
+    push_event(P, tb, p, lc);
+    escape_tally(P, T, p);
+  }
+  return 1;
+}
+
+/* census write (src/imctrk2d.f:528-578) */
+__device__ __forceinline__ void census_write(const KParams& P, const Tal& T, const Pkt& p, LaneCnt& lc) {
+  const Geo* g = T.g;
+  int cell = (p.jph - 1) * P.nr + (p.kph - 1);
+  atomicAdd(&T_NPCEN(P, T)[cell], 1.0);
+  atomicAdd(&T_ECENS(P, T)[cell], p.ew);
+  int i = grid_index(g->E_field, C2D_NPHFIELD, p.xnu);
+  double Egg_min = (g->E_field[1] * g->E_field[1]) / g->E_field[2];
+  if (p.xnu > Egg_min)
+    atomicAdd(&P.T[P.off.n_field + (int64_t)cell * C2D_NPHFIELD + (i - 1)], 6.25e8 * p.ew / p.xnu);
+  unsigned long long slot = wave_reserve(P.n_cout);
+  if (slot < (unsigned long long)P.cap_cout) {
+    P.cout.rpre[slot] = p.rpre;
+    P.cout.zpre[slot] = p.zpre;
+    P.cout.wmu[slot] = p.wmu;
+    P.cout.phi[slot] = p.phi;
+    P.cout.ew[slot] = p.ew;
+    P.cout.xnu[slot] = p.xnu;
+    P.cout.jk[slot] = ((uint32_t)p.jph << 16) | (uint32_t)p.kph;
+    P.cout.bins[slot] = (uint32_t)p.jgpsp | ((uint32_t)p.jgplc << 8) | ((uint32_t)p.jgpmu << 16);
+    P.cout.key[slot] = c2d_derive(p.key, C2D_TAG_CENSUS, p.ctr, 0u);
+  } else {
+    atomicOr(P.err, ERR_CENSUS);
+  }
+  lc.census++;
+}
+
+__device__ __forceinline__ void push_scat(const KParams& P, ScatRec* q, unsigned long long* n, const ScatRec& r) {
+  unsigned long long slot = wave_reserve(n);
+  if (slot < (unsigned long long)P.cap_q) {
+    q[slot] = r;
+  } else {
+    atomicOr(P.err, ERR_QUEUE);
+  }
+}
+
+__device__ __forceinline__ ScatRec make_rec(const Pkt& p, uint64_t key, uint32_t ctr) {
+  ScatRec r;
+  r.rpre = p.rpre; r.zpre = p.zpre; r.wmu = p.wmu; r.phi = p.phi; r.ew = p.ew; r.xnu = p.xnu;
+  r.dcen = p.dcen;
+  r.jk = ((uint32_t)p.jph << 16) | (uint32_t)p.kph;
+  r.ctr = ctr;
+  r.key = key;
+  r.kap = (uint32_t)p.kap;
+  r.pad = 0;
+  return r;
+}
+
+__device__ __forceinline__ void load_rec(Pkt& p, const ScatRec& r) {
+  p.rpre = r.rpre; p.zpre = r.zpre; p.wmu = r.wmu; p.phi = r.phi; p.ew = r.ew; p.xnu = r.xnu;
+  p.dcen = r.dcen;
+  p.jph = (int32_t)(r.jk >> 16);
+  p.kph = (int32_t)(r.jk & 0xffffu);
+  p.kap = (int32_t)r.kap;
+}
+
+/* ------------------------------------------------------------------ */
+/* one packet-step: label 100 ... 900 of src/imctrk2d.f:139-578          */
+/* ------------------------------------------------------------------ */
+struct ComCache {
+  int32_t cell0, cell1;
+  double v0, v1;
+};
+
+__device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, ComCache& cc, LaneCnt& lc) {
+  const double lim8 = 9.9999999e-1, lim9 = 0.999999999;
+  const Geo* g = T.g;
+  double mb_ran;
+  if (p.mode == 0) {
+    mb_ran = 1.0e-10;
+  } else {
+    mb_ran = U(p);   /* Philox uniform is never 0: the `goto 100` redraw cannot trigger */
+  }
+  double colmfp = -c2d_log(mb_ran);
+  if (p.ew < 1.0e-40) return FL_END;
+  if (++p.nflight > MAX_FLIGHTS) {
+    lc.aborted++;
+    return FL_END;
+  }
+  p.wmu = clampd(p.wmu, lim8);
+  const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
+  double comac = 0.0;
+  if (p.mode != 0) {
+#if C2D_TABLE_COMTOT
+    comac = comtot_table(P, cell, p.xnu);
+    (void)cc;
+#else
+    /* comtot is a pure function of (cell, xnu): caching per packet is exact
+     * (the reference caches per imctrk2d(-1) call, imctrk2d.f:170-178) */
+    if (cc.cell0 == cell) {
+      comac = cc.v0;
+    } else if (cc.cell1 == cell) {
+      comac = cc.v1;
+    } else {
+      comac = comtot_exact(P, cell, p.xnu);
+      cc.cell1 = cc.cell0; cc.v1 = cc.v0;
+      cc.cell0 = cell; cc.v0 = comac;
+    }
+#endif
+  }
+  const double sigsc = comac;
+  const double rkm1 = (p.kph == 1) ? P.rmin : g->r[p.kph - 1];
+  const double xqsqleft = rkm1 * rkm1;
+  double dcol;
+  if (p.mode != 0)
+    dcol = colmfp / sigsc;
+  else
+    dcol = 100 * (g->r[P.nr] > g->z[P.nz] ? g->r[P.nr] : g->z[P.nz]);
+  double trld;
+  int ikind;
+  if (p.dcen <= dcol) { trld = p.dcen; ikind = 2; }
+  else { trld = dcol; ikind = 3; }
+  lc.steps++;
+  /* geometry (imctrk2d.f:228-379) */
+  double Eta = c2d_cos(p.phi);
+  const int eta_switch = (p.phi <= PI_REF && p.phi >= 1.0e-10) ? 1 : -1;
+  Eta = clampd(Eta, lim8);
+  const double rpre = p.rpre, zpre = p.zpre, wmu = p.wmu;
+  const double disp = Eta * rpre;
+  const double psq = rpre * rpre * (1.0 - Eta * Eta);
+  int kbnd, inout, knew, jnew;
+  double rbnd, Zbnd;
+  if (Eta < 0.0 && psq < xqsqleft) {
+    kbnd = p.kph - 1;
+    inout = -1;
+    rbnd = rkm1;
+  } else {
+    kbnd = p.kph;
+    inout = 1;
+    rbnd = g->r[p.kph];
+  }
+  double dpbsq = rbnd * rbnd - psq;
+  if (dpbsq < 1.0e-6) dpbsq = 1.0e-6;
+  const double disbr = (double)inout * __builtin_sqrt(dpbsq) - disp;
+  const double swmu = __builtin_sqrt(1.0 - wmu * wmu);
+  double trldb = disbr / swmu;
+  const double Zr = zpre + wmu * trldb;
+  const double zlow = (p.jph == 1) ? P.zmin : g->z[p.jph - 1];
+  const double zup = g->z[p.jph];
+  if (Zr > zup || Zr < zlow) {
+    Zbnd = (Zr > zup) ? zup : zlow;
+    knew = p.kph;
+    jnew = (Zr > zup) ? p.jph + 1 : p.jph - 1;
+    const double f = (Zbnd - zpre) * swmu / wmu;
+    rbnd = __builtin_sqrt(rpre * rpre + f * f + 2.0 * rpre * f * Eta);
+    trldb = __builtin_sqrt(f * f + (Zbnd - zpre) * (Zbnd - zpre));
+  } else {
+    knew = p.kph + inout;
+    jnew = p.jph;
+    rbnd = (kbnd > 0) ? g->r[kbnd] : P.rmin;
+    Zbnd = Zr;
+  }
+  double rnew, znew;
+  if (trldb < trld) {
+    ikind = 1;
+    trld = trldb;
+    rnew = rbnd;
+    znew = Zbnd;
+  } else {
+    jnew = p.jph;
+    knew = p.kph;
+    const double f = trld * swmu;
+    rnew = __builtin_sqrt(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
+    znew = zpre + trld * wmu;
+  }
+  /* absorption (imctrk2d.f:382-462); gamma-gamma opacity inert (H6) */
+  const int ie = grid_index(g->E_ph, C2D_N_VOL, p.xnu);
+  const double* kap = p.kap ? P.kappa_s : P.kappa_cv;
+  double sigabs = 1.0e-40 + 1.0 * kap[(int64_t)cell * C2D_N_VOL + (ie - 1)];
+  if (sigabs < 1.0e-40) sigabs = 1.0e-40;
+  const double xabs = sigabs * trld;
+  const double ewnew = (xabs < 100.0) ? p.ew * c2d_exp(-xabs) : 0.0;
+  double deleabs = p.ew - ewnew;
+  if (deleabs < 1.0e-50) deleabs = 1.0e-50;
+  double wmustar;
+  if (xabs <= 0.00001) {
+    wmustar = wmu;
+  } else {
+    double mr, sstar = 0.0;
+    for (int guard = 0; guard < MAX_REJECT; guard++) {
+      mr = U(p);
+      if (mr < p.ew / deleabs) {
+        sstar = -c2d_log(1.0 - mr * deleabs / p.ew) / sigabs;
+        break;
+      }
+    }
+    const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
+    wmustar = (wmu * rpre + sstar) / denom;
+  }
+  const double delpr = deleabs * wmustar * C_LIGHT;
+  if (p.mode != 0) {
+    atomicAdd(&T_EDEP(P, T)[cell], deleabs);
+    atomicAdd(&T_PRDEP(P, T)[cell], delpr);
+  }
+  if (ewnew <= p.wtmin) {
+    lc.killed++;
+    return FL_END;
+  }
+  p.ew = ewnew;
+  p.dcen = p.dcen - trld;
+  Eta = (trld + Eta * rpre) / rnew;          /* hazard H1: trld, not f (imctrk2d.f:472) */
+  Eta = clampd(Eta, lim9);
+  p.phi = c2d_acos(Eta);
+  if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
+  p.rpre = rnew;
+  p.zpre = znew;
+  if (ikind == 1) {
+    if (jnew == P.nz + 1 || jnew == 0 || knew == P.nr + 1 || knew == 0) {
+      p.jph = jnew;
+      p.kph = knew;
+      if (p.mode == -1) return FL_END;
+      if (imcleak(P, T, p, lc) == 1) return FL_END;
+      return FL_CONT;
+    }
+    p.kph = knew;
+    p.jph = jnew;
+    return FL_CONT;
+  }
+  if (ikind == 2) {
+    if (p.mode != -1) census_write(P, T, p, lc);
+    return FL_END;
+  }
+  lc.collide++;
+  return FL_COLLIDE;
+}
+
+/* ------------------------------------------------------------------ */
+/* sources                                                             */
+/* ------------------------------------------------------------------ */
+/* planck (src/planck2d.f:1-141) */
+__device__ __forceinline__ void planck(const KParams& P, const Tal& T, Pkt& p, double tpl) {
+  double u4, ap0, ap1 = 1.0, ap2 = 1.0, ap3 = 1.0, rn1;
+  do {
+    u4 = U(p);
+    u4 = u4 * U(p);
+    u4 = u4 * U(p);
+    u4 = u4 * U(p);
+  } while (u4 <= 1.0e-200);
+  ap0 = -c2d_log(u4);
+  rn1 = 1.08232 * U(p);
+  while (!(rn1 <= ap1)) {
+    ap2 = ap2 + 1.0;
+    ap3 = 1.0 / ap2;
+    ap1 = ap1 + (ap3 * ap3) * (ap3 * ap3);
+  }
+  p.xnu = ap0 * ap3 * tpl;
+  p.jgpsp = bin_sp(T.g, P.nphtotal, p.xnu, F32(1.000001), F32(0.999999), 0);
+  p.jgplc = bin_lc(T.g, P.nph_lc, p.xnu);
+  p.jgpmu = bin_mu(T.g, P.nmu, p.wmu);
+}
+
+/* file_sample (src/imcsurf2d_para.f:694-788) */
+__device__ __forceinline__ void file_sample(const KParams& P, const Tal& T, Pkt& p, int spec) {
+  if (spec < 0 || spec >= P.n_spectra) {
+    atomicOr(P.err, ERR_SPEC);
+    p.xnu = 1.0;
+    p.jgpsp = 0; p.jgplc = 0; p.jgpmu = bin_mu(T.g, P.nmu, p.wmu);
+    return;
+  }
+  const SpecDev sp = P.spectra[spec];
+  double x1 = U(p);
+  int i;
+  for (i = 1; i <= sp.nfile - 1; i++)
+    if (sp.P_file[i - 1] > x1) break;
+  if (i > sp.nfile - 1) i = sp.nfile - 1;
+  double x2 = U(p);
+  double Ei = sp.E_file[i - 1], a1 = sp.a1[i - 1], Ii = sp.I_file[i - 1], Fi = sp.F_file[i - 1];
+  p.xnu = Ei * c2d_pow(a1 * Ii * x2 / (Fi * Ei) + 1.0, 1.0 / a1);
+  p.jgpsp = bin_sp(T.g, P.nphtotal, p.xnu, 1.000001, 0.999999, 0);
+  p.jgplc = bin_lc(T.g, P.nph_lc, p.xnu);
+  p.jgpmu = bin_mu(T.g, P.nmu, p.wmu);
+}
+
+/* one volume packet of vol_calc (src/imcvol2d_para.f:157-392) */
+__device__ __forceinline__ void vol_source(const KParams& P, const Tal& T, Pkt& p, int jv, int kv) {
+  const Geo* g = T.g;
+  const int cell = (jv - 1) * P.nr + (kv - 1);
+  const double* vf = P.vfrac + 4 * cell;
+  const double f_thermal = vf[0], f_inn = vf[1], f_outer = vf[2], f_upper = vf[3];
+  const double rlow = (kv == 1) ? P.rmin : g->r[kv - 1];
+  p.jph = jv;
+  p.kph = kv;
+  p.ew = P.ewsv[cell];
+  p.dcen = C_LIGHT * P.dt * U(p);
+  double rnum = U(p), psi;
+  if (rnum < f_thermal) {
+    rnum = U(p);
+    int i = cdf_index(P.eps_th + (int64_t)cell * C2D_N_VOL, C2D_N_VOL, rnum, P.eps_linear);
+    if (i < C2D_N_VOL) p.xnu = g->E_ph[i] + U(p) * (g->E_ph[i + 1] - g->E_ph[i]);
+    else p.xnu = g->E_ph[i];
+    double rnum0 = U(p);
+    if (rnum0 < f_inn) {
+      p.wmu = clampd(2.0 * U(p) - 1.0, 9.9999999e-1);
+      double x1 = U(p), x2 = U(p);
+      if (x1 < 0.5) {
+        p.phi = 1.1e1 / 7.0 + (1.1e1 / 7.0) * x2;
+        if (p.phi < 1.57079638) p.phi = 1.57079638;
+      } else {
+        p.phi = -1.1e1 / 7.0 - (1.1e1 / 7.0) * x2;
+        if (p.phi > -1.57079638) p.phi = -1.57079638;
+      }
+      p.rpre = (kv == 1) ? F32(1.00001) * P.rmin : F32(1.00001) * g->r[kv - 1];
+      p.zpre = (jv == 1) ? g->z[1] * U(p) : g->z[jv - 1] + U(p) * (g->z[jv] - g->z[jv - 1]);
+    } else if (rnum0 < f_outer) {
+      p.wmu = clampd(2.0 * U(p) - 1.0, 9.9999999e-1);
+      p.rpre = F32(0.999999) * g->r[kv];
+      p.zpre = (jv == 1) ? g->z[1] * U(p) : g->z[jv - 1] + U(p) * (g->z[jv] - g->z[jv - 1]);
+      p.phi = -1.1e1 / 7.0 + 2.2e1 / 7.0 * U(p);
+      if (p.phi < -1.5707963) p.phi = -1.57079063;
+      if (p.phi > 1.5707963) p.phi = 1.5707963;
+    } else if (rnum0 < f_upper) {
+      p.wmu = U(p);
+      if (p.wmu > 9.9999999e-1) p.wmu = 9.9999999e-1;
+      if (p.wmu < 0.0) p.wmu = 0.0;
+      p.phi = 4.4e1 / 7.0 * U(p);
+      if (p.phi > 2.0 * PI_REF) p.phi = 2.0 * PI_REF;
+      psi = U(p);
+      p.zpre = F32(0.999999) * g->z[jv];
+      p.rpre = __builtin_sqrt(rlow * rlow + psi * (g->r[kv] * g->r[kv] - rlow * rlow));
+    } else {
+      p.wmu = -U(p);
+      p.phi = 4.4e1 / 7.0 * U(p);
+      if (p.wmu > 0.0) p.wmu = 0.0;
+      if (p.wmu < -9.9999999e-1) p.wmu = -9.9999999e-1;
+      if (p.phi > 2.0 * PI_REF) p.phi = 2.0 * PI_REF;
+      if (jv == 1) {
+        p.zpre = F32(1.000001) * P.zmin;
+        if (p.zpre <= P.zmin) p.zpre = P.zmin + 1.0e-6;
+      } else {
+        p.zpre = F32(1.000001) * g->z[jv - 1];
+        if (p.zpre <= g->z[jv - 1]) p.zpre = g->z[jv - 1] + 1.0e-6;
+      }
+      psi = U(p);
+      p.rpre = __builtin_sqrt(rlow * rlow + psi * (g->r[kv] * g->r[kv] - rlow * rlow));
+    }
+  } else {
+    rnum = U(p);
+    int i = cdf_index(P.eps_tot + (int64_t)cell * C2D_N_VOL, C2D_N_VOL, rnum, P.eps_linear);
+    if (i < C2D_N_VOL) p.xnu = g->E_ph[i] + U(p) * (g->E_ph[i + 1] - g->E_ph[i]);
+    else p.xnu = g->E_ph[i];
+    p.wmu = 2.0 * U(p) - 1.0;
+    p.phi = 4.4e1 / 7.0 * U(p);
+    p.wmu = clampd(p.wmu, 9.9999999e-1);
+    if (p.phi > 2.0 * PI_REF) p.phi = 2.0 * PI_REF;
+    p.zpre = (jv == 1) ? g->z[1] * U(p) : g->z[jv - 1] + U(p) * (g->z[jv] - g->z[jv - 1]);
+    psi = U(p);
+    p.rpre = __builtin_sqrt(rlow * rlow + psi * (g->r[kv] * g->r[kv] - rlow * rlow));
+  }
+  p.jgpsp = bin_sp(g, P.nphtotal, p.xnu, F32(1.000001), F32(0.999999), P.nphtotal);
+  p.jgplc = bin_lc(g, P.nph_lc, p.xnu);
+  p.jgpmu = bin_mu(g, P.nmu, p.wmu);
+}
+
+/* surface packets: z_surf_calc / r_surf_calc (src/imcsurf2d_para.f:254-528).
+ * side 0 inner z-surface js, 1 outer js, 2 upper r-surface ks, 3 lower ks. */
+__device__ __forceinline__ void surf_source(const KParams& P, const Tal& T, Pkt& p, int side, int s1, int slot) {
+  const Geo* g = T.g;
+  const double lim10 = 0.9999999999;
+  const double ew = P.surf_ew[slot], tbb = P.surf_tbb[slot];
+  const int spec = P.surf_spec[slot];
+  if (side == 0) {
+    const int js = s1;
+    p.jph = js;
+    p.wmu = clampd(2.0 * U(p) - 1.0, lim10);
+    p.phi = -1.1e1 / 7.0 + 2.2e1 / 7.0 * U(p);
+    if (p.phi < -1.5707963) p.phi = -1.57079063;
+    if (p.phi > 1.5707963) p.phi = 1.5707963;
+    p.rpre = P.rmin;
+    p.zpre = (js == 1) ? g->z[1] * U(p) : g->z[js - 1] + U(p) * (g->z[js] - g->z[js - 1]);
+    p.ew = ew;
+    p.dcen = U(p) * C_LIGHT * P.dt;
+    if (tbb > 0.0) planck(P, T, p, tbb);
+    else file_sample(P, T, p, spec);
+    p.kph = 1;
+  } else if (side == 1) {
+    const int js = s1;
+    p.jph = js;
+    p.wmu = clampd(2.0 * U(p) - 1.0, lim10);
+    p.rpre = g->r[P.nr];
+    p.zpre = (js == 1) ? g->z[1] * U(p) : g->z[js - 1] + U(p) * (g->z[js] - g->z[js - 1]);
+    double x1 = U(p), x2 = U(p);
+    if (x1 < 0.5) {
+      p.phi = 1.1e1 / 7.0 + (1.1e1 / 7.0) * x2;
+      if (p.phi < 1.57079638) p.phi = 1.57079638;
+    } else {
+      p.phi = -1.1e1 / 7.0 - (1.1e1 / 7.0) * x2;
+      if (p.phi > -1.57079638) p.phi = -1.57079638;
+    }
+    p.ew = ew;
+    p.dcen = U(p) * C_LIGHT * P.dt;
+    if (tbb > 0.0) planck(P, T, p, tbb);
+    else file_sample(P, T, p, spec);
+    p.kph = P.nr;
+  } else {
+    const int ks = s1;
+    const double rlow = (ks == 1) ? P.rmin : g->r[ks - 1];
+    p.kph = ks;
+    if (side == 2) {
+      p.wmu = clampd(-U(p), lim10);
+      p.phi = 2.0 * PI_REF * U(p);
+      double psi = U(p);
+      p.zpre = g->z[P.nz];
+      p.rpre = __builtin_sqrt(rlow * rlow + psi * (g->r[ks] * g->r[ks] - rlow * rlow));
+      p.ew = ew;
+      p.dcen = U(p) * C_LIGHT * P.dt;
+      if (tbb > 0.0) planck(P, T, p, tbb);
+      else file_sample(P, T, p, spec);
+      p.jph = P.nz;
+    } else {
+      p.wmu = 9.9999999e-1;
+      p.phi = 2.0 * PI_REF * U(p);
+      double psi = U(p);
+      p.zpre = P.zmin;
+      p.rpre = __builtin_sqrt(rlow * rlow + psi * (g->r[ks] * g->r[ks] - rlow * rlow));
+      p.ew = ew;
+      if (tbb > 0.0) planck(P, T, p, tbb);
+      else file_sample(P, T, p, spec);
+      p.dcen = U(p) * C_LIGHT * P.dt;
+      p.jph = 1;
+    }
+  }
+}
+
+__device__ __forceinline__ int upper_index(const int64_t* prefix, int n, int64_t gidx) {
+  /* largest c in [0, n) with prefix[c] <= gidx */
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (prefix[mid] <= gidx) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+}  // namespace
+
+/* ------------------------------------------------------------------ */
+/* the transport kernel                                                */
+/* ------------------------------------------------------------------ */
+__global__ void __launch_bounds__(BLOCK) C2D_SFX(c2d_transport_kernel)(const KParams* __restrict__ Pg) {
+  const KParams& P = *Pg;
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  /* LDS carve-up: Geo image | cell tallies (optional) | escape tallies */
+  double* cur = lds + GEO_DOUBLES;
+  Tal T;
+  T.g = reinterpret_cast<const Geo*>(lds);
+  double* cells_lds = cur;
+  if (P.lds_cells) {
+    T.cells = cur;
+    cur += 4 * P.ncell;
+  } else {
+    T.cells = P.T + P.off.edep;
+  }
+  double* esc_lds = cur;
+  T.esc = cur;
+  cur += P.nmu * (C2D_NPHOMAX + C2D_NPHLCMAX) + 2 * P.nz + 2 * P.nr;
+  const int n_cells_lds = (int)(esc_lds - cells_lds);
+  const int n_esc = (int)(cur - esc_lds);
+  {
+    const double* gsrc = reinterpret_cast<const double*>(P.geo);
+    for (int i = tid; i < GEO_DOUBLES; i += BLOCK) lds[i] = gsrc[i];
+    for (int i = tid; i < (int)(cur - cells_lds); i += BLOCK) cells_lds[i] = 0.0;
+  }
+  __syncthreads();
+
+  Pkt p;
+  p.mode = 0; p.kap = 0; p.ctr = 0; p.key = 0; p.nflight = 0;
+  /* source save of the split1 loop (imctrk2d.f:106-123) */
+  double s_xnu = 0, s_wmu = 0, s_phi = 0, s_rpre = 0, s_zpre = 0, s_dcen = 0, s_ew = 0, s_wtmin = 0;
+  int32_t s_jph = 0, s_kph = 0, s_bins = 0;
+  uint64_t s_key = 0;
+  int32_t state = ST_IDLE, probe = 0, nscat = 0;
+  ComCache cc = {-1, -1, 0.0, 0.0};
+  LaneCnt lc = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  long long chunk_base = 0, chunk_end = 0;
+  bool exhausted = false;
+  const double twopi = 2.0 * PI_REF;
+
+  for (;;) {
+    /* ---- refill idle lanes: chunked, wave-aggregated work fetch ---- */
+    bool got = false;
+    long long item = -1;
+    if (!exhausted) {
+      unsigned long long needm = __ballot(state == ST_IDLE);
+      while (needm != 0ull) {
+        if (chunk_base >= chunk_end) {
+          unsigned long long nb = 0;
+          if (lane == 0) nb = atomicAdd(P.work_counter, (unsigned long long)CHUNK);
+          nb = rfl64(nb);
+          if ((long long)nb >= P.n_items) { exhausted = true; break; }
+          chunk_base = (long long)nb;
+          chunk_end = chunk_base + CHUNK < P.n_items ? chunk_base + CHUNK : P.n_items;
+        }
+        const long long avail = chunk_end - chunk_base;
+        const unsigned long long lt = (lane == 0) ? 0ull : (needm & ((~0ull) >> (64 - lane)));
+        const long long rank = __popcll(lt);
+        const long long nneed = __popcll(needm);
+        if (((needm >> lane) & 1ull) && rank < avail) {
+          item = chunk_base + rank;
+          got = true;
+        }
+        chunk_base += (nneed < avail ? nneed : avail);
+        needm = __ballot(state == ST_IDLE && !got);
+      }
+    }
+    if (got) {
+      /* ---- initialise the work item ---- */
+      int start_source = 0;
+      if (P.gen == 0) {
+        if (item < P.n_cens_items) {
+          const int64_t i = item;
+          p.rpre = P.cin.rpre[i]; p.zpre = P.cin.zpre[i]; p.wmu = P.cin.wmu[i];
+          p.phi = P.cin.phi[i]; p.ew = P.cin.ew[i]; p.xnu = P.cin.xnu[i];
+          const uint32_t jk = P.cin.jk[i], bn = P.cin.bins[i];
+          p.jph = (int32_t)(jk >> 16); p.kph = (int32_t)(jk & 0xffffu);
+          p.jgpsp = (int32_t)(bn & 0xffu); p.jgplc = (int32_t)((bn >> 8) & 0xffu);
+          p.jgpmu = (int32_t)((bn >> 16) & 0xffu);
+          p.key = P.cin.key[i]; p.ctr = 0;
+          p.dcen = P.cdt;                                    /* imcfield2d.f:117 */
+          p.wmu = clampd(p.wmu, 0.99999999);
+          p.kap = 0;
+          start_source = 1;
+        } else if (item < P.n_cens_items + P.n_vol_items) {
+          const int64_t gidx = (item - P.n_cens_items) * P.world + P.rank;
+          const int cell = upper_index(P.vol_prefix, P.ncell, gidx);
+          const int64_t n = gidx - P.vol_prefix[cell];
+          p.key = c2d_derive(P.step_key, C2D_TAG_VOL, (uint32_t)n, (uint32_t)cell);
+          p.ctr = 0;
+          p.kap = 0;
+          vol_source(P, T, p, cell / P.nr + 1, cell % P.nr + 1);
+          start_source = 1;
+        } else {
+          const int64_t gidx = (item - P.n_cens_items - P.n_vol_items) * P.world + P.rank;
+          const int slot = upper_index(P.surf_prefix, P.nslot, gidx);
+          const int64_t n = gidx - P.surf_prefix[slot];
+          int side, s1;
+          if (slot < 2 * P.nz) { side = slot & 1; s1 = slot / 2 + 1; }
+          else { side = 2 + ((slot - 2 * P.nz) & 1); s1 = (slot - 2 * P.nz) / 2 + 1; }
+          p.key = c2d_derive(P.step_key, C2D_TAG_SURF + (uint32_t)side, (uint32_t)n,
+                             (uint32_t)(s1 - 1));
+          p.ctr = 0;
+          p.kap = 1;
+          surf_source(P, T, p, side, s1, slot);
+          start_source = 1;
+        }
+      } else {
+        const int64_t n2items = P.n2_in * P.split2;
+        if (item < n2items) {
+          /* split2 copy ii of a collision (imctrk2d.f:611-679) */
+          const ScatRec rec = P.q2_in[item / P.split2];
+          const uint32_t ii = (uint32_t)(item % P.split2);
+          load_rec(p, rec);
+          const double ewcsv = rec.ew / P.split2;
+          p.ew = ewcsv;
+          p.key = c2d_derive(rec.key, C2D_TAG_SCAT2, ii, rec.ctr);
+          p.ctr = 0;
+          double ewold = p.ew;
+          int i_gam = compb2d(P, T, p, lc);
+          if (p.ew > ewold * P.split2 * P.split1 * P.spl3_trg) {
+            /* third split (imctrk2d.f:631-661): resampled in the next generation */
+            ScatRec r3 = rec;
+            r3.key = p.key;
+            r3.ctr = p.ctr;
+            push_scat(P, P.q3_out, P.n3_out, r3);
+          } else {
+            const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
+            atomicAdd(&T_EDEP(P, T)[cell], p.ew - ewold);
+            atomicAdd(&P.T[P.off.E_IC + i_gam], p.ew - ewold);
+            if (p.phi > twopi) p.phi = p.phi - twopi;
+            p.mode = 1;
+            p.wtmin = 1.0e-10 * p.ew;
+            p.nflight = 0;
+            cc.cell0 = -1; cc.cell1 = -1;
+            state = ST_TRACK;
+          }
+        } else {
+          /* split3 copy ii2 (imctrk2d.f:633-661) */
+          const int64_t it3 = item - n2items;
+          const ScatRec rec = P.q3_in[it3 / P.split3];
+          const uint32_t ii2 = (uint32_t)(it3 % P.split3);
+          const double ewcsv = rec.ew / P.split2;
+          const double ewold = ewcsv / P.split3;
+          p.key = c2d_derive(rec.key, C2D_TAG_SCAT3, ii2, rec.ctr);
+          p.ctr = 0;
+          int i_gam, guard = 0;
+          do {
+            load_rec(p, rec);
+            p.ew = ewcsv / P.split3;
+            i_gam = compb2d(P, T, p, lc);
+            if (++guard > MAX_REJECT) { lc.aborted++; break; }
+          } while (p.ew <= ewold * P.split2 * P.split1 * P.spl3_trg);
+          const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
+          atomicAdd(&T_EDEP(P, T)[cell], p.ew - ewold);
+          atomicAdd(&P.T[P.off.E_IC + i_gam], p.ew - ewold);
+          if (p.phi > twopi) p.phi = p.phi - twopi;
+          p.mode = 1;
+          p.wtmin = 1.0e-10 * p.ew;
+          p.nflight = 0;
+          cc.cell0 = -1; cc.cell1 = -1;
+          state = ST_TRACK;
+        }
+      }
+      if (start_source) {
+        /* imctrk2d(-1) entry (imctrk2d.f:91,106-123) */
+        lc.sources++;
+        s_key = p.key;
+        s_wtmin = 1.0e-10 * p.ew;
+        s_ew = p.ew / P.split1;
+        s_xnu = p.xnu; s_wmu = p.wmu; s_phi = p.phi; s_rpre = p.rpre; s_zpre = p.zpre;
+        s_dcen = p.dcen; s_jph = p.jph; s_kph = p.kph;
+        s_bins = p.jgpsp | (p.jgplc << 8) | (p.jgpmu << 16);
+        p.ew = s_ew;
+        p.wtmin = s_wtmin;
+        p.mode = -1;
+        p.key = c2d_derive(s_key, C2D_TAG_PROBE, 0u, 0u);
+        p.ctr = 0;
+        p.nflight = 0;
+        probe = 0;
+        nscat = 0;
+        cc.cell0 = -1; cc.cell1 = -1;
+        state = ST_PROBE;
+      }
+    }
+    if (exhausted && __ballot(state != ST_IDLE) == 0ull) break;
+    if (state != ST_IDLE) {
+      const int out = flight(P, T, p, cc, lc);
+      if (out != FL_CONT) {
+        if (out == FL_COLLIDE) {
+          push_scat(P, P.q2_out, P.n2_out, make_rec(p, p.key, p.ctr));
+          if (state == ST_PROBE) nscat++;
+        }
+        if (state == ST_PROBE) {
+          probe++;
+          if (probe < P.split1 || P.split1 - nscat > 0) {
+            p.xnu = s_xnu; p.wmu = s_wmu; p.phi = s_phi; p.rpre = s_rpre; p.zpre = s_zpre;
+            p.dcen = s_dcen; p.jph = s_jph; p.kph = s_kph;
+            p.jgpsp = s_bins & 0xff; p.jgplc = (s_bins >> 8) & 0xff; p.jgpmu = (s_bins >> 16) & 0xff;
+            p.ctr = 0;
+            p.nflight = 0;
+            if (probe < P.split1) {
+              p.ew = s_ew;
+              p.wtmin = s_wtmin;
+              p.key = c2d_derive(s_key, C2D_TAG_PROBE, (uint32_t)probe, 0u);
+            } else {
+              /* recombined unscattered copies, imctrk2d(0) (imctrk2d.f:690-704) */
+              p.ew = (double)(P.split1 - nscat) * s_ew;
+              p.wtmin = 1.0e-10 * p.ew;
+              p.mode = 0;
+              p.key = c2d_derive(s_key, C2D_TAG_RECOMB, 0u, 0u);
+              state = ST_TRACK;
+            }
+          } else {
+            state = ST_IDLE;
+          }
+        } else {
+          state = ST_IDLE;
+        }
+      }
+    }
+  }
+
+  /* ---- flush: LDS tallies and counters ---- */
+  __syncthreads();
+  if (P.lds_cells) {
+    double* gdst = P.T + P.off.edep;    /* edep, prdep, ecens, npcen are contiguous */
+    for (int i = tid; i < n_cells_lds; i += BLOCK) {
+      double v = cells_lds[i];
+      if (v != 0.0) atomicAdd(&gdst[i], v);
+    }
+  }
+  {
+    double* gdst = P.T + P.off.fout;    /* fout, edout, erlki, erlko, erlku, erlkl */
+    for (int i = tid; i < n_esc; i += BLOCK) {
+      double v = esc_lds[i];
+      if (v != 0.0) atomicAdd(&gdst[i], v);
+    }
+  }
+  const uint32_t c0 = wave_sum(lc.steps), c1 = wave_sum(lc.escapes), c2 = wave_sum(lc.census),
+                 c3 = wave_sum(lc.collide), c4 = wave_sum(lc.killed), c5 = wave_sum(lc.sources),
+                 c6 = wave_sum(lc.compb), c7 = wave_sum(lc.events), c8 = wave_sum(lc.aborted);
+  if (lane == 0) {
+    if (c0) atomicAdd(&P.cnt[C2D_CNT_STEPS], (unsigned long long)c0);
+    if (c1) atomicAdd(&P.cnt[C2D_CNT_ESCAPES], (unsigned long long)c1);
+    if (c2) atomicAdd(&P.cnt[C2D_CNT_CENSUS], (unsigned long long)c2);
+    if (c3) atomicAdd(&P.cnt[C2D_CNT_COLLIDE], (unsigned long long)c3);
+    if (c4) atomicAdd(&P.cnt[C2D_CNT_KILLED], (unsigned long long)c4);
+    if (c5) atomicAdd(&P.cnt[C2D_CNT_SOURCES], (unsigned long long)c5);
+    if (c6) atomicAdd(&P.cnt[C2D_CNT_COMPB], (unsigned long long)c6);
+    if (c7) atomicAdd(&P.cnt[C2D_CNT_EVENTS], (unsigned long long)c7);
+    if (c8) atomicAdd(&P.cnt[C2D_CNT_ABORTED], (unsigned long long)c8);
+  }
+}
+
+#if C2D_TABLE_COMTOT
+/* Per-step comtot table: tab[cell][g] = sum_i sigma_E(i, x_g) f_nt(cell,i) dg_i
+ * (src/comtot2d.f:220-241 without the n_e factor).  sigma_E(i, x_g) does not
+ * depend on the cell, so it is evaluated once per run into S[g][i]
+ * (c2d_comtab_sigma) and the per-step table is the small GEMM
+ * tab = W * S^T with W[cell][i] = f_nt(cell,i) * dg_i. */
+__global__ void __launch_bounds__(256) c2d_comtab_sigma(const double* gnt, double* S) {
+  const int gi = blockIdx.x;                 /* grid point */
+  const double du = (C2D_COMTAB_U1 - C2D_COMTAB_U0) / (double)(C2D_COMTAB_N - 1);
+  const double x = c2d_exp(C2D_COMTAB_U0 + du * gi) / EMASSKEV;
+  for (int i = threadIdx.x; i < C2D_NUM_NT - 1; i += blockDim.x)
+    S[(int64_t)gi * C2D_NUM_NT + i] = sigma_E_bin(gnt[i], x);
+  if (threadIdx.x == 0) S[(int64_t)gi * C2D_NUM_NT + C2D_NUM_NT - 1] = 0.0;
+}
+
+/* one 64x64 output tile per 256-thread block; K = 200 staged through LDS */
+__global__ void __launch_bounds__(256) c2d_comtab_gemm(const double* f_nt, const double* gnt,
+                                                       const double* S, double* tab, int ncell) {
+  __shared__ double Ws[64][41];
+  __shared__ double Ss[64][41];
+  const int c0 = blockIdx.y * 64, g0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  double acc[4][4] = {};
+  for (int k0 = 0; k0 < C2D_NUM_NT; k0 += 40) {
+    for (int e = threadIdx.x; e < 64 * 40; e += 256) {
+      const int rr = e / 40, kk = e % 40, k = k0 + kk;
+      const int c = c0 + rr, gg = g0 + rr;
+      double w = 0.0;
+      if (c < ncell && k < C2D_NUM_NT - 1) w = f_nt[(int64_t)c * C2D_NUM_NT + k] * (gnt[k + 1] - gnt[k]);
+      Ws[rr][kk] = w;
+      Ss[rr][kk] = (gg < C2D_COMTAB_N && k < C2D_NUM_NT) ? S[(int64_t)gg * C2D_NUM_NT + k] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int kk = 0; kk < 40; kk++) {
+      double a[4], b[4];
+#pragma unroll
+      for (int m = 0; m < 4; m++) a[m] = Ws[ty + 16 * m][kk];
+#pragma unroll
+      for (int n = 0; n < 4; n++) b[n] = Ss[tx + 16 * n][kk];
+#pragma unroll
+      for (int m = 0; m < 4; m++)
+#pragma unroll
+        for (int n = 0; n < 4; n++) acc[m][n] += a[m] * b[n];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int m = 0; m < 4; m++)
+#pragma unroll
+    for (int n = 0; n < 4; n++) {
+      const int c = c0 + ty + 16 * m, gg = g0 + tx + 16 * n;
+      if (c < ncell && gg < C2D_COMTAB_N) tab[(int64_t)c * C2D_COMTAB_N + gg] = acc[m][n];
+    }
+}
+#endif
+
+}  // namespace c2d
+
+/* ------------------------------------------------------------------ */
+/* launchers (called from capi.cpp)                                    */
+/* ------------------------------------------------------------------ */
+extern "C" int C2D_SFX(c2d_launch_transport)(const c2d::KParams* P_dev, int grid, size_t lds_bytes,
+                                             hipStream_t stream) {
+  hipLaunchKernelGGL(C2D_SFX(c2d::c2d_transport_kernel), dim3(grid), dim3(c2d::BLOCK), lds_bytes,
+                     stream, P_dev);
+  return (int)hipGetLastError();
+}
+
+extern "C" int C2D_SFX(c2d_transport_attrs)(int* block, int* max_lds) {
+  *block = c2d::BLOCK;
+  hipFuncAttributes a;
+  hipError_t e = hipFuncGetAttributes(&a, (const void*)C2D_SFX(c2d::c2d_transport_kernel));
+  *max_lds = (int)a.maxDynamicSharedSizeBytes;
+  return (int)e;
+}
+
+#if C2D_TABLE_COMTOT
+extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t stream) {
+  hipLaunchKernelGGL(c2d::c2d_comtab_sigma, dim3(C2D_COMTAB_N), dim3(256), 0, stream, gnt, S);
+  return (int)hipGetLastError();
+}
+extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
+                                      double* tab, int ncell, hipStream_t stream) {
+  dim3 grid(C2D_COMTAB_N / 64, (ncell + 63) / 64);
+  hipLaunchKernelGGL(c2d::c2d_comtab_gemm, grid, dim3(256), 0, stream, f_nt, gnt, S, tab, ncell);
+  return (int)hipGetLastError();
+}
+#endif

@@ -1,0 +1,228 @@
+"""Host-side mirror of the reference's per-step transport interface.
+
+The reference runs, each Monte-Carlo time step (src/xec2d.f:67-87):
+
+    imcgen2d   -> budgets + tables          (host side here: StepInputs)
+    imcfield2d -> census transport          \\
+    imcvol2d   -> volume-source transport    > Engine.transport_step()
+    imcsurf2d  -> surface-source transport  /   (one C-ABI call, c2d_transport_step)
+    imcredist  -> census rebalance          (not needed: census stays on its GPU)
+    xec_add / graphics_collect / cens_add_up -> Engine.allreduce_tallies()
+
+`Engine` owns one c2d context (one GPU).  Errors raise `C2DError` carrying
+the library's message (the reference `stop`s instead).  The HIP library is
+required: there is no CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+
+from . import abi
+
+LIB_PATH = Path(__file__).resolve().parent / "libcompton2d.so"
+_lib = None
+
+
+class C2DError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__("%s (%d): %s" % (abi.ERRORS.get(code, "C2D_E_?"), code, msg))
+        self.code = code
+
+
+def load_library(path: Optional[Path] = None) -> C.CDLL:
+    """Load libcompton2d.so (built by `make -C compton2d_amd/csrc`); raise if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise RuntimeError(
+            "compton2d_amd: HIP library %s is missing; build it with "
+            "`make -C compton2d_amd/csrc` (hipcc --offload-arch=gfx950)" % p)
+    lib = C.CDLL(str(p))
+    vp = C.c_void_p
+    lib.c2d_version.restype = C.c_char_p
+    lib.c2d_init.restype = C.c_int
+    lib.c2d_init.argtypes = [C.POINTER(abi.Config), C.POINTER(vp)]
+    lib.c2d_finalize.argtypes = [vp]
+    lib.c2d_last_error.restype = C.c_char_p
+    lib.c2d_last_error.argtypes = [vp]
+    for fn in ("c2d_transport_step", "c2d_set_step"):
+        getattr(lib, fn).restype = C.c_int
+        getattr(lib, fn).argtypes = [vp, C.POINTER(abi.StepIn)]
+    lib.c2d_set_clock.restype = C.c_int
+    lib.c2d_set_clock.argtypes = [vp, C.c_int32, C.c_double, C.c_double]
+    lib.c2d_run_step.restype = C.c_int
+    lib.c2d_run_step.argtypes = [vp]
+    lib.c2d_set_tally_buffer.restype = C.c_int
+    lib.c2d_set_tally_buffer.argtypes = [vp, C.c_void_p]
+    lib.c2d_tally_layout_get.restype = C.c_int
+    lib.c2d_tally_layout_get.argtypes = [vp, C.POINTER(abi.TallyLayout)]
+    lib.c2d_tally_device_ptr.restype = C.c_void_p
+    lib.c2d_tally_device_ptr.argtypes = [vp]
+    lib.c2d_tally_download.restype = C.c_int
+    lib.c2d_tally_download.argtypes = [vp, C.POINTER(C.c_double), C.c_int64]
+    lib.c2d_events.restype = C.c_int
+    lib.c2d_events.argtypes = [vp, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_int64)]
+    lib.c2d_census_count.restype = C.c_int
+    lib.c2d_census_count.argtypes = [vp, C.POINTER(C.c_int64)]
+    lib.c2d_census_export.restype = C.c_int
+    lib.c2d_census_export.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32),
+                                      C.POINTER(C.c_uint64), C.c_int64, C.POINTER(C.c_int64)]
+    lib.c2d_census_import.restype = C.c_int
+    lib.c2d_census_import.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32),
+                                      C.POINTER(C.c_uint64), C.c_int64]
+    lib.c2d_fp_tridag.restype = C.c_int
+    lib.c2d_fp_tridag.argtypes = [vp, C.POINTER(abi.FpIn), C.POINTER(C.c_double)]
+    lib.c2d_selftest_math.restype = C.c_int
+    lib.c2d_selftest_math.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double),
+                                      C.POINTER(C.c_double), C.c_int64]
+    lib.c2d_last_kernel_ms.restype = C.c_int
+    lib.c2d_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                       C.POINTER(C.c_int32)]
+    if path is None:
+        _lib = lib
+    return lib
+
+
+class Engine:
+    """One GPU's transport context (c2d_ctx)."""
+
+    def __init__(self, grid: abi.GridConfig, lib_path: Optional[Path] = None):
+        self.lib = load_library(lib_path)
+        self.grid = grid
+        self._cfg = grid.to_ctypes()
+        ctx = C.c_void_p()
+        rc = self.lib.c2d_init(C.byref(self._cfg), C.byref(ctx))
+        self.ctx = ctx
+        if rc != 0:
+            msg = self.lib.c2d_last_error(ctx).decode() if ctx.value else "c2d_init rejected config"
+            if ctx.value:
+                self.lib.c2d_finalize(ctx)
+            self.ctx = None
+            raise C2DError(rc, msg)
+        L = abi.TallyLayout()
+        self._check(self.lib.c2d_tally_layout_get(self.ctx, C.byref(L)))
+        self.layout = L
+        self.nz, self.nr, self.nmu = grid.nz, grid.nr, int(np.asarray(grid.mu).size)
+        self._tally_tensor = None
+
+    # -- lifecycle -------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "ctx", None):
+            self.lib.c2d_finalize(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int) -> None:
+        if rc != 0:
+            raise C2DError(rc, self.lib.c2d_last_error(self.ctx).decode())
+
+    # -- the step ------------------------------------------------------------
+    def set_step(self, si: abi.StepInputs) -> None:
+        self._si = si.to_ctypes()
+        self._check(self.lib.c2d_set_step(self.ctx, C.byref(self._si)))
+
+    def set_clock(self, ncycle: int, time: float, dt: float) -> None:
+        self._check(self.lib.c2d_set_clock(self.ctx, int(ncycle), float(time), float(dt)))
+
+    def run_step(self) -> None:
+        self._check(self.lib.c2d_run_step(self.ctx))
+
+    def transport_step(self, si: abi.StepInputs) -> None:
+        """imcfield2d + imcvol2d + imcsurf2d of one time step."""
+        self.set_step(si)
+        self.run_step()
+
+    # -- tallies -------------------------------------------------------------
+    def use_tally_tensor(self, tensor) -> None:
+        """Write tallies into a caller-owned device tensor (float64, >= layout.total)."""
+        assert tensor.dtype.itemsize == 8 and tensor.numel() >= self.layout.total
+        self._tally_tensor = tensor
+        self._check(self.lib.c2d_set_tally_buffer(self.ctx, C.c_void_p(tensor.data_ptr())))
+
+    def tallies_raw(self) -> np.ndarray:
+        out = np.zeros(self.layout.total, np.float64)
+        self._check(self.lib.c2d_tally_download(
+            self.ctx, out.ctypes.data_as(C.POINTER(C.c_double)), out.size))
+        return out
+
+    def tallies(self) -> dict:
+        return abi.split_tallies(self.tallies_raw(), self.nz, self.nr, self.nmu)
+
+    def events(self) -> np.ndarray:
+        n = C.c_int64()
+        self._check(self.lib.c2d_events(self.ctx, None, 0, C.byref(n)))
+        out = np.zeros((max(n.value, 1), abi.EVENT_WORDS))
+        self._check(self.lib.c2d_events(self.ctx, out.ctypes.data_as(C.POINTER(C.c_double)),
+                                        n.value, C.byref(n)))
+        return out[:n.value]
+
+    def census_count(self) -> int:
+        n = C.c_int64()
+        self._check(self.lib.c2d_census_count(self.ctx, C.byref(n)))
+        return n.value
+
+    def census(self):
+        n = self.census_count()
+        d6 = np.zeros((max(n, 1), 6))
+        i5 = np.zeros((max(n, 1), 5), np.int32)
+        keys = np.zeros(max(n, 1), np.uint64)
+        m = C.c_int64()
+        self._check(self.lib.c2d_census_export(
+            self.ctx, d6.ctypes.data_as(C.POINTER(C.c_double)),
+            i5.ctypes.data_as(C.POINTER(C.c_int32)), keys.ctypes.data_as(C.POINTER(C.c_uint64)),
+            n, C.byref(m)))
+        return d6[:n], i5[:n], keys[:n]
+
+    def import_census(self, d6, i5, keys) -> None:
+        d6 = np.ascontiguousarray(d6, np.float64)
+        i5 = np.ascontiguousarray(i5, np.int32)
+        keys = np.ascontiguousarray(keys, np.uint64)
+        self._check(self.lib.c2d_census_import(
+            self.ctx, d6.ctypes.data_as(C.POINTER(C.c_double)),
+            i5.ctypes.data_as(C.POINTER(C.c_int32)), keys.ctypes.data_as(C.POINTER(C.c_uint64)),
+            len(keys)))
+
+    def last_kernel_ms(self):
+        g0, al, nl = C.c_double(), C.c_double(), C.c_int32()
+        self._check(self.lib.c2d_last_kernel_ms(self.ctx, C.byref(g0), C.byref(al), C.byref(nl)))
+        return g0.value, al.value, nl.value
+
+    # -- Fokker-Planck -------------------------------------------------------
+    def fp_tridag(self, a, b, c, r, x0=None) -> np.ndarray:
+        """Batched tridag (src/update2d.f:2476-2518); arrays [ncell, nt]."""
+        a, b, c, r = (np.ascontiguousarray(x, np.float64) for x in (a, b, c, r))
+        ncell, nt = a.shape
+        x = np.zeros_like(a) if x0 is None else np.array(x0, np.float64, copy=True)
+        fin = abi.FpIn(ncell, a.ctypes.data_as(abi.PD), b.ctypes.data_as(abi.PD),
+                       c.ctypes.data_as(abi.PD), r.ctypes.data_as(abi.PD), nt)
+        self._check(self.lib.c2d_fp_tridag(self.ctx, C.byref(fin), x.ctypes.data_as(abi.PD)))
+        return x
+
+
+def device_math(fn: int, x: np.ndarray, device: int = 0) -> np.ndarray:
+    """Evaluate c2d_math function `fn` on the GPU (c2d_selftest_math)."""
+    lib = load_library()
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.zeros_like(x)
+    rc = lib.c2d_selftest_math(device, fn, x.ctypes.data_as(abi.PD), y.ctypes.data_as(abi.PD),
+                               x.size)
+    if rc != 0:
+        raise C2DError(rc, "c2d_selftest_math failed")
+    return y

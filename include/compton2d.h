@@ -162,6 +162,7 @@ typedef struct c2d_tally_layout {
 #define C2D_CNT_COMPB      6   /* compb2d calls                                    */
 #define C2D_CNT_EVENTS     7   /* event-file records written                      */
 #define C2D_CNT_GENS       8   /* scatter generations launched                    */
+#define C2D_CNT_ABORTED    9   /* packets stopped by a safety cap (must stay 0)   */
 #define C2D_NCOUNTERS      16
 
 static inline void c2d_tally_layout_for(int32_t nz, int32_t nr, int32_t nmu,
@@ -212,8 +213,21 @@ void c2d_finalize(c2d_ctx* ctx);
 const char* c2d_last_error(c2d_ctx* ctx);
 
 /* One MC time step: census + volume + surface transport, all scatter
- * generations, tallies into the fused device buffer.  Synchronous. */
+ * generations, tallies into the fused device buffer.  Synchronous.
+ * Equivalent to c2d_set_step followed by c2d_run_step. */
 int  c2d_transport_step(c2d_ctx* ctx, const c2d_step_in* in);
+
+/* Upload the per-step tables (what imcgen2d/volume_em/file_sp produce) and
+ * the clock; rebuilds the comtot table in C2D_COMTOT_TABLE mode. */
+int  c2d_set_step(c2d_ctx* ctx, const c2d_step_in* in);
+/* Advance the clock only (tables unchanged, e.g. T_const=1 runs). */
+int  c2d_set_clock(c2d_ctx* ctx, int32_t ncycle, double time, double dt);
+/* Transport with the tables of the last c2d_set_step. */
+int  c2d_run_step(c2d_ctx* ctx);
+/* Use caller-owned device memory (>= layout.total doubles on the context's
+ * device) as the fused tally buffer, e.g. a torch tensor that is then
+ * all-reduced over RCCL in place.  NULL restores the internal buffer. */
+int  c2d_set_tally_buffer(c2d_ctx* ctx, double* device_ptr);
 
 int  c2d_tally_layout_get(c2d_ctx* ctx, c2d_tally_layout* out);
 /* Device pointer of the fused tally buffer (layout above), valid until the
@@ -240,6 +254,11 @@ int  c2d_fp_tridag(c2d_ctx* ctx, const c2d_fp_in* in, double* x);
  * milliseconds and launches, measured with HIP events on the library's
  * own stream. */
 int  c2d_last_kernel_ms(c2d_ctx* ctx, double* gen0_ms, double* all_ms, int32_t* launches);
+
+/* Diagnostics: evaluate the transport kernels' elementary functions on the
+ * device (fn 0 log, 1 exp, 2 cos, 3 acos, 4 cbrt-by-pow, 5 sqrt, 6 x/3,
+ * 7 Philox draw with key=x, counter=index) for bit-parity checks. */
+int  c2d_selftest_math(int device, int fn, const double* x, double* y, int64_t n);
 
 #ifdef __cplusplus
 }

@@ -308,6 +308,7 @@ typedef struct c2o_ctx {
   int split1, split2, split3, spl3_trg;
   int spec_switch, cr_sent, pair_switch, kappa_lag, rand_switch;
   int rng_mode, h4_stale;
+  int rank, world;              /* lineage-sharded sources (global index % world == rank) */
   uint64_t seed;
   double t_bound_last;
   fibstate fs;
@@ -1210,6 +1211,8 @@ c2o_ctx* c2o_create(const c2d_config* cfg, int rng_mode, int rand_switch, int32_
   g_ran1_seed = rseed;
   c->h4_stale = h4_stale;
   c->seed = cfg->seed;
+  c->rank = cfg->world > 1 ? cfg->rank : 0;
+  c->world = cfg->world > 1 ? cfg->world : 1;
   int64_t nc = c->ncell;
   c->kappa = (double*)calloc(nc * C2D_N_VOL, sizeof(double));
   c->kappa_prev = (double*)calloc(nc * C2D_N_VOL, sizeof(double));
@@ -1313,6 +1316,7 @@ int c2o_step(c2o_ctx* c, const c2d_step_in* in) {
     if (c->err) return c->err;
   }
   /* volume (vol_calc) */
+  int64_t vol_global = 0, surf_global = 0;
   int32_t seeds_job[C2D_MAXZONE * C2D_MAXZONE];
   memcpy(seeds_job, c->seeds, sizeof(int32_t) * c->ncell);
   for (int jv = 1; jv <= c->nz; jv++)
@@ -1324,8 +1328,10 @@ int c2o_step(c2o_ctx* c, const c2d_step_in* in) {
       double f_th, f_inn, f_out, f_up;
       vol_zone_fractions(c, jv, kv, &f_th, &f_inn, &f_out, &f_up);
       for (int n = 0; n < more; n++) {
+        int64_t gidx = vol_global++;
         rng_t g = g0;
         if (c->rng_mode == C2O_RNG_LINEAGE) {
+          if (gidx % c->world != c->rank) continue;
           g.key = c2d_derive(c->step_key, C2D_TAG_VOL, (uint32_t)n, (uint32_t)cell);
           g.ctr = 0;
         }
@@ -1341,8 +1347,10 @@ int c2o_step(c2o_ctx* c, const c2d_step_in* in) {
       const int32_t* ns = side ? in->nsurfo : in->nsurfi;
       int cnt = ns ? ns[js - 1] : 0;
       for (int n = 0; n < cnt; n++) {
+        int64_t gidx = surf_global++;
         rng_t g = g0;
         if (c->rng_mode == C2O_RNG_LINEAGE) {
+          if (gidx % c->world != c->rank) continue;
           g.key = c2d_derive(c->step_key, C2D_TAG_SURF + side, (uint32_t)n, (uint32_t)(js - 1));
           g.ctr = 0;
         }
@@ -1357,8 +1365,10 @@ int c2o_step(c2o_ctx* c, const c2d_step_in* in) {
       const int32_t* ns = side ? in->nsurfl : in->nsurfu;
       int cnt = ns ? ns[ks - 1] : 0;
       for (int n = 0; n < cnt; n++) {
+        int64_t gidx = surf_global++;
         rng_t g = g0;
         if (c->rng_mode == C2O_RNG_LINEAGE) {
+          if (gidx % c->world != c->rank) continue;
           g.key = c2d_derive(c->step_key, C2D_TAG_SURF + 2 + side, (uint32_t)n, (uint32_t)(ks - 1));
           g.ctr = 0;
         }
@@ -1467,4 +1477,18 @@ int c2o_is_detmath(void) {
 #else
   return 0;
 #endif
+}
+
+/* elementary functions of this build (c2d_math.h in the det flavor, glibc
+ * otherwise): fn 0 log, 1 exp, 2 cos, 3 acos, 4 pow(x, 1/3) */
+void c2o_unit_math(int fn, const double* x, double* y, int64_t n) {
+  for (int64_t i = 0; i < n; i++) {
+    switch (fn) {
+      case 0: y[i] = LOG(x[i]); break;
+      case 1: y[i] = EXP(x[i]); break;
+      case 2: y[i] = COS(x[i]); break;
+      case 3: y[i] = ACOS(x[i]); break;
+      default: y[i] = POW(x[i], 1.0 / 3.0); break;
+    }
+  }
 }

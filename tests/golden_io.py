@@ -1,0 +1,50 @@
+"""Load the golden fixtures of tests/golden/ (made by tests/golden/make_golden.py
+from the reference itself) into compton2d_amd.abi structures — TEST INFRASTRUCTURE."""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+import numpy as np
+
+from compton2d_amd import abi
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+CASES = ("ssc_tau", "ec_lower", "grid3x4")
+IN_KEYS = ("kappa_tot", "eps_tot", "eps_th", "f_nt", "Pnt", "n_e", "Eloss_th", "Eloss_tot",
+           "zsurf", "ewsv", "nsv", "nsurfi", "nsurfo", "ewsurfi", "ewsurfo", "nsurfu", "nsurfl",
+           "ewsurfu", "ewsurfl", "tbbi", "tbbo", "tbbu", "tbbl")
+
+
+class GoldenCase:
+    def __init__(self, name: str):
+        self.name = name
+        z = np.load(GOLDEN / (name + ".npz"), allow_pickle=False)
+        self.a = {k: z[k] for k in z.files}
+        self.meta = json.loads(bytes(self.a.pop("meta_json")).decode())
+        self.nsteps = self.meta["nsteps"]
+        self.nz, self.nr, self.nmu = self.meta["nz"], self.meta["nr"], self.meta["nmu"]
+
+    def grid(self, **over) -> abi.GridConfig:
+        m, a = self.meta, self.a
+        g = abi.GridConfig(
+            nz=m["nz"], nr=m["nr"], rmin=m["rmin"], zmin=m["zmin"], z=a["cfg_z"], r=a["cfg_r"],
+            E_ph=a["E_ph"], E_field=a["cfg_E_field"], gnt=a["cfg_gnt"], hu=a["cfg_hu"],
+            Elcmin=a["cfg_Elcmin"], Elcmax=a["cfg_Elcmax"], mu=a["cfg_mu"], split1=m["split1"],
+            split2=m["split2"], split3=m["split3"], spl3_trg=m["spl3_trg"],
+            spec_switch=m["spec_switch"], cr_sent=m["cr_sent"], pair_switch=m["pair_switch"])
+        for k, v in over.items():
+            setattr(g, k, v)
+        return g
+
+    def step_inputs(self, n: int) -> abi.StepInputs:
+        st = self.meta["step%d" % n]
+        spectra = []
+        if st["nfile"] >= 2 and ("out%d_E_file" % n) in self.a:
+            spectra.append(abi.SpectrumTable(*(self.a["out%d_%s" % (n, k)] for k in
+                                               ("E_file", "a1", "I_file", "F_file", "P_file"))))
+        return abi.StepInputs(ncycle=st["ncycle"], time=st["time"], dt=st["dt"], spectra=spectra,
+                              **{k: self.a["in%d_%s" % (n, k)] for k in IN_KEYS})
+
+    def out(self, n: int, key: str) -> np.ndarray:
+        return self.a["out%d_%s" % (n, key)]
