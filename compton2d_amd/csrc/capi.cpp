@@ -88,6 +88,7 @@ struct c2d_ctx {
   int eps_linear = 0;
   std::vector<double> h_stage;
   double last_g0_ms = 0.0, last_all_ms = 0.0;
+  int64_t last_g0_steps = 0;
   int last_launches = 0;
 };
 
@@ -514,9 +515,11 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
                         hipGetErrorString((hipError_t)rc));
     launches++;
     if (gen == 0) HIPCHK(c, hipEventRecord(c->ev_g0b, c->stream));
-    unsigned long long nq[2];
+    /* n2, n3 (ctl[3..4]) and the running packet-step counter (ctl[CTL_CNT]) */
+    unsigned long long nq[CTL_CNT + 1 - CTL_N2];
     HIPCHK(c, hipMemcpyAsync(nq, c->ctl + CTL_N2, sizeof nq, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (gen == 0) c->last_g0_steps = (int64_t)nq[CTL_CNT - CTL_N2];
     if ((int64_t)nq[0] > cfg.queue_capacity || (int64_t)nq[1] > cfg.queue_capacity)
       return fail(c, C2D_E_QUEUE_OVERFLOW, "scatter queue overflow in generation %d (%llu, %llu > %lld)",
                   gen, nq[0], nq[1], (long long)cfg.queue_capacity);
@@ -688,6 +691,12 @@ extern "C" int c2d_fp_tridag(c2d_ctx* c, const c2d_fp_in* in, double* x) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(x, xd, n * sizeof(double), hipMemcpyDeviceToHost));
   (void)hipFree(a); (void)hipFree(b); (void)hipFree(cc); (void)hipFree(r); (void)hipFree(xd);
+  return C2D_OK;
+}
+
+extern "C" int c2d_last_gen0_steps(c2d_ctx* c, int64_t* steps) {
+  if (!c || !steps) return C2D_E_ARG;
+  *steps = c->last_g0_steps;
   return C2D_OK;
 }
 

@@ -81,6 +81,8 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_selftest_math.restype = C.c_int
     lib.c2d_selftest_math.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double), C.c_int64]
+    lib.c2d_last_gen0_steps.restype = C.c_int
+    lib.c2d_last_gen0_steps.argtypes = [vp, C.POINTER(C.c_int64)]
     lib.c2d_last_kernel_ms.restype = C.c_int
     lib.c2d_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                        C.POINTER(C.c_int32)]
@@ -200,9 +202,15 @@ class Engine:
             len(keys)))
 
     def last_kernel_ms(self):
+        """(generation-0 kernel ms, all launches ms, launches) of the last step (HIP events)."""
         g0, al, nl = C.c_double(), C.c_double(), C.c_int32()
         self._check(self.lib.c2d_last_kernel_ms(self.ctx, C.byref(g0), C.byref(al), C.byref(nl)))
         return g0.value, al.value, nl.value
+
+    def last_gen0_steps(self) -> int:
+        n = C.c_int64()
+        self._check(self.lib.c2d_last_gen0_steps(self.ctx, C.byref(n)))
+        return n.value
 
     # -- Fokker-Planck -------------------------------------------------------
     def fp_tridag(self, a, b, c, r, x0=None) -> np.ndarray:

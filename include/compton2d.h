@@ -254,6 +254,8 @@ int  c2d_fp_tridag(c2d_ctx* ctx, const c2d_fp_in* in, double* x);
  * milliseconds and launches, measured with HIP events on the library's
  * own stream. */
 int  c2d_last_kernel_ms(c2d_ctx* ctx, double* gen0_ms, double* all_ms, int32_t* launches);
+/* Packet-steps executed by that generation-0 launch (roofline numerator). */
+int  c2d_last_gen0_steps(c2d_ctx* ctx, int64_t* steps);
 
 /* Diagnostics: evaluate the transport kernels' elementary functions on the
  * device (fn 0 log, 1 exp, 2 cos, 3 acos, 4 cbrt-by-pow, 5 sqrt, 6 x/3,
