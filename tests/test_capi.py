@@ -1,0 +1,87 @@
+"""The C-ABI library: it loads without a GPU, exports every function that
+include/compton2d.h declares, and its struct layouts match the ctypes mirror."""
+import ctypes as C
+import re
+import subprocess
+import tempfile
+from pathlib import Path
+
+import pytest
+
+from compton2d_amd import abi, engine
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "compton2d.h"
+
+
+def declared_functions():
+    txt = HEADER.read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(c2d_\w+)\s*\(", txt, flags=re.M))
+                  - {"c2d_tally_layout_for"})
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    lib = engine.load_library()
+    assert lib.c2d_version().startswith(b"compton2d_amd")
+    out = subprocess.run(["nm", "-D", "--defined-only", str(engine.LIB_PATH)],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (c2d_\w+)", out))
+    missing = [f for f in declared_functions() if f not in exported]
+    assert not missing, missing
+    assert len(declared_functions()) >= 20
+
+
+def test_struct_layouts_match_header():
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "compton2d.h"
+#define P(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  printf("c2d_config %zu\nc2d_step_in %zu\nc2d_tally_layout %zu\nc2d_fp_in %zu\nc2d_spectrum %zu\n",
+         sizeof(c2d_config), sizeof(c2d_step_in), sizeof(c2d_tally_layout), sizeof(c2d_fp_in),
+         sizeof(c2d_spectrum));
+  P(c2d_config, seed) P(c2d_config, rank) P(c2d_config, queue_capacity) P(c2d_config, mu)
+  P(c2d_step_in, kappa_tot) P(c2d_step_in, nsv) P(c2d_step_in, tbbl) P(c2d_step_in, spectra)
+  P(c2d_step_in, n_spectra) P(c2d_step_in, dt)
+  return 0;
+}
+'''
+    with tempfile.TemporaryDirectory() as d:
+        c = Path(d) / "l.c"
+        c.write_text(src)
+        exe = Path(d) / "l"
+        subprocess.run(["gcc", "-I", str(ROOT / "include"), str(c), "-o", str(exe)], check=True)
+        out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
+    got = dict(line.rsplit(" ", 1) for line in out.strip().splitlines())
+    assert int(got["c2d_config"]) == C.sizeof(abi.Config)
+    assert int(got["c2d_step_in"]) == C.sizeof(abi.StepIn)
+    assert int(got["c2d_tally_layout"]) == C.sizeof(abi.TallyLayout)
+    assert int(got["c2d_fp_in"]) == C.sizeof(abi.FpIn)
+    assert int(got["c2d_spectrum"]) == C.sizeof(abi.Spectrum)
+    for key, val in got.items():
+        if "." in key:
+            t, f = key.split(".")
+            cls = abi.Config if t == "c2d_config" else abi.StepIn
+            assert getattr(cls, f).offset == int(val), key
+
+
+def test_tally_layout_python_matches_c():
+    import oracle_lib as OL
+    from golden_io import GoldenCase
+    g = GoldenCase("grid3x4")
+    o = OL.Oracle(g.grid(), OL.RNG_LINEAGE, "det")
+    assert o.tallies().size == abi.tally_layout(3, 4, 2)["total"][0]
+    o.close()
+
+
+def test_init_fails_loudly_without_gpu():
+    """No silent CPU fallback: without a device c2d_init reports a HIP error."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from golden_io import GoldenCase
+    with pytest.raises(engine.C2DError) as e:
+        engine.Engine(GoldenCase("ssc_tau").grid())
+    assert "C2D_E_HIP" in str(e.value)

@@ -1,0 +1,96 @@
+"""Deterministic math (c2d_math.h) and the lineage RNG (c2d_rng.h) on the CPU.
+
+c2d_math restates fdlibm; it must stay within 1 ulp of glibc (2 for acos/pow)
+so that the det-math oracle is a faithful stand-in for the reference's libm.
+Philox4x32-10 is checked against the Random123 known-answer vectors.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib as OL
+from compton2d_amd import abi
+
+
+def ulp_diff(a, b):
+    ia = a.view(np.int64)
+    ib = b.view(np.int64)
+    ia = np.where(ia < 0, np.int64(-0x8000000000000000) - ia, ia)
+    ib = np.where(ib < 0, np.int64(-0x8000000000000000) - ib, ib)
+    return np.abs(ia - ib)
+
+
+@pytest.mark.parametrize("fn,lo,hi,maxulp", [
+    (0, 1e-300, 1e300, 1), (1, -700.0, 700.0, 1), (2, -7.0, 14.0, 1), (3, -1.0, 1.0, 2),
+    (4, 1e-30, 1e30, 32)])  # pow = exp(y*log x): error grows with |y ln x| (<= 23 here)
+def test_det_math_vs_glibc(fn, lo, hi, maxulp):
+    rng = np.random.default_rng(100 + fn)
+    if fn in (0, 4):
+        x = np.exp(rng.uniform(np.log(lo), np.log(hi), 100000))
+    else:
+        x = rng.uniform(lo, hi, 100000)
+    special = {0: [1.0, 2.0, 0.5, 1e-310, 5e-324, 1.0000001], 1: [0.0, 1e-20, -1e-20, 0.5, -0.34657359],
+               2: [0.0, 1e-9, np.pi / 4, 3.1415926536, 6.283185307], 3: [0.0, 0.5, -0.5, 1.0, -1.0, 0.999999999],
+               4: [1.0, 8.0, 27.0]}[fn]
+    x[:len(special)] = special
+    yd, yr = np.zeros_like(x), np.zeros_like(x)
+    OL.load("det").c2o_unit_math(fn, x.ctypes.data_as(abi.PD), yd.ctypes.data_as(abi.PD), x.size)
+    OL.load("ref").c2o_unit_math(fn, x.ctypes.data_as(abi.PD), yr.ctypes.data_as(abi.PD), x.size)
+    assert ulp_diff(yd, yr).max() <= maxulp
+
+
+def test_philox_known_answers():
+    lib = OL.load("det")
+    # Random123 kat_vectors, philox4x32-10: (ctr, key) -> out
+    kats = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+            ((0xffffffff,) * 4, (0xffffffff, 0xffffffff),
+             (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+            ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+             (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, out in kats:
+        # c2o_unit_derive(key, tag, a, b) runs philox on ctr = (a, b, tag, DERIVE_C3)
+        # -> test the raw permutation through the draw/derive wrappers is not
+        # possible for arbitrary ctr[3]; use the python restatement instead
+        got = philox_py(ctr, key)
+        assert got == out
+    # the C implementation agrees with the Python one on derive()/draw()
+    for key in (0, 1, 0x5EEDC2D, (1 << 64) - 1):
+        for (a, b, tag) in ((0, 0, 1), (7, 3, 9), (123456, 99, 11)):
+            d = lib.c2o_unit_derive(key, tag, a, b)
+            w = philox_py((a, b, tag, 0x9E3779B9), (key & 0xffffffff, key >> 32))
+            assert d == (w[1] << 32) | w[0]
+        for n in (0, 1, 17, 1 << 20):
+            u = lib.c2o_unit_philox_draw(key, n)
+            w = philox_py((n, 0, 0, 0x5EEDD1CE), (key & 0xffffffff, key >> 32))
+            x = (((w[0] << 32) | w[1]) >> 11)
+            assert u == (x + 0.5) * 2.0 ** -53
+            assert 0.0 < u < 1.0
+
+
+def philox_py(ctr, key):
+    M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+    c0, c1, c2, c3 = ctr
+    k0, k1 = key
+    m = 0xffffffff
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        hi0, lo0 = p0 >> 32, p0 & m
+        hi1, lo1 = p1 >> 32, p1 & m
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & m, lo1, (hi0 ^ c3 ^ k1) & m, lo0
+        k0 = (k0 + W0) & m
+        k1 = (k1 + W1) & m
+    return (c0, c1, c2, c3)
+
+
+def test_lineage_streams_are_distinct():
+    lib = OL.load("det")
+    keys = set()
+    base = 0x5EEDC2D
+    for tag in range(1, 12):
+        for a in range(200):
+            keys.add(lib.c2o_unit_derive(base, tag, a, 0))
+    assert len(keys) == 11 * 200
+    u = np.array([lib.c2o_unit_philox_draw(base, n) for n in range(20000)])
+    assert abs(u.mean() - 0.5) < 0.01 and abs(u.var() - 1 / 12) < 0.005
