@@ -52,6 +52,17 @@ struct ScatRec {
   uint32_t pad;
 };
 
+/* In-flight packet store, SoA: generation-0 sources sampled by
+ * c2d_source_kernel and scatter secondaries sampled by c2d_scatter_kernel,
+ * consumed by the transport kernel (coalesced: lane i reads element i). */
+struct PktSoA {
+  double* rpre; double* zpre; double* wmu; double* phi; double* ew; double* xnu; double* dcen;
+  uint32_t* jk;      /* jph << 16 | kph                                         */
+  uint32_t* bins;    /* jgpsp | jgplc << 8 | jgpmu << 16 | kap << 24            */
+  uint32_t* ctr;     /* RNG counter position of `key`                           */
+  uint64_t* key;
+};
+
 struct TallyOff {
   int64_t edep, prdep, ecens, npcen, n_field, E_IC, nelectron, fout, edout;
   int64_t erlki, erlko, erlku, erlkl, Ed_in, counters;
@@ -69,7 +80,7 @@ enum : int32_t {
 struct KParams {
   int32_t nz, nr, ncell, nphtotal, nph_lc, nmu;
   int32_t split1, split2, split3, spl3_trg, spec_switch;
-  int32_t rank, world, ncycle, gen, eps_linear;
+  int32_t rank, world, ncycle, eps_linear;
   double time, dt, rmin, zmin, cdt;
   uint64_t step_key;
   const Geo* geo;
@@ -101,22 +112,36 @@ struct KParams {
   double* ev;
   int64_t cap_ev;
   unsigned long long* n_ev;
-  /* scatter queues: in (this generation) / out (next) */
-  const ScatRec* q2_in; const ScatRec* q3_in;
-  int64_t n2_in, n3_in;
-  ScatRec* q2_out; ScatRec* q3_out;
-  unsigned long long* n2_out; unsigned long long* n3_out;
+  /* scatter queues */
   int64_t cap_q;
-  /* work items of this launch */
-  int64_t n_items, n_cens_items, n_vol_items, n_surf_items;
+  /* packet store (sources of generation 0 / secondaries of generation >= 1) */
+  PktSoA pk;
+  int64_t cap_pk;
+  /* this step's work */
+  int64_t n_cens_items, n_vol_items, n_surf_items;
   int64_t n_vol_global, n_surf_global;
-  unsigned long long* work_counter;
   /* tallies */
   double* T;
   TallyOff off;
   unsigned long long* cnt;  /* [C2D_NCOUNTERS] */
   int32_t* err;
   int32_t lds_cells;        /* 1: cell tallies privatised in LDS */
+};
+
+/* Per-launch arguments (passed by value; KParams stays constant over a step). */
+struct GenArgs {
+  const ScatRec* q2_in;            /* scatter kernel: this generation's records   */
+  const ScatRec* q3_in;
+  ScatRec* q2_out;                 /* transport kernel: collisions -> next gen    */
+  ScatRec* q3_out;                 /* scatter kernel: third splits -> next gen    */
+  unsigned long long* n2_out;
+  unsigned long long* n3_out;
+  unsigned long long* n_pk;        /* scatter: secondaries written; transport: item count */
+  unsigned long long* work_counter;
+  int64_t item_begin, item_end;    /* scatter kernel item range                   */
+  int64_t n_items;                 /* transport, generation 0: census + sources    */
+  int64_t n2_in, n3_in;
+  int32_t gen;
 };
 
 }  // namespace c2d

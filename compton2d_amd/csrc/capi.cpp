@@ -20,10 +20,16 @@
 
 using namespace c2d;
 
-extern "C" int c2d_launch_transport_exact(const KParams* P, int grid, size_t lds, hipStream_t s);
-extern "C" int c2d_launch_transport_fast(const KParams* P, int grid, size_t lds, hipStream_t s);
-extern "C" int c2d_transport_attrs_exact(int* block, int* max_lds);
-extern "C" int c2d_transport_attrs_fast(int* block, int* max_lds);
+extern "C" int c2d_launch_transport_exact(const KParams* P, const GenArgs* A, int grid, size_t lds,
+                                          hipStream_t s);
+extern "C" int c2d_launch_transport_fast(const KParams* P, const GenArgs* A, int grid, size_t lds,
+                                         hipStream_t s);
+extern "C" int c2d_launch_source_exact(const KParams* P, int grid, hipStream_t s);
+extern "C" int c2d_launch_source_fast(const KParams* P, int grid, hipStream_t s);
+extern "C" int c2d_launch_scatter_exact(const KParams* P, const GenArgs* A, int grid, hipStream_t s);
+extern "C" int c2d_launch_scatter_fast(const KParams* P, const GenArgs* A, int grid, hipStream_t s);
+extern "C" int c2d_transport_occupancy_exact(int* blocks_per_cu, size_t lds);
+extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t s);
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
                                       double* tab, int ncell, hipStream_t s);
@@ -32,8 +38,34 @@ extern "C" int c2d_launch_tridag(const double* a, const double* b, const double*
 
 namespace {
 
-enum { CTL_WORK = 0, CTL_NCOUT = 1, CTL_NEV = 2, CTL_N2 = 3, CTL_N3 = 4, CTL_CNT = 8,
+enum { CTL_WORK = 0, CTL_NCOUT = 1, CTL_NEV = 2, CTL_N2 = 3, CTL_N3 = 4, CTL_NPK = 5, CTL_CNT = 8,
        CTL_WORDS = 8 + C2D_NCOUNTERS };
+
+/* the packet store (c2d_device.hpp PktSoA) */
+struct DevPk {
+  double* d[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint32_t* jk = nullptr;
+  uint32_t* bins = nullptr;
+  uint32_t* ctr = nullptr;
+  uint64_t* key = nullptr;
+  int64_t cap = 0;
+  PktSoA soa() const {
+    PktSoA s;
+    s.rpre = d[0]; s.zpre = d[1]; s.wmu = d[2]; s.phi = d[3]; s.ew = d[4]; s.xnu = d[5];
+    s.dcen = d[6]; s.jk = jk; s.bins = bins; s.ctr = ctr; s.key = key;
+    return s;
+  }
+  void release() {
+    for (double*& p : d) { if (p) (void)hipFree(p); p = nullptr; }
+    if (jk) (void)hipFree(jk);
+    if (bins) (void)hipFree(bins);
+    if (ctr) (void)hipFree(ctr);
+    if (key) (void)hipFree(key);
+    jk = bins = ctr = nullptr;
+    key = nullptr;
+    cap = 0;
+  }
+};
 
 struct DevCensus {
   double* d[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -55,7 +87,7 @@ struct c2d_ctx {
   int nz = 0, nr = 0, ncell = 0, nmu = 0, nslot = 0;
   std::string err;
   hipStream_t stream = nullptr;
-  hipEvent_t ev_g0a = nullptr, ev_g0b = nullptr, ev_end = nullptr;
+  hipEvent_t ev_g0a = nullptr, ev_g0t = nullptr, ev_g0b = nullptr, ev_end = nullptr;
   int n_cu = 0, max_grid = 0, lds_cells = 0;
   size_t lds_bytes = 0;
   c2d_tally_layout L;
@@ -76,6 +108,7 @@ struct c2d_ctx {
   double* ev = nullptr;
   int64_t n_ev = 0;
   ScatRec *q2[2] = {nullptr, nullptr}, *q3[2] = {nullptr, nullptr};
+  DevPk pk;
   double* T = nullptr;
   double* T_own = nullptr;
   unsigned long long* ctl = nullptr;
@@ -88,6 +121,7 @@ struct c2d_ctx {
   int eps_linear = 0;
   std::vector<double> h_stage;
   double last_g0_ms = 0.0, last_all_ms = 0.0;
+  float last_src_ms = 0.f;
   int64_t last_g0_steps = 0;
   int last_launches = 0;
 };
@@ -146,6 +180,7 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(c, hipEventCreate(&c->ev_g0a));
   HIPCHK(c, hipEventCreate(&c->ev_g0b));
+  HIPCHK(c, hipEventCreate(&c->ev_g0t));
   HIPCHK(c, hipEventCreate(&c->ev_end));
   hipDeviceProp_t prop;
   HIPCHK(c, hipGetDeviceProperties(&prop, cfg->device));
@@ -218,18 +253,14 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   const size_t esc = (size_t)c->nmu * (C2D_NPHOMAX + C2D_NPHLCMAX) + 2 * c->nz + 2 * c->nr;
   c->lds_cells = (4 * nc * sizeof(double) <= 48 * 1024) ? 1 : 0;
   c->lds_bytes = sizeof(double) * (GEO_DOUBLES + (c->lds_cells ? 4 * nc : 0) + esc);
+  /* persistent grid = CUs x resident blocks per CU (VGPR- or LDS-limited,
+   * from the runtime's occupancy calculator for this kernel and LDS size) */
   int blocks_per_cu = 0;
-  const void* kfn = nullptr;
-  (void)kfn;
-  int block = 512, max_lds = 0;
-  if (cfg->comtot_mode == C2D_COMTOT_TABLE)
-    c2d_transport_attrs_fast(&block, &max_lds);
-  else
-    c2d_transport_attrs_exact(&block, &max_lds);
-  /* occupancy: VGPR-limited to 2 waves/SIMD today (8 waves = 1 block/CU); LDS
-   * allows 160 KiB / lds_bytes blocks.  Persistent grid = CUs x blocks. */
-  blocks_per_cu = std::max(1, std::min<int>(2, (int)((160 * 1024) / c->lds_bytes)));
-  c->max_grid = c->n_cu * blocks_per_cu;
+  int orc = cfg->comtot_mode == C2D_COMTOT_TABLE
+                ? c2d_transport_occupancy_fast(&blocks_per_cu, c->lds_bytes)
+                : c2d_transport_occupancy_exact(&blocks_per_cu, c->lds_bytes);
+  if (orc) return fail(c, C2D_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)orc));
+  c->max_grid = c->n_cu * std::max(1, blocks_per_cu);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return C2D_OK;
 }
@@ -252,8 +283,10 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
     if (c->cens[b].key) (void)hipFree(c->cens[b].key);
   }
   for (double* p : c->spec_bufs) (void)hipFree(p);
+  c->pk.release();
   if (c->ev_g0a) (void)hipEventDestroy(c->ev_g0a);
   if (c->ev_g0b) (void)hipEventDestroy(c->ev_g0b);
+  if (c->ev_g0t) (void)hipEventDestroy(c->ev_g0t);
   if (c->ev_end) (void)hipEventDestroy(c->ev_end);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -460,8 +493,6 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.n_cout = c->ctl + CTL_NCOUT;
   P.ev = c->ev; P.cap_ev = cfg.event_capacity; P.n_ev = c->ctl + CTL_NEV;
   P.cap_q = cfg.queue_capacity;
-  P.work_counter = c->ctl + CTL_WORK;
-  P.n2_out = c->ctl + CTL_N2; P.n3_out = c->ctl + CTL_N3;
   P.T = c->T;
   P.off.edep = c->L.edep; P.off.prdep = c->L.prdep; P.off.ecens = c->L.ecens;
   P.off.npcen = c->L.npcen; P.off.n_field = c->L.n_field; P.off.E_IC = c->L.E_IC;
@@ -480,52 +511,105 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.n_cens_items = c->n_census;
   P.n_vol_items = share(c->n_vol_global);
   P.n_surf_items = share(c->n_surf_global);
+  const int64_t n_src = P.n_vol_items + P.n_surf_items;
+  {
+    /* packet store: all of this step's sources, and secondaries in chunks */
+    const int64_t want = std::max<int64_t>(
+        n_src, std::min<int64_t>(int64_t(1) << 22,
+                                 std::max<int64_t>(65536, cfg.queue_capacity *
+                                                              std::max(cfg.split2, cfg.split3))));
+    if (c->pk.cap < want) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      c->pk.release();
+      for (int f = 0; f < 7; f++) HIPCHK(c, dalloc(&c->pk.d[f], want));
+      HIPCHK(c, dalloc(&c->pk.jk, want));
+      HIPCHK(c, dalloc(&c->pk.bins, want));
+      HIPCHK(c, dalloc(&c->pk.ctr, want));
+      HIPCHK(c, dalloc(&c->pk.key, want));
+      c->pk.cap = want;
+    }
+  }
+  P.pk = c->pk.soa();
+  P.cap_pk = c->pk.cap;
 
   HIPCHK(c, hipMemsetAsync(c->T, 0, sizeof(double) * c->L.total, c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl, 0, sizeof(unsigned long long) * CTL_WORDS, c->stream));
   HIPCHK(c, hipMemsetAsync(c->derr, 0, sizeof(int32_t), c->stream));
 
-  auto launch = cfg.comtot_mode == C2D_COMTOT_TABLE ? c2d_launch_transport_fast
-                                                    : c2d_launch_transport_exact;
-  int gen = 0, qin = 0;
+  const bool fast = cfg.comtot_mode == C2D_COMTOT_TABLE;
+  auto launch_tr = fast ? c2d_launch_transport_fast : c2d_launch_transport_exact;
+  auto launch_src = fast ? c2d_launch_source_fast : c2d_launch_source_exact;
+  auto launch_sc = fast ? c2d_launch_scatter_fast : c2d_launch_scatter_exact;
+  const int aux_grid_max = c->n_cu * 8;
+  auto aux_grid = [&](int64_t n) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(aux_grid_max, (n + 255) / 256));
+  };
+  auto tr_grid = [&](int64_t n) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(c->max_grid, (n + 511) / 512));
+  };
+  HIPCHK(c, hipMemcpyAsync(c->dP, &P, sizeof(KParams), hipMemcpyHostToDevice, c->stream));
+  int gen = 0, qin = 0, launches = 0;
   int64_t n2 = 0, n3 = 0;
-  int launches = 0;
-  for (;;) {
-    P.gen = gen;
-    if (gen == 0) {
-      P.n_items = P.n_cens_items + P.n_vol_items + P.n_surf_items;
-      P.q2_in = nullptr; P.q3_in = nullptr; P.n2_in = 0; P.n3_in = 0;
-    } else {
-      P.n2_in = n2; P.n3_in = n3;
-      P.q2_in = c->q2[qin]; P.q3_in = c->q3[qin];
-      P.n_items = n2 * cfg.split2 + n3 * cfg.split3;
+  unsigned long long nq[CTL_CNT + 1 - CTL_N2];
+  /* ---- generation 0: census + sampled sources ---- */
+  {
+    HIPCHK(c, hipEventRecord(c->ev_g0a, c->stream));
+    if (n_src > 0) {
+      int rc = launch_src(c->dP, aux_grid(n_src), c->stream);
+      if (rc) return fail(c, C2D_E_HIP, "source launch: %s", hipGetErrorString((hipError_t)rc));
+      launches++;
     }
-    P.q2_out = c->q2[1 - qin];
-    P.q3_out = c->q3[1 - qin];
-    if (P.n_items <= 0) break;
-    HIPCHK(c, hipMemcpyAsync(c->dP, &P, sizeof(KParams), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->ctl + CTL_WORK, 0, sizeof(unsigned long long), c->stream));
-    HIPCHK(c, hipMemsetAsync(c->ctl + CTL_N2, 0, 2 * sizeof(unsigned long long), c->stream));
-    const int64_t waves = (P.n_items + 63) / 64;
-    const int64_t blocks = (waves + 7) / 8;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->max_grid, blocks));
-    if (gen == 0) HIPCHK(c, hipEventRecord(c->ev_g0a, c->stream));
-    int rc = launch(c->dP, grid, c->lds_bytes, c->stream);
-    if (rc) return fail(c, C2D_E_HIP, "transport launch (gen %d): %s", gen,
-                        hipGetErrorString((hipError_t)rc));
-    launches++;
-    if (gen == 0) HIPCHK(c, hipEventRecord(c->ev_g0b, c->stream));
-    /* n2, n3 (ctl[3..4]) and the running packet-step counter (ctl[CTL_CNT]) */
-    unsigned long long nq[CTL_CNT + 1 - CTL_N2];
+    GenArgs A = {};
+    A.gen = 0;
+    A.n_items = P.n_cens_items + n_src;
+    A.q2_out = c->q2[1]; A.q3_out = c->q3[1];
+    A.n2_out = c->ctl + CTL_N2; A.n3_out = c->ctl + CTL_N3;
+    A.n_pk = c->ctl + CTL_NPK;
+    A.work_counter = c->ctl + CTL_WORK;
+    HIPCHK(c, hipEventRecord(c->ev_g0t, c->stream));
+    if (A.n_items > 0) {
+      int rc = launch_tr(c->dP, &A, tr_grid(A.n_items), c->lds_bytes, c->stream);
+      if (rc) return fail(c, C2D_E_HIP, "transport launch (gen 0): %s", hipGetErrorString((hipError_t)rc));
+      launches++;
+    }
+    HIPCHK(c, hipEventRecord(c->ev_g0b, c->stream));
     HIPCHK(c, hipMemcpyAsync(nq, c->ctl + CTL_N2, sizeof nq, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (gen == 0) c->last_g0_steps = (int64_t)nq[CTL_CNT - CTL_N2];
+    c->last_g0_steps = (int64_t)nq[CTL_CNT - CTL_N2];
+    gen = 1;
+  }
+  /* ---- generations >= 1: scatter sampling, then transport of the secondaries ---- */
+  for (;;) {
     if ((int64_t)nq[0] > cfg.queue_capacity || (int64_t)nq[1] > cfg.queue_capacity)
       return fail(c, C2D_E_QUEUE_OVERFLOW, "scatter queue overflow in generation %d (%llu, %llu > %lld)",
-                  gen, nq[0], nq[1], (long long)cfg.queue_capacity);
+                  gen - 1, nq[0], nq[1], (long long)cfg.queue_capacity);
     n2 = (int64_t)nq[0];
     n3 = (int64_t)nq[1];
-    qin = 1 - qin;
+    if (n2 + n3 == 0) break;
+    qin = 1 - qin;              /* this generation's input = last generation's output */
+    HIPCHK(c, hipMemsetAsync(c->ctl + CTL_N2, 0, 2 * sizeof(unsigned long long), c->stream));
+    const int64_t total = n2 * cfg.split2 + n3 * cfg.split3;
+    for (int64_t b = 0; b < total; b += c->pk.cap) {
+      const int64_t e = std::min<int64_t>(total, b + c->pk.cap);
+      HIPCHK(c, hipMemsetAsync(c->ctl + CTL_NPK, 0, sizeof(unsigned long long), c->stream));
+      HIPCHK(c, hipMemsetAsync(c->ctl + CTL_WORK, 0, sizeof(unsigned long long), c->stream));
+      GenArgs A = {};
+      A.gen = gen;
+      A.q2_in = c->q2[qin]; A.q3_in = c->q3[qin];
+      A.q2_out = c->q2[1 - qin]; A.q3_out = c->q3[1 - qin];
+      A.n2_out = c->ctl + CTL_N2; A.n3_out = c->ctl + CTL_N3;
+      A.n_pk = c->ctl + CTL_NPK;
+      A.work_counter = c->ctl + CTL_WORK;
+      A.item_begin = b; A.item_end = e;
+      A.n2_in = n2; A.n3_in = n3;
+      int rc = launch_sc(c->dP, &A, aux_grid(e - b), c->stream);
+      if (rc) return fail(c, C2D_E_HIP, "scatter launch (gen %d): %s", gen, hipGetErrorString((hipError_t)rc));
+      rc = launch_tr(c->dP, &A, tr_grid(e - b), c->lds_bytes, c->stream);
+      if (rc) return fail(c, C2D_E_HIP, "transport launch (gen %d): %s", gen, hipGetErrorString((hipError_t)rc));
+      launches += 2;
+    }
+    HIPCHK(c, hipMemcpyAsync(nq, c->ctl + CTL_N2, sizeof nq, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     gen++;
   }
   HIPCHK(c, hipEventRecord(c->ev_end, c->stream));
@@ -539,7 +623,8 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   float ms0 = 0.f, msall = 0.f;
   if (launches > 0) {
-    (void)hipEventElapsedTime(&ms0, c->ev_g0a, c->ev_g0b);
+    (void)hipEventElapsedTime(&ms0, c->ev_g0t, c->ev_g0b);
+    (void)hipEventElapsedTime(&c->last_src_ms, c->ev_g0a, c->ev_g0t);
     (void)hipEventElapsedTime(&msall, c->ev_g0a, c->ev_end);
   }
   c->last_g0_ms = ms0;

@@ -1,21 +1,30 @@
 /*
  * transport.hip — MI355X (gfx950) photon-packet transport kernels.
  *
- * One launch tracks every packet of one "generation" of a Monte-Carlo time
- * step.  Generation 0 = the step's sources: census packets of the previous
- * step (src/imcfield2d.f:57-144), volume packets (src/imcvol2d_para.f:90-414)
- * and surface packets (src/imcsurf2d_para.f:228-534); generation g+1 = the
- * split2/split3 scatter secondaries created by collisions in generation g
- * (src/imctrk2d.f:580-684).  The reference's recursive depth-first tracker
- * (src/imctrk2d.f:8-708) becomes a persistent per-lane state machine:
+ * A Monte-Carlo time step is processed in "generations".  Generation 0 =
+ * the step's sources: census packets of the previous step
+ * (src/imcfield2d.f:57-144), volume packets (src/imcvol2d_para.f:90-414) and
+ * surface packets (src/imcsurf2d_para.f:228-534); generation g+1 = the
+ * split2/split3 scatter secondaries of the collisions of generation g
+ * (src/imctrk2d.f:580-684).  Three kernels:
  *
- *   lane idle -> fetch a work item (wave-aggregated, chunked atomic) ->
- *   sample the source into registers -> split1 probe copies, one packet-step
- *   per loop iteration -> recombined unscattered copy (imctrk2d(0)) ->
- *   next work item.
+ *   c2d_source_kernel     samples the generation-0 volume/surface sources
+ *                         into the packet store (PktSoA, one lane per packet);
+ *   c2d_scatter_kernel    samples compb2d for every split2/split3 copy of the
+ *                         generation's collision records, deposits the
+ *                         energy change, and writes the secondaries to the
+ *                         packet store (or a third-split record to q3);
+ *   c2d_transport_kernel  the reference's recursive depth-first tracker
+ *                         (src/imctrk2d.f:8-708) as a persistent per-lane
+ *                         state machine: lane idle -> fetch a packet
+ *                         (wave-aggregated, chunked atomic) -> split1 probe
+ *                         copies, one packet-step per loop iteration ->
+ *                         recombined unscattered copy (imctrk2d(0)) -> next.
  *
- * Packet state never leaves registers between packet-steps; HBM sees only
- * the source records, the census/event/scatter appends (wave-ballot
+ * Keeping the rejection samplers out of the tracking loop keeps its register
+ * footprint (and so its occupancy) at what one packet-step needs.  Packet
+ * state never leaves registers between packet-steps; HBM sees only the
+ * packet records, the census/event/collision appends (wave-ballot
  * compaction: one atomic per wave) and the tally flush.  Cell tallies
  * (edep, prdep, ecens, npcen) and escape tallies (fout, edout, erlk*) are
  * privatised per workgroup in LDS and flushed once with atomics.  Every
@@ -24,7 +33,8 @@
  *
  * Built twice (see Makefile): C2D_VARIANT=0 "exact" (comtot by the full
  * 199-term sum, -ffp-contract=off: bit-identical to the oracle's lineage
- * mode) and C2D_VARIANT=1 "fast" (comtot from the per-step cubic table).
+ * mode) and C2D_VARIANT=1 "fast" (comtot from the per-step cubic table,
+ * cos(phi) carried between packet-steps, FMA contraction).
  */
 #include <hip/hip_runtime.h>
 
@@ -43,6 +53,17 @@
 #define C2D_TABLE_COMTOT 1
 #endif
 
+/* occupancy target of the transport kernel (waves per SIMD; 0 = compiler's
+ * choice for BLOCK-thread groups, i.e. up to 256 VGPRs) */
+#ifndef C2D_WAVES_PER_EU
+#define C2D_WAVES_PER_EU 0
+#endif
+#if C2D_WAVES_PER_EU > 0
+#define C2D_TR_ATTR __attribute__((amdgpu_waves_per_eu(C2D_WAVES_PER_EU)))
+#else
+#define C2D_TR_ATTR
+#endif
+
 namespace c2d {
 namespace {
 
@@ -51,8 +72,8 @@ constexpr double C_LIGHT = 2.9979245620e10;    /* general.pa:25 */
 constexpr double RAD_CP = 3.333564097e-11;     /* general.pa:23 */
 constexpr double EMASSKEV = 5.11e2;
 constexpr double SIGTHOM = 6.6516e-25;
-constexpr int WAVE = 64;
-constexpr int BLOCK = 512;
+constexpr int BLOCK = 512;        /* transport kernel */
+constexpr int SBLOCK = 256;       /* source / scatter kernels */
 constexpr long long CHUNK = 64;
 
 /* Fortran REAL literals promoted to double (src/imcvol2d_para.f:204,221,247,268,336) */
@@ -63,7 +84,14 @@ enum : int32_t { FL_CONT = 0, FL_END = 1, FL_COLLIDE = 2 };
 
 struct Pkt {
   double xnu, wmu, phi, rpre, zpre, dcen, ew, wtmin;
+#if C2D_TABLE_COMTOT
+  double eta;         /* fast build: cos(phi) carried between packet-steps       */
+  double tt;          /* comtot table abscissa fraction for xnu                   */
+  int32_t tg;         /* comtot table index (0: outside the table, exact sum)     */
+  int32_t esw;        /* Eta_switch (quadrant of phi), constant between events    */
+#endif
   int32_t jph, kph, jgpsp, jgplc, jgpmu, mode, kap;
+  int32_t ie;         /* E_ph bin of xnu (imctrk2d.f:382-384), cached per xnu     */
   uint64_t key;
   uint32_t ctr;
   uint32_t nflight;   /* safety cap: a history that stops progressing is aborted */
@@ -74,10 +102,13 @@ struct Pkt {
 constexpr uint32_t MAX_FLIGHTS = 1u << 20;
 constexpr int MAX_REJECT = 1 << 20;
 
-/* per-thread counters, reduced once per wave at the end */
+/* Counters: packet-steps in a register (one per step), the rarer events
+ * as LDS atomics on a per-workgroup array, flushed once at the end. */
 struct LaneCnt {
-  uint32_t steps, escapes, census, collide, killed, sources, compb, events, aborted;
+  uint32_t steps;
+  uint32_t* sh;      /* LDS [C2D_NCOUNTERS] */
 };
+#define LC_ADD(lc, which) atomicAdd(&(lc).sh[which], 1u)
 
 /* Tally views.  Cell tallies edep|prdep|ecens|npcen (stride ncell) and
  * escape tallies fout|edout|erlki|erlko|erlku|erlkl have the same layout in
@@ -219,18 +250,16 @@ __device__ __noinline__ double comtot_exact(const KParams& P, int cell, double x
 }
 
 #if C2D_TABLE_COMTOT
-/* cubic Lagrange interpolation of the per-step table in u = ln(xnu) */
-__device__ __forceinline__ double comtot_table(const KParams& P, int cell, double xnu) {
-  double u = c2d_log(xnu);
-  double s = (u - C2D_COMTAB_U0) * P.comtab_du_inv;
-  if (!(s >= 1.0 && s < (double)(C2D_COMTAB_N - 3))) return comtot_exact(P, cell, xnu);
-  int g = (int)s;
-  double t = s - (double)g;
-  const double* tb = P.comtab + (int64_t)cell * C2D_COMTAB_N + (g - 1);
-  double y0 = tb[0], y1 = tb[1], y2 = tb[2], y3 = tb[3];
-  double tm1 = t - 1.0, tm2 = t - 2.0, tp1 = t + 1.0;
-  double cosig = -(t * tm1 * tm2) * (1.0 / 6.0) * y0 + (tp1 * tm1 * tm2) * 0.5 * y1 -
-                 (tp1 * t * tm2) * 0.5 * y2 + (tp1 * t * tm1) * (1.0 / 6.0) * y3;
+/* cubic Lagrange interpolation of the per-step table at the packet's cached
+ * abscissa (tg, tt); tg == 0 means xnu lies outside the table: exact sum. */
+__device__ __forceinline__ double comtot_table(const KParams& P, int cell, const double xnu,
+                                               const int tg, const double t) {
+  if (tg == 0) return comtot_exact(P, cell, xnu);
+  const double* tb = P.comtab + (int64_t)cell * C2D_COMTAB_N + (tg - 1);
+  const double y0 = tb[0], y1 = tb[1], y2 = tb[2], y3 = tb[3];
+  const double tm1 = t - 1.0, tm2 = t - 2.0, tp1 = t + 1.0;
+  const double cosig = -(t * tm1 * tm2) * (1.0 / 6.0) * y0 + (tp1 * tm1 * tm2) * 0.5 * y1 -
+                       (tp1 * t * tm2) * 0.5 * y2 + (tp1 * t * tm1) * (1.0 / 6.0) * y3;
   if (cosig < 1.0e-40) return 1.0e-40;
   return P.n_e[cell] * cosig;
 }
@@ -296,7 +325,7 @@ __device__ __forceinline__ int cdf_index(const double* cdf /*0-based*/, int n, d
 /* ------------------------------------------------------------------ */
 /* nth2d (src/nontherm2d.f:159-183) + compb2d (src/compb_2d.f:1-318)    */
 /* ------------------------------------------------------------------ */
-__device__ __noinline__ int compb2d(const KParams& P, const Tal T, Pkt& p, LaneCnt& lc) {
+__device__ __forceinline__ int compb2d(const KParams& P, const Geo* g, double* nel, Pkt& p, LaneCnt& lc) {
   const double fuzz = 1.0e-10, lim = 9.9999999e-1;
   const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
   const double* Pc = P.Pnt + (int64_t)cell * C2D_NUM_NT;
@@ -305,9 +334,9 @@ __device__ __noinline__ int compb2d(const KParams& P, const Tal T, Pkt& p, LaneC
   double sz, games, phat, znues, wa, wb, swa;
   int i_gam;
   int guard = 0;
-  lc.compb++;
+  LC_ADD(lc, C2D_CNT_COMPB);
   for (;;) {
-    if (++guard > MAX_REJECT) { lc.aborted++; break; }
+    if (++guard > MAX_REJECT) { LC_ADD(lc, C2D_CNT_ABORTED); break; }
     /* nth2d */
     double rnum = U(p);
     rnum = (double)(int32_t)(rnum * 1.0e6) / 1.0e6 + 1.0e-6 * U(p);
@@ -323,7 +352,7 @@ __device__ __noinline__ int compb2d(const KParams& P, const Tal T, Pkt& p, LaneC
     }
     gamm = __builtin_sqrt(P.gnt[i - 1] * P.gnt[i - 2]) + 1.0;
     betb = __builtin_sqrt(1.0 - 1.0 / (gamm * gamm));
-    atomicAdd(&P.T[P.off.nelectron + i], 1.0);
+    atomicAdd(&nel[i], 1.0);
     i_gam = i;
     omeg = 2.0 * U(p) - 1.0;
     omeg = clampd(omeg, lim);
@@ -347,7 +376,7 @@ __device__ __noinline__ int compb2d(const KParams& P, const Tal T, Pkt& p, LaneC
   }
   betz = 1.0 + 2.0 * znue;
   for (;;) {
-    if (++guard > 2 * MAX_REJECT) { lc.aborted++; break; }
+    if (++guard > 2 * MAX_REJECT) { LC_ADD(lc, C2D_CNT_ABORTED); break; }
     sz = (1.0 + 2.0 * znue * U(p)) / betz;
     games = 1.0 + (1.0 - 1.0 / sz) / znue;
     if ((1.0 - games * games) < 0.0) continue;
@@ -358,7 +387,7 @@ __device__ __noinline__ int compb2d(const KParams& P, const Tal T, Pkt& p, LaneC
   }
   znues = znue * sz;
   for (;;) {
-    if (++guard > 3 * MAX_REJECT) { lc.aborted++; break; }
+    if (++guard > 3 * MAX_REJECT) { LC_ADD(lc, C2D_CNT_ABORTED); break; }
     wa = U(p);
     wb = 2.0 * U(p) - 1.0;
     swa = wa * wa + wb * wb;
@@ -373,7 +402,7 @@ __device__ __noinline__ int compb2d(const KParams& P, const Tal T, Pkt& p, LaneC
   double znus = (1.0 + betb * omeges) * gamm * znues;
   double gams = clampd(1.0 - (znue - znues) / (znu * znus), lim);
   for (;;) {
-    if (++guard > 4 * MAX_REJECT) { lc.aborted++; break; }
+    if (++guard > 4 * MAX_REJECT) { LC_ADD(lc, C2D_CNT_ABORTED); break; }
     wa = U(p);
     wb = 2.0 * U(p) - 1.0;
     swa = wa * wa + wb * wb;
@@ -390,9 +419,9 @@ __device__ __noinline__ int compb2d(const KParams& P, const Tal T, Pkt& p, LaneC
                           lim);
   double dphi = c2d_acos(cosdphi);
   double phis = p.phi + dphi;
-  p.jgpsp = bin_sp(T.g, P.nphtotal, xnus, 1.000001, 0.999999, 0);
-  p.jgplc = bin_lc(T.g, P.nph_lc, xnus);
-  p.jgpmu = bin_mu(T.g, P.nmu, wmus);
+  p.jgpsp = bin_sp(g, P.nphtotal, xnus, 1.000001, 0.999999, 0);
+  p.jgplc = bin_lc(g, P.nph_lc, xnus);
+  p.jgpmu = bin_mu(g, P.nmu, wmus);
   p.ew = p.ew * xnus / p.xnu;
   p.xnu = xnus;
   p.wmu = wmus;
@@ -411,7 +440,7 @@ __device__ __forceinline__ void push_event(const KParams& P, double tb, const Pk
   } else {
     atomicOr(P.err, ERR_EVENT);
   }
-  lc.events++;
+  LC_ADD(lc, C2D_CNT_EVENTS);
 }
 
 __device__ __forceinline__ void escape_tally(const KParams& P, const Tal& T, const Pkt& p) {
@@ -425,14 +454,14 @@ __device__ __forceinline__ int imcleak(const KParams& P, const Tal& T, Pkt& p, L
   if (p.kph == 0) {
     if (P.rmin > 1.0e-10) {
       atomicAdd(&T_ERLKI(P, T)[p.jph - 1], p.ew);
-      lc.escapes++;
+      LC_ADD(lc, C2D_CNT_ESCAPES);
       return 1;
     }
     p.phi = 1.0e-6;
     p.kph = 1;
     return 0;
   }
-  lc.escapes++;
+  LC_ADD(lc, C2D_CNT_ESCAPES);
   const double tb = P.time + P.dt - RAD_CP * p.dcen;   /* H4: fresh t_bound everywhere */
   if (p.jph <= 0) {
     if (P.tbbl[p.kph - 1] > 0.0) {
@@ -485,7 +514,7 @@ __device__ __forceinline__ void census_write(const KParams& P, const Tal& T, con
   } else {
     atomicOr(P.err, ERR_CENSUS);
   }
-  lc.census++;
+  LC_ADD(lc, C2D_CNT_CENSUS);
 }
 
 __device__ __forceinline__ void push_scat(const KParams& P, ScatRec* q, unsigned long long* n, const ScatRec& r) {
@@ -518,6 +547,38 @@ __device__ __forceinline__ void load_rec(Pkt& p, const ScatRec& r) {
 }
 
 /* ------------------------------------------------------------------ */
+/* per-packet caches                                                   */
+/* ------------------------------------------------------------------ */
+/* E_ph bin and comtot-table position depend on xnu only: computed when a
+ * packet starts (source, probe restart, secondary) instead of every step. */
+__device__ __forceinline__ void cache_energy(const KParams& P, const Geo* g, Pkt& p) {
+  p.ie = grid_index(g->E_ph, C2D_N_VOL, p.xnu);
+#if C2D_TABLE_COMTOT
+  const double s = (c2d_log(p.xnu) - C2D_COMTAB_U0) * P.comtab_du_inv;
+  if (s >= 1.0 && s < (double)(C2D_COMTAB_N - 3)) {
+    p.tg = (int32_t)s;
+    p.tt = s - (double)p.tg;
+  } else {
+    p.tg = 0;
+    p.tt = 0.0;
+  }
+#endif
+}
+
+/* azimuth bookkeeping.  Exact build: phi as in the reference (cos(phi) each
+ * step, acos after the move).  Fast build: carry Eta = cos(phi) and its
+ * quadrant switch between steps (cos(acos(E)) = E to an ulp; drops the
+ * reference's 4e-11 rad/step rotation from pi = 3.1415926536), and
+ * materialise phi only when an event needs it. */
+__device__ __forceinline__ void set_phi(Pkt& p, double phi) {
+  p.phi = phi;
+#if C2D_TABLE_COMTOT
+  p.eta = c2d_cos(phi);
+  p.esw = (phi <= PI_REF && phi >= 1.0e-10) ? 1 : -1;
+#endif
+}
+
+/* ------------------------------------------------------------------ */
 /* one packet-step: label 100 ... 900 of src/imctrk2d.f:139-578          */
 /* ------------------------------------------------------------------ */
 struct ComCache {
@@ -537,7 +598,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   double colmfp = -c2d_log(mb_ran);
   if (p.ew < 1.0e-40) return FL_END;
   if (++p.nflight > MAX_FLIGHTS) {
-    lc.aborted++;
+    LC_ADD(lc, C2D_CNT_ABORTED);
     return FL_END;
   }
   p.wmu = clampd(p.wmu, lim8);
@@ -545,7 +606,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   double comac = 0.0;
   if (p.mode != 0) {
 #if C2D_TABLE_COMTOT
-    comac = comtot_table(P, cell, p.xnu);
+    comac = comtot_table(P, cell, p.xnu, p.tg, p.tt);
     (void)cc;
 #else
     /* comtot is a pure function of (cell, xnu): caching per packet is exact
@@ -575,8 +636,13 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   else { trld = dcol; ikind = 3; }
   lc.steps++;
   /* geometry (imctrk2d.f:228-379) */
+#if C2D_TABLE_COMTOT
+  double Eta = p.eta;
+  const int eta_switch = p.esw;
+#else
   double Eta = c2d_cos(p.phi);
   const int eta_switch = (p.phi <= PI_REF && p.phi >= 1.0e-10) ? 1 : -1;
+#endif
   Eta = clampd(Eta, lim8);
   const double rpre = p.rpre, zpre = p.zpre, wmu = p.wmu;
   const double disp = Eta * rpre;
@@ -627,9 +693,8 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
     znew = zpre + trld * wmu;
   }
   /* absorption (imctrk2d.f:382-462); gamma-gamma opacity inert (H6) */
-  const int ie = grid_index(g->E_ph, C2D_N_VOL, p.xnu);
   const double* kap = p.kap ? P.kappa_s : P.kappa_cv;
-  double sigabs = 1.0e-40 + 1.0 * kap[(int64_t)cell * C2D_N_VOL + (ie - 1)];
+  double sigabs = 1.0e-40 + 1.0 * kap[(int64_t)cell * C2D_N_VOL + (p.ie - 1)];
   if (sigabs < 1.0e-40) sigabs = 1.0e-40;
   const double xabs = sigabs * trld;
   const double ewnew = (xabs < 100.0) ? p.ew * c2d_exp(-xabs) : 0.0;
@@ -656,23 +721,33 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
     atomicAdd(&T_PRDEP(P, T)[cell], delpr);
   }
   if (ewnew <= p.wtmin) {
-    lc.killed++;
+    LC_ADD(lc, C2D_CNT_KILLED);
     return FL_END;
   }
   p.ew = ewnew;
   p.dcen = p.dcen - trld;
   Eta = (trld + Eta * rpre) / rnew;          /* hazard H1: trld, not f (imctrk2d.f:472) */
   Eta = clampd(Eta, lim9);
+  const bool leaves = (jnew == P.nz + 1 || jnew == 0 || knew == P.nr + 1 || knew == 0);
+#if C2D_TABLE_COMTOT
+  p.eta = Eta;
+  if (p.mode != -1 && (ikind != 1 || leaves)) {   /* an event will read phi */
+    p.phi = c2d_acos(Eta);
+    if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
+  }
+#else
   p.phi = c2d_acos(Eta);
   if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
+#endif
   p.rpre = rnew;
   p.zpre = znew;
   if (ikind == 1) {
-    if (jnew == P.nz + 1 || jnew == 0 || knew == P.nr + 1 || knew == 0) {
+    if (leaves) {
       p.jph = jnew;
       p.kph = knew;
       if (p.mode == -1) return FL_END;
       if (imcleak(P, T, p, lc) == 1) return FL_END;
+      set_phi(p, p.phi);                        /* axis pass-through set phi = 1e-6 */
       return FL_CONT;
     }
     p.kph = knew;
@@ -683,7 +758,13 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
     if (p.mode != -1) census_write(P, T, p, lc);
     return FL_END;
   }
-  lc.collide++;
+  LC_ADD(lc, C2D_CNT_COLLIDE);
+  if (p.mode == -1) {   /* probes read phi too (the collision record) */
+#if C2D_TABLE_COMTOT
+    p.phi = c2d_acos(Eta);
+    if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
+#endif
+  }
   return FL_COLLIDE;
 }
 
@@ -691,7 +772,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
 /* sources                                                             */
 /* ------------------------------------------------------------------ */
 /* planck (src/planck2d.f:1-141) */
-__device__ __forceinline__ void planck(const KParams& P, const Tal& T, Pkt& p, double tpl) {
+__device__ __forceinline__ void planck(const KParams& P, const Geo* G, Pkt& p, double tpl) {
   double u4, ap0, ap1 = 1.0, ap2 = 1.0, ap3 = 1.0, rn1;
   do {
     u4 = U(p);
@@ -707,17 +788,17 @@ __device__ __forceinline__ void planck(const KParams& P, const Tal& T, Pkt& p, d
     ap1 = ap1 + (ap3 * ap3) * (ap3 * ap3);
   }
   p.xnu = ap0 * ap3 * tpl;
-  p.jgpsp = bin_sp(T.g, P.nphtotal, p.xnu, F32(1.000001), F32(0.999999), 0);
-  p.jgplc = bin_lc(T.g, P.nph_lc, p.xnu);
-  p.jgpmu = bin_mu(T.g, P.nmu, p.wmu);
+  p.jgpsp = bin_sp(G, P.nphtotal, p.xnu, F32(1.000001), F32(0.999999), 0);
+  p.jgplc = bin_lc(G, P.nph_lc, p.xnu);
+  p.jgpmu = bin_mu(G, P.nmu, p.wmu);
 }
 
 /* file_sample (src/imcsurf2d_para.f:694-788) */
-__device__ __forceinline__ void file_sample(const KParams& P, const Tal& T, Pkt& p, int spec) {
+__device__ __forceinline__ void file_sample(const KParams& P, const Geo* G, Pkt& p, int spec) {
   if (spec < 0 || spec >= P.n_spectra) {
     atomicOr(P.err, ERR_SPEC);
     p.xnu = 1.0;
-    p.jgpsp = 0; p.jgplc = 0; p.jgpmu = bin_mu(T.g, P.nmu, p.wmu);
+    p.jgpsp = 0; p.jgplc = 0; p.jgpmu = bin_mu(G, P.nmu, p.wmu);
     return;
   }
   const SpecDev sp = P.spectra[spec];
@@ -729,14 +810,13 @@ __device__ __forceinline__ void file_sample(const KParams& P, const Tal& T, Pkt&
   double x2 = U(p);
   double Ei = sp.E_file[i - 1], a1 = sp.a1[i - 1], Ii = sp.I_file[i - 1], Fi = sp.F_file[i - 1];
   p.xnu = Ei * c2d_pow(a1 * Ii * x2 / (Fi * Ei) + 1.0, 1.0 / a1);
-  p.jgpsp = bin_sp(T.g, P.nphtotal, p.xnu, 1.000001, 0.999999, 0);
-  p.jgplc = bin_lc(T.g, P.nph_lc, p.xnu);
-  p.jgpmu = bin_mu(T.g, P.nmu, p.wmu);
+  p.jgpsp = bin_sp(G, P.nphtotal, p.xnu, 1.000001, 0.999999, 0);
+  p.jgplc = bin_lc(G, P.nph_lc, p.xnu);
+  p.jgpmu = bin_mu(G, P.nmu, p.wmu);
 }
 
 /* one volume packet of vol_calc (src/imcvol2d_para.f:157-392) */
-__device__ __forceinline__ void vol_source(const KParams& P, const Tal& T, Pkt& p, int jv, int kv) {
-  const Geo* g = T.g;
+__device__ __forceinline__ void vol_source(const KParams& P, const Geo* g, Pkt& p, int jv, int kv) {
   const int cell = (jv - 1) * P.nr + (kv - 1);
   const double* vf = P.vfrac + 4 * cell;
   const double f_thermal = vf[0], f_inn = vf[1], f_outer = vf[2], f_upper = vf[3];
@@ -816,8 +896,7 @@ __device__ __forceinline__ void vol_source(const KParams& P, const Tal& T, Pkt& 
 
 /* surface packets: z_surf_calc / r_surf_calc (src/imcsurf2d_para.f:254-528).
  * side 0 inner z-surface js, 1 outer js, 2 upper r-surface ks, 3 lower ks. */
-__device__ __forceinline__ void surf_source(const KParams& P, const Tal& T, Pkt& p, int side, int s1, int slot) {
-  const Geo* g = T.g;
+__device__ __forceinline__ void surf_source(const KParams& P, const Geo* g, Pkt& p, int side, int s1, int slot) {
   const double lim10 = 0.9999999999;
   const double ew = P.surf_ew[slot], tbb = P.surf_tbb[slot];
   const int spec = P.surf_spec[slot];
@@ -832,8 +911,8 @@ __device__ __forceinline__ void surf_source(const KParams& P, const Tal& T, Pkt&
     p.zpre = (js == 1) ? g->z[1] * U(p) : g->z[js - 1] + U(p) * (g->z[js] - g->z[js - 1]);
     p.ew = ew;
     p.dcen = U(p) * C_LIGHT * P.dt;
-    if (tbb > 0.0) planck(P, T, p, tbb);
-    else file_sample(P, T, p, spec);
+    if (tbb > 0.0) planck(P, g, p, tbb);
+    else file_sample(P, g, p, spec);
     p.kph = 1;
   } else if (side == 1) {
     const int js = s1;
@@ -851,8 +930,8 @@ __device__ __forceinline__ void surf_source(const KParams& P, const Tal& T, Pkt&
     }
     p.ew = ew;
     p.dcen = U(p) * C_LIGHT * P.dt;
-    if (tbb > 0.0) planck(P, T, p, tbb);
-    else file_sample(P, T, p, spec);
+    if (tbb > 0.0) planck(P, g, p, tbb);
+    else file_sample(P, g, p, spec);
     p.kph = P.nr;
   } else {
     const int ks = s1;
@@ -866,8 +945,8 @@ __device__ __forceinline__ void surf_source(const KParams& P, const Tal& T, Pkt&
       p.rpre = __builtin_sqrt(rlow * rlow + psi * (g->r[ks] * g->r[ks] - rlow * rlow));
       p.ew = ew;
       p.dcen = U(p) * C_LIGHT * P.dt;
-      if (tbb > 0.0) planck(P, T, p, tbb);
-      else file_sample(P, T, p, spec);
+      if (tbb > 0.0) planck(P, g, p, tbb);
+      else file_sample(P, g, p, spec);
       p.jph = P.nz;
     } else {
       p.wmu = 9.9999999e-1;
@@ -876,8 +955,8 @@ __device__ __forceinline__ void surf_source(const KParams& P, const Tal& T, Pkt&
       p.zpre = P.zmin;
       p.rpre = __builtin_sqrt(rlow * rlow + psi * (g->r[ks] * g->r[ks] - rlow * rlow));
       p.ew = ew;
-      if (tbb > 0.0) planck(P, T, p, tbb);
-      else file_sample(P, T, p, spec);
+      if (tbb > 0.0) planck(P, g, p, tbb);
+      else file_sample(P, g, p, spec);
       p.dcen = U(p) * C_LIGHT * P.dt;
       p.jph = 1;
     }
@@ -907,12 +986,188 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
+__device__ __forceinline__ void init_counters(uint32_t* sh) {
+  if (threadIdx.x < C2D_NCOUNTERS) sh[threadIdx.x] = 0u;
+}
+
+/* after the final __syncthreads of the kernel */
+__device__ __forceinline__ void flush_counters(const KParams& P, LaneCnt& lc, uint32_t lane) {
+  const uint32_t st = wave_sum(lc.steps);
+  if (lane == 0 && st) atomicAdd(&lc.sh[C2D_CNT_STEPS], st);
+  __syncthreads();
+  if (threadIdx.x < C2D_NCOUNTERS && lc.sh[threadIdx.x])
+    atomicAdd(&P.cnt[threadIdx.x], (unsigned long long)lc.sh[threadIdx.x]);
+}
+
+__device__ __forceinline__ void store_pk(const PktSoA& s, int64_t i, const Pkt& p) {
+  s.rpre[i] = p.rpre; s.zpre[i] = p.zpre; s.wmu[i] = p.wmu; s.phi[i] = p.phi;
+  s.ew[i] = p.ew; s.xnu[i] = p.xnu; s.dcen[i] = p.dcen;
+  s.jk[i] = ((uint32_t)p.jph << 16) | (uint32_t)p.kph;
+  s.bins[i] = (uint32_t)p.jgpsp | ((uint32_t)p.jgplc << 8) | ((uint32_t)p.jgpmu << 16) |
+              ((uint32_t)p.kap << 24);
+  s.ctr[i] = p.ctr;
+  s.key[i] = p.key;
+}
+
+__device__ __forceinline__ void load_pk(Pkt& p, const PktSoA& s, int64_t i) {
+  p.rpre = s.rpre[i]; p.zpre = s.zpre[i]; p.wmu = s.wmu[i]; p.phi = s.phi[i];
+  p.ew = s.ew[i]; p.xnu = s.xnu[i]; p.dcen = s.dcen[i];
+  const uint32_t jk = s.jk[i], bn = s.bins[i];
+  p.jph = (int32_t)(jk >> 16); p.kph = (int32_t)(jk & 0xffffu);
+  p.jgpsp = (int32_t)(bn & 0xffu); p.jgplc = (int32_t)((bn >> 8) & 0xffu);
+  p.jgpmu = (int32_t)((bn >> 16) & 0xffu); p.kap = (int32_t)(bn >> 24);
+  p.ctr = s.ctr[i];
+  p.key = s.key[i];
+}
+
 }  // namespace
+
+/* ------------------------------------------------------------------ */
+/* generation-0 sources: volume (imcvol2d_para.f:90-414) and surface     */
+/* (imcsurf2d_para.f:228-534) packets, one lane per packet               */
+/* ------------------------------------------------------------------ */
+__global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_source_kernel)(const KParams* __restrict__ Pg) {
+  const KParams& P = *Pg;
+  __shared__ double geo_lds[GEO_DOUBLES];
+  {
+    const double* gsrc = reinterpret_cast<const double*>(P.geo);
+    for (int i = threadIdx.x; i < GEO_DOUBLES; i += SBLOCK) geo_lds[i] = gsrc[i];
+  }
+  __syncthreads();
+  const Geo* g = reinterpret_cast<const Geo*>(geo_lds);
+  const int64_t n = P.n_vol_items + P.n_surf_items;
+  const int64_t stride = (int64_t)gridDim.x * SBLOCK;
+  for (int64_t it = (int64_t)blockIdx.x * SBLOCK + threadIdx.x; it < n; it += stride) {
+    Pkt p;
+    p.ctr = 0;
+    if (it < P.n_vol_items) {
+      const int64_t gidx = it * P.world + P.rank;
+      const int cell = upper_index(P.vol_prefix, P.ncell, gidx);
+      const int64_t nn = gidx - P.vol_prefix[cell];
+      p.key = c2d_derive(P.step_key, C2D_TAG_VOL, (uint32_t)nn, (uint32_t)cell);
+      p.kap = 0;
+      vol_source(P, g, p, cell / P.nr + 1, cell % P.nr + 1);
+    } else {
+      const int64_t gidx = (it - P.n_vol_items) * P.world + P.rank;
+      const int slot = upper_index(P.surf_prefix, P.nslot, gidx);
+      const int64_t nn = gidx - P.surf_prefix[slot];
+      int side, s1;
+      if (slot < 2 * P.nz) { side = slot & 1; s1 = slot / 2 + 1; }
+      else { side = 2 + ((slot - 2 * P.nz) & 1); s1 = (slot - 2 * P.nz) / 2 + 1; }
+      p.key = c2d_derive(P.step_key, C2D_TAG_SURF + (uint32_t)side, (uint32_t)nn,
+                         (uint32_t)(s1 - 1));
+      p.kap = 1;
+      surf_source(P, g, p, side, s1, slot);
+    }
+    p.ctr = 0;   /* a source's own draws are done: its copies use derived keys */
+    store_pk(P.pk, it, p);
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* scatter secondaries (imctrk2d.f:580-684): one lane per split copy     */
+/* ------------------------------------------------------------------ */
+__global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KParams* __restrict__ Pg,
+                                                                     const GenArgs A) {
+  const KParams& P = *Pg;
+  __shared__ double geo_lds[GEO_DOUBLES];
+  __shared__ double nel_lds[C2D_NUM_NT + 2];
+  __shared__ double eic_lds[C2D_NUM_NT + 2];
+  for (int i = threadIdx.x; i < GEO_DOUBLES; i += SBLOCK)
+    geo_lds[i] = reinterpret_cast<const double*>(P.geo)[i];
+  __shared__ uint32_t cnt_lds[C2D_NCOUNTERS];
+  for (int i = threadIdx.x; i < C2D_NUM_NT + 2; i += SBLOCK) {
+    nel_lds[i] = 0.0;
+    eic_lds[i] = 0.0;
+  }
+  init_counters(cnt_lds);
+  __syncthreads();
+  const Geo* g = reinterpret_cast<const Geo*>(geo_lds);
+  LaneCnt lc = {0u, cnt_lds};
+  const double twopi = 2.0 * PI_REF;
+  const int64_t n2items = A.n2_in * P.split2;
+  const int64_t stride = (int64_t)gridDim.x * SBLOCK;
+  for (int64_t item = A.item_begin + (int64_t)blockIdx.x * SBLOCK + threadIdx.x; item < A.item_end;
+       item += stride) {
+    const bool is2 = item < n2items;
+    ScatRec rec;
+    uint32_t ii;
+    if (is2) {
+      rec = A.q2_in[item / P.split2];
+      ii = (uint32_t)(item % P.split2);
+    } else {
+      const int64_t it3 = item - n2items;
+      rec = A.q3_in[it3 / P.split3];
+      ii = (uint32_t)(it3 % P.split3);
+    }
+    Pkt p;
+    const double ewcsv = rec.ew / P.split2;
+    /* split2 copy: ew = ewcsv; split3 copy: ew = ewcsv / split3 (imctrk2d.f:611,636) */
+    const double ewold = is2 ? ewcsv : ewcsv / P.split3;
+    const double thr = ewold * P.split2 * P.split1 * P.spl3_trg;
+    p.key = c2d_derive(rec.key, is2 ? C2D_TAG_SCAT2 : C2D_TAG_SCAT3, ii, rec.ctr);
+    p.ctr = 0;
+    int i_gam = 0, guard = 0;
+    bool third = false;
+    for (;;) {
+      load_rec(p, rec);
+      p.ew = ewold;
+      i_gam = compb2d(P, g, nel_lds, p, lc);
+      if (is2) {
+        third = p.ew > thr;   /* third split (imctrk2d.f:631-661): resampled next generation */
+        break;
+      }
+      if (p.ew > thr) break;   /* split3 copies resample until the gain exceeds the trigger */
+      if (++guard > MAX_REJECT) { LC_ADD(lc, C2D_CNT_ABORTED); break; }
+    }
+    if (third) {
+      ScatRec r3 = rec;
+      r3.key = p.key;
+      r3.ctr = p.ctr;
+      push_scat(P, A.q3_out, A.n3_out, r3);
+    } else {
+      const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
+      atomicAdd(&P.T[P.off.edep + cell], p.ew - ewold);
+      atomicAdd(&eic_lds[i_gam], p.ew - ewold);
+      if (p.phi > twopi) p.phi = p.phi - twopi;
+      const unsigned long long slot = wave_reserve(A.n_pk);
+      if (slot < (unsigned long long)P.cap_pk) store_pk(P.pk, (int64_t)slot, p);
+      else atomicOr(P.err, ERR_QUEUE);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C2D_NUM_NT + 2; i += SBLOCK) {
+    if (nel_lds[i] != 0.0) atomicAdd(&P.T[P.off.nelectron + i], nel_lds[i]);
+    if (eic_lds[i] != 0.0) atomicAdd(&P.T[P.off.E_IC + i], eic_lds[i]);
+  }
+  flush_counters(P, lc, lane_id());
+}
+
+/* a generation-0 source record: census packet (imcfield2d.f:98-117) or a
+ * sampled volume/surface packet from the packet store */
+__device__ __forceinline__ void load_source(const KParams& P, Pkt& p, long long item) {
+  if (item < P.n_cens_items) {
+    const int64_t i = item;
+    p.rpre = P.cin.rpre[i]; p.zpre = P.cin.zpre[i];
+    p.wmu = clampd(P.cin.wmu[i], 0.99999999);
+    p.phi = P.cin.phi[i]; p.ew = P.cin.ew[i]; p.xnu = P.cin.xnu[i];
+    const uint32_t jk = P.cin.jk[i], bn = P.cin.bins[i];
+    p.jph = (int32_t)(jk >> 16); p.kph = (int32_t)(jk & 0xffffu);
+    p.jgpsp = (int32_t)(bn & 0xffu); p.jgplc = (int32_t)((bn >> 8) & 0xffu);
+    p.jgpmu = (int32_t)((bn >> 16) & 0xffu);
+    p.key = P.cin.key[i];
+    p.dcen = P.cdt;                                    /* imcfield2d.f:117 */
+    p.kap = 0;
+  } else {
+    load_pk(p, P.pk, item - P.n_cens_items);
+  }
+}
 
 /* ------------------------------------------------------------------ */
 /* the transport kernel                                                */
 /* ------------------------------------------------------------------ */
-__global__ void __launch_bounds__(BLOCK) C2D_SFX(c2d_transport_kernel)(const KParams* __restrict__ Pg) {
+__global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kernel)(const KParams* __restrict__ Pg,
+                                                                      const GenArgs A) {
   const KParams& P = *Pg;
   extern __shared__ double lds[];
   const int tid = threadIdx.x;
@@ -938,20 +1193,22 @@ __global__ void __launch_bounds__(BLOCK) C2D_SFX(c2d_transport_kernel)(const KPa
     for (int i = tid; i < GEO_DOUBLES; i += BLOCK) lds[i] = gsrc[i];
     for (int i = tid; i < (int)(cur - cells_lds); i += BLOCK) cells_lds[i] = 0.0;
   }
+  __shared__ uint32_t cnt_lds[C2D_NCOUNTERS];
+  init_counters(cnt_lds);
   __syncthreads();
+  const long long n_items = A.gen == 0 ? (long long)A.n_items : (long long)rfl64(*A.n_pk);
 
   Pkt p;
   p.mode = 0; p.kap = 0; p.ctr = 0; p.key = 0; p.nflight = 0;
-  /* source save of the split1 loop (imctrk2d.f:106-123) */
-  double s_xnu = 0, s_wmu = 0, s_phi = 0, s_rpre = 0, s_zpre = 0, s_dcen = 0, s_ew = 0, s_wtmin = 0;
-  int32_t s_jph = 0, s_kph = 0, s_bins = 0;
-  uint64_t s_key = 0;
+  /* The split1 loop (imctrk2d.f:106-123) restarts every copy from the source
+   * record, which stays in memory (census store / packet store) for the whole
+   * launch: it is re-read instead of being held in registers. */
+  long long src_item = 0;
   int32_t state = ST_IDLE, probe = 0, nscat = 0;
   ComCache cc = {-1, -1, 0.0, 0.0};
-  LaneCnt lc = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  LaneCnt lc = {0u, cnt_lds};
   long long chunk_base = 0, chunk_end = 0;
   bool exhausted = false;
-  const double twopi = 2.0 * PI_REF;
 
   for (;;) {
     /* ---- refill idle lanes: chunked, wave-aggregated work fetch ---- */
@@ -962,11 +1219,11 @@ __global__ void __launch_bounds__(BLOCK) C2D_SFX(c2d_transport_kernel)(const KPa
       while (needm != 0ull) {
         if (chunk_base >= chunk_end) {
           unsigned long long nb = 0;
-          if (lane == 0) nb = atomicAdd(P.work_counter, (unsigned long long)CHUNK);
+          if (lane == 0) nb = atomicAdd(A.work_counter, (unsigned long long)CHUNK);
           nb = rfl64(nb);
-          if ((long long)nb >= P.n_items) { exhausted = true; break; }
+          if ((long long)nb >= n_items) { exhausted = true; break; }
           chunk_base = (long long)nb;
-          chunk_end = chunk_base + CHUNK < P.n_items ? chunk_base + CHUNK : P.n_items;
+          chunk_end = chunk_base + CHUNK < n_items ? chunk_base + CHUNK : n_items;
         }
         const long long avail = chunk_end - chunk_base;
         const unsigned long long lt = (lane == 0) ? 0ull : (needm & ((~0ull) >> (64 - lane)));
@@ -981,149 +1238,58 @@ __global__ void __launch_bounds__(BLOCK) C2D_SFX(c2d_transport_kernel)(const KPa
       }
     }
     if (got) {
-      /* ---- initialise the work item ---- */
-      int start_source = 0;
-      if (P.gen == 0) {
-        if (item < P.n_cens_items) {
-          const int64_t i = item;
-          p.rpre = P.cin.rpre[i]; p.zpre = P.cin.zpre[i]; p.wmu = P.cin.wmu[i];
-          p.phi = P.cin.phi[i]; p.ew = P.cin.ew[i]; p.xnu = P.cin.xnu[i];
-          const uint32_t jk = P.cin.jk[i], bn = P.cin.bins[i];
-          p.jph = (int32_t)(jk >> 16); p.kph = (int32_t)(jk & 0xffffu);
-          p.jgpsp = (int32_t)(bn & 0xffu); p.jgplc = (int32_t)((bn >> 8) & 0xffu);
-          p.jgpmu = (int32_t)((bn >> 16) & 0xffu);
-          p.key = P.cin.key[i]; p.ctr = 0;
-          p.dcen = P.cdt;                                    /* imcfield2d.f:117 */
-          p.wmu = clampd(p.wmu, 0.99999999);
-          p.kap = 0;
-          start_source = 1;
-        } else if (item < P.n_cens_items + P.n_vol_items) {
-          const int64_t gidx = (item - P.n_cens_items) * P.world + P.rank;
-          const int cell = upper_index(P.vol_prefix, P.ncell, gidx);
-          const int64_t n = gidx - P.vol_prefix[cell];
-          p.key = c2d_derive(P.step_key, C2D_TAG_VOL, (uint32_t)n, (uint32_t)cell);
-          p.ctr = 0;
-          p.kap = 0;
-          vol_source(P, T, p, cell / P.nr + 1, cell % P.nr + 1);
-          start_source = 1;
-        } else {
-          const int64_t gidx = (item - P.n_cens_items - P.n_vol_items) * P.world + P.rank;
-          const int slot = upper_index(P.surf_prefix, P.nslot, gidx);
-          const int64_t n = gidx - P.surf_prefix[slot];
-          int side, s1;
-          if (slot < 2 * P.nz) { side = slot & 1; s1 = slot / 2 + 1; }
-          else { side = 2 + ((slot - 2 * P.nz) & 1); s1 = (slot - 2 * P.nz) / 2 + 1; }
-          p.key = c2d_derive(P.step_key, C2D_TAG_SURF + (uint32_t)side, (uint32_t)n,
-                             (uint32_t)(s1 - 1));
-          p.ctr = 0;
-          p.kap = 1;
-          surf_source(P, T, p, side, s1, slot);
-          start_source = 1;
-        }
-      } else {
-        const int64_t n2items = P.n2_in * P.split2;
-        if (item < n2items) {
-          /* split2 copy ii of a collision (imctrk2d.f:611-679) */
-          const ScatRec rec = P.q2_in[item / P.split2];
-          const uint32_t ii = (uint32_t)(item % P.split2);
-          load_rec(p, rec);
-          const double ewcsv = rec.ew / P.split2;
-          p.ew = ewcsv;
-          p.key = c2d_derive(rec.key, C2D_TAG_SCAT2, ii, rec.ctr);
-          p.ctr = 0;
-          double ewold = p.ew;
-          int i_gam = compb2d(P, T, p, lc);
-          if (p.ew > ewold * P.split2 * P.split1 * P.spl3_trg) {
-            /* third split (imctrk2d.f:631-661): resampled in the next generation */
-            ScatRec r3 = rec;
-            r3.key = p.key;
-            r3.ctr = p.ctr;
-            push_scat(P, P.q3_out, P.n3_out, r3);
-          } else {
-            const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
-            atomicAdd(&T_EDEP(P, T)[cell], p.ew - ewold);
-            atomicAdd(&P.T[P.off.E_IC + i_gam], p.ew - ewold);
-            if (p.phi > twopi) p.phi = p.phi - twopi;
-            p.mode = 1;
-            p.wtmin = 1.0e-10 * p.ew;
-            p.nflight = 0;
-            cc.cell0 = -1; cc.cell1 = -1;
-            state = ST_TRACK;
-          }
-        } else {
-          /* split3 copy ii2 (imctrk2d.f:633-661) */
-          const int64_t it3 = item - n2items;
-          const ScatRec rec = P.q3_in[it3 / P.split3];
-          const uint32_t ii2 = (uint32_t)(it3 % P.split3);
-          const double ewcsv = rec.ew / P.split2;
-          const double ewold = ewcsv / P.split3;
-          p.key = c2d_derive(rec.key, C2D_TAG_SCAT3, ii2, rec.ctr);
-          p.ctr = 0;
-          int i_gam, guard = 0;
-          do {
-            load_rec(p, rec);
-            p.ew = ewcsv / P.split3;
-            i_gam = compb2d(P, T, p, lc);
-            if (++guard > MAX_REJECT) { lc.aborted++; break; }
-          } while (p.ew <= ewold * P.split2 * P.split1 * P.spl3_trg);
-          const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
-          atomicAdd(&T_EDEP(P, T)[cell], p.ew - ewold);
-          atomicAdd(&P.T[P.off.E_IC + i_gam], p.ew - ewold);
-          if (p.phi > twopi) p.phi = p.phi - twopi;
-          p.mode = 1;
-          p.wtmin = 1.0e-10 * p.ew;
-          p.nflight = 0;
-          cc.cell0 = -1; cc.cell1 = -1;
-          state = ST_TRACK;
-        }
-      }
-      if (start_source) {
-        /* imctrk2d(-1) entry (imctrk2d.f:91,106-123) */
-        lc.sources++;
-        s_key = p.key;
-        s_wtmin = 1.0e-10 * p.ew;
-        s_ew = p.ew / P.split1;
-        s_xnu = p.xnu; s_wmu = p.wmu; s_phi = p.phi; s_rpre = p.rpre; s_zpre = p.zpre;
-        s_dcen = p.dcen; s_jph = p.jph; s_kph = p.kph;
-        s_bins = p.jgpsp | (p.jgplc << 8) | (p.jgpmu << 16);
-        p.ew = s_ew;
-        p.wtmin = s_wtmin;
+      if (A.gen == 0) {
+        /* imctrk2d(-1) entry (imctrk2d.f:91,106-123): first probe copy */
+        LC_ADD(lc, C2D_CNT_SOURCES);
+        src_item = item;
+        load_source(P, p, item);
+        p.wtmin = 1.0e-10 * p.ew;
+        p.ew = p.ew / P.split1;
         p.mode = -1;
-        p.key = c2d_derive(s_key, C2D_TAG_PROBE, 0u, 0u);
+        p.key = c2d_derive(p.key, C2D_TAG_PROBE, 0u, 0u);
         p.ctr = 0;
-        p.nflight = 0;
         probe = 0;
         nscat = 0;
-        cc.cell0 = -1; cc.cell1 = -1;
         state = ST_PROBE;
+      } else {
+        /* a scatter secondary, tracked as imctrk2d(1) (imctrk2d.f:662-679) */
+        load_pk(p, P.pk, item);
+        p.mode = 1;
+        p.wtmin = 1.0e-10 * p.ew;
+        state = ST_TRACK;
       }
+      p.nflight = 0;
+      cc.cell0 = -1; cc.cell1 = -1;
+      cache_energy(P, T.g, p);
+      set_phi(p, p.phi);
     }
     if (exhausted && __ballot(state != ST_IDLE) == 0ull) break;
     if (state != ST_IDLE) {
       const int out = flight(P, T, p, cc, lc);
       if (out != FL_CONT) {
         if (out == FL_COLLIDE) {
-          push_scat(P, P.q2_out, P.n2_out, make_rec(p, p.key, p.ctr));
+          push_scat(P, A.q2_out, A.n2_out, make_rec(p, p.key, p.ctr));
           if (state == ST_PROBE) nscat++;
         }
         if (state == ST_PROBE) {
           probe++;
           if (probe < P.split1 || P.split1 - nscat > 0) {
-            p.xnu = s_xnu; p.wmu = s_wmu; p.phi = s_phi; p.rpre = s_rpre; p.zpre = s_zpre;
-            p.dcen = s_dcen; p.jph = s_jph; p.kph = s_kph;
-            p.jgpsp = s_bins & 0xff; p.jgplc = (s_bins >> 8) & 0xff; p.jgpmu = (s_bins >> 16) & 0xff;
+            load_source(P, p, src_item);
+            const double ew0 = p.ew;
+            const double s_ew = ew0 / P.split1;
             p.ctr = 0;
             p.nflight = 0;
+            set_phi(p, p.phi);   /* same xnu: the energy caches and ComCache stay valid */
             if (probe < P.split1) {
               p.ew = s_ew;
-              p.wtmin = s_wtmin;
-              p.key = c2d_derive(s_key, C2D_TAG_PROBE, (uint32_t)probe, 0u);
+              p.wtmin = 1.0e-10 * ew0;
+              p.key = c2d_derive(p.key, C2D_TAG_PROBE, (uint32_t)probe, 0u);
             } else {
               /* recombined unscattered copies, imctrk2d(0) (imctrk2d.f:690-704) */
               p.ew = (double)(P.split1 - nscat) * s_ew;
               p.wtmin = 1.0e-10 * p.ew;
               p.mode = 0;
-              p.key = c2d_derive(s_key, C2D_TAG_RECOMB, 0u, 0u);
+              p.key = c2d_derive(p.key, C2D_TAG_RECOMB, 0u, 0u);
               state = ST_TRACK;
             }
           } else {
@@ -1152,20 +1318,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_SFX(c2d_transport_kernel)(const KPa
       if (v != 0.0) atomicAdd(&gdst[i], v);
     }
   }
-  const uint32_t c0 = wave_sum(lc.steps), c1 = wave_sum(lc.escapes), c2 = wave_sum(lc.census),
-                 c3 = wave_sum(lc.collide), c4 = wave_sum(lc.killed), c5 = wave_sum(lc.sources),
-                 c6 = wave_sum(lc.compb), c7 = wave_sum(lc.events), c8 = wave_sum(lc.aborted);
-  if (lane == 0) {
-    if (c0) atomicAdd(&P.cnt[C2D_CNT_STEPS], (unsigned long long)c0);
-    if (c1) atomicAdd(&P.cnt[C2D_CNT_ESCAPES], (unsigned long long)c1);
-    if (c2) atomicAdd(&P.cnt[C2D_CNT_CENSUS], (unsigned long long)c2);
-    if (c3) atomicAdd(&P.cnt[C2D_CNT_COLLIDE], (unsigned long long)c3);
-    if (c4) atomicAdd(&P.cnt[C2D_CNT_KILLED], (unsigned long long)c4);
-    if (c5) atomicAdd(&P.cnt[C2D_CNT_SOURCES], (unsigned long long)c5);
-    if (c6) atomicAdd(&P.cnt[C2D_CNT_COMPB], (unsigned long long)c6);
-    if (c7) atomicAdd(&P.cnt[C2D_CNT_EVENTS], (unsigned long long)c7);
-    if (c8) atomicAdd(&P.cnt[C2D_CNT_ABORTED], (unsigned long long)c8);
-  }
+  flush_counters(P, lc, lane);
 }
 
 #if C2D_TABLE_COMTOT
@@ -1230,18 +1383,28 @@ __global__ void __launch_bounds__(256) c2d_comtab_gemm(const double* f_nt, const
 /* ------------------------------------------------------------------ */
 /* launchers (called from capi.cpp)                                    */
 /* ------------------------------------------------------------------ */
-extern "C" int C2D_SFX(c2d_launch_transport)(const c2d::KParams* P_dev, int grid, size_t lds_bytes,
-                                             hipStream_t stream) {
+extern "C" int C2D_SFX(c2d_launch_transport)(const c2d::KParams* P_dev, const c2d::GenArgs* A, int grid,
+                                             size_t lds_bytes, hipStream_t stream) {
   hipLaunchKernelGGL(C2D_SFX(c2d::c2d_transport_kernel), dim3(grid), dim3(c2d::BLOCK), lds_bytes,
-                     stream, P_dev);
+                     stream, P_dev, *A);
   return (int)hipGetLastError();
 }
 
-extern "C" int C2D_SFX(c2d_transport_attrs)(int* block, int* max_lds) {
-  *block = c2d::BLOCK;
-  hipFuncAttributes a;
-  hipError_t e = hipFuncGetAttributes(&a, (const void*)C2D_SFX(c2d::c2d_transport_kernel));
-  *max_lds = (int)a.maxDynamicSharedSizeBytes;
+extern "C" int C2D_SFX(c2d_launch_source)(const c2d::KParams* P_dev, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(C2D_SFX(c2d::c2d_source_kernel), dim3(grid), dim3(c2d::SBLOCK), 0, stream, P_dev);
+  return (int)hipGetLastError();
+}
+
+extern "C" int C2D_SFX(c2d_launch_scatter)(const c2d::KParams* P_dev, const c2d::GenArgs* A, int grid,
+                                           hipStream_t stream) {
+  hipLaunchKernelGGL(C2D_SFX(c2d::c2d_scatter_kernel), dim3(grid), dim3(c2d::SBLOCK), 0, stream, P_dev,
+                     *A);
+  return (int)hipGetLastError();
+}
+
+extern "C" int C2D_SFX(c2d_transport_occupancy)(int* blocks_per_cu, size_t lds_bytes) {
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      blocks_per_cu, C2D_SFX(c2d::c2d_transport_kernel), c2d::BLOCK, lds_bytes);
   return (int)e;
 }
 

@@ -23,7 +23,11 @@ import numpy as np
 
 from . import abi
 
-LIB_PATH = Path(__file__).resolve().parent / "libcompton2d.so"
+import os
+
+# C2D_LIBRARY selects an alternative build of the same library (tuning sweeps)
+LIB_PATH = Path(os.environ.get("C2D_LIBRARY") or
+                Path(__file__).resolve().parent / "libcompton2d.so")
 _lib = None
 
 
