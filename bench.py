@@ -90,14 +90,16 @@ def cpu_baseline(target_s: float = 15.0) -> dict:
 
 
 def load_pmc(workload_key: str):
-    """HBM traffic per generation-0 launch from the committed rocprofv3 PMC summary."""
+    """HBM bytes per packet-step of the generation-0 transport launch, from the
+    committed rocprofv3 PMC summary (tools/gpu_profile.sh + tools/pmc_summary.py:
+    separate FETCH_SIZE and WRITE_SIZE passes, FETCH_SIZE doubled for gfx950)."""
     p = ROOT / "profiles" / "pmc_latest.json"
     if not p.exists():
         return None
     try:
         d = json.loads(p.read_text())
         if d.get("workload_key") == workload_key:
-            return d.get("hbm_bytes_per_launch")
+            return float(d["hbm_bytes_per_step"])
     except Exception:
         return None
     return None
@@ -172,7 +174,9 @@ def main():
     value = steps_global / elapsed
     achieved = g0_steps * BYTES_PER_STEP / (g0_ms * 1e-3) / 1e9 if g0_ms > 0 else 0.0
     workload_key = "c2_%dx%d_%d_%s" % (args.grid, args.grid, args.sources, args.mode)
-    traffic = load_pmc(workload_key)
+    bps = load_pmc(workload_key)
+    # HBM bytes of one generation-0 launch: measured bytes/packet-step x this run's steps/launch
+    traffic = bps * (g0_steps / args.steps) if bps is not None else None
     out = {
         "metric": METRIC,
         "value": value,
@@ -206,6 +210,8 @@ def main():
             "kernel": "c2d_transport_kernel_%s (generation 0)" % args.mode,
             "per_unit_bytes": BYTES_PER_STEP,
             "kernel_ms_avg": g0_ms / args.steps,
+            "traffic_unit": "bytes per launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",
+            "traffic_bytes_per_step": bps,
             "steps_per_launch_avg": g0_steps / args.steps,
         },
         "cpu_baseline": None,

@@ -49,7 +49,7 @@ struct ScatRec {
   uint32_t ctr;      /* RNG counter of the parent (SCAT2) / child (SCAT3) */
   uint64_t key;      /* parent key (SCAT2) / child key (SCAT3)            */
   uint32_t kap;      /* 0: census/volume phase kappa (H3), 1: surface phase */
-  uint32_t pad;
+  uint32_t sub;      /* lineage sub-stream of `key` (c2d_rng.h)           */
 };
 
 /* In-flight packet store, SoA: generation-0 sources sampled by

@@ -5,20 +5,27 @@
  * seed_zone, initialize_rand, fibran, RNFSTR/RNFARR) whose draws depend on
  * the depth-first order in which one worker tracks every packet of a zone.
  * Here every packet owns a Philox4x32-10 stream (key = 64-bit lineage key,
- * counter = draws consumed), and children derive their keys from the
+ * counter = draws consumed, two draws per Philox block), and children derive their keys from the
  * parent's key at the point of the split, so a packet history is the same
  * whatever lane, wave, generation or GPU tracks it.
+ *
+ * A stream is (key, sub): sub = 0 for a packet's own stream, and the split1
+ * copies of a source (which only differ in their random numbers) use
+ * sub-streams of the source key instead of derived keys, so starting a
+ * copy costs no Philox call.
  *
  * Lineage rules (shared by the HIP kernels and the oracle's lineage mode):
  *   step key      S  = derive(seed, TAG_STEP, ncycle, 0)
  *   volume source    = derive(S, TAG_VOL,   n, cell)          n = packet index in zone
  *   surface source   = derive(S, TAG_SURF+side, n, surface)   side 0..3 = i,o,u,l
  *   census source    = key stored in the census record
- *   probe copy p     = derive(K_src, TAG_PROBE, p, 0)         (imctrk2d.f:125 split1 loop)
- *   recombined       = derive(K_src, TAG_RECOMB, 0, 0)        (imctrk2d.f:690-704)
- *   scatter copy ii  = derive(K_par, TAG_SCAT2, ii, ctr_par)  (imctrk2d.f:611 split2 loop)
- *   split3 copy ii2  = derive(K_chd, TAG_SCAT3, ii2, ctr_chd) (imctrk2d.f:633 split3 loop)
- *   census key       = derive(K_pkt, TAG_CENSUS, ctr_pkt, 0)  (imctrk2d.f:571 new seed)
+ *   probe copy p     = (K_src, sub 1+p)                       (imctrk2d.f:125 split1 loop)
+ *   recombined       = (K_src, sub C2D_SUB_RECOMB)            (imctrk2d.f:690-704)
+ *   scatter copy ii  = derive(K_par, TAG_SCAT2, ii, ctr_par; sub_par)  (imctrk2d.f:611)
+ *   split3 copy ii2  = derive(K_chd, TAG_SCAT3, ii2, ctr_chd)          (imctrk2d.f:633)
+ *   census key       = derive(K_pkt, TAG_CENSUS, ctr_pkt, 0; sub_pkt)  (imctrk2d.f:571)
+ * Draw n of (key, sub) is half (n & 1) of Philox_key({n >> 1, sub, 0, C_DRAW});
+ * derive(key, tag, a, b; sub) = Philox_key({a, b, tag | sub << 8, C_DERIVE}).
  */
 #ifndef C2D_RNG_H
 #define C2D_RNG_H
@@ -34,8 +41,6 @@
 #define C2D_TAG_STEP    0x01u
 #define C2D_TAG_VOL     0x02u
 #define C2D_TAG_SURF    0x03u   /* + side (0..3) */
-#define C2D_TAG_PROBE   0x07u
-#define C2D_TAG_RECOMB  0x08u
 #define C2D_TAG_SCAT2   0x09u
 #define C2D_TAG_SCAT3   0x0Au
 #define C2D_TAG_CENSUS  0x0Bu
@@ -66,17 +71,35 @@ C2D_RHD double c2d_u01_bits(uint32_t a, uint32_t b) {
   return ((double)x + 0.5) * 1.1102230246251565404e-16;   /* 2^-53 */
 }
 
-/* Draw number n of stream `key`. */
-C2D_RHD double c2d_draw(uint64_t key, uint32_t n) {
-  uint32_t c[4] = {n, 0u, 0u, C2D_DRAW_C3};
+#define C2D_SUB_RECOMB  0xFFFFFFu   /* 24-bit sub-stream ids: probes use 1 .. split1 */
+
+/* Draw number n of stream (key, sub).  One Philox block gives two uniforms:
+ * draws 2m and 2m+1 are the low and high halves of block m, so a tracker
+ * that keeps the high half (c2d_draw_pair) pays one block per two draws. */
+C2D_RHD double c2d_draw_s(uint64_t key, uint32_t sub, uint32_t n) {
+  uint32_t c[4] = {n >> 1, sub, 0u, C2D_DRAW_C3};
   c2d_philox(c, (uint32_t)key, (uint32_t)(key >> 32));
+  return (n & 1u) ? c2d_u01_bits(c[2], c[3]) : c2d_u01_bits(c[0], c[1]);
+}
+
+C2D_RHD double c2d_draw(uint64_t key, uint32_t n) { return c2d_draw_s(key, 0u, n); }
+
+/* Both draws of block m = n >> 1 (n even): returns draw n, *next = draw n+1. */
+C2D_RHD double c2d_draw_pair(uint64_t key, uint32_t sub, uint32_t n, double* next) {
+  uint32_t c[4] = {n >> 1, sub, 0u, C2D_DRAW_C3};
+  c2d_philox(c, (uint32_t)key, (uint32_t)(key >> 32));
+  *next = c2d_u01_bits(c[2], c[3]);
   return c2d_u01_bits(c[0], c[1]);
 }
 
-C2D_RHD uint64_t c2d_derive(uint64_t key, uint32_t tag, uint32_t a, uint32_t b) {
-  uint32_t c[4] = {a, b, tag, C2D_DERIVE_C3};
+C2D_RHD uint64_t c2d_derive_s(uint64_t key, uint32_t tag, uint32_t a, uint32_t b, uint32_t sub) {
+  uint32_t c[4] = {a, b, tag | (sub << 8), C2D_DERIVE_C3};
   c2d_philox(c, (uint32_t)key, (uint32_t)(key >> 32));
   return ((uint64_t)c[1] << 32) | (uint64_t)c[0];
+}
+
+C2D_RHD uint64_t c2d_derive(uint64_t key, uint32_t tag, uint32_t a, uint32_t b) {
+  return c2d_derive_s(key, tag, a, b, 0u);
 }
 
 C2D_RHD uint64_t c2d_step_key(uint64_t seed, int32_t ncycle) {

@@ -92,7 +92,9 @@ struct Pkt {
 #endif
   int32_t jph, kph, jgpsp, jgplc, jgpmu, mode, kap;
   int32_t ie;         /* E_ph bin of xnu (imctrk2d.f:382-384), cached per xnu     */
+  double rnext;       /* draw ctr of `key` when ctr is odd (second half of a block) */
   uint64_t key;
+  uint32_t sub;       /* lineage sub-stream: split1 copies of a source (c2d_rng.h) */
   uint32_t ctr;
   uint32_t nflight;   /* safety cap: a history that stops progressing is aborted */
 };
@@ -129,7 +131,18 @@ struct Tal {
 #define T_ERLKU(P, T) (T_ERLKI(P, T) + 2 * (P).nz)
 #define T_ERLKL(P, T) (T_ERLKI(P, T) + 2 * (P).nz + (P).nr)
 
-__device__ __forceinline__ double U(Pkt& p) { return c2d_draw(p.key, p.ctr++); }
+/* Next draw of the packet's stream.  Every key change sets ctr = 0, except a
+ * packet loaded from a record mid-stream, which calls rng_sync first. */
+__device__ __forceinline__ double U(Pkt& p) {
+  double v;
+  if (p.ctr & 1u) v = p.rnext;
+  else v = c2d_draw_pair(p.key, p.sub, p.ctr, &p.rnext);
+  p.ctr++;
+  return v;
+}
+__device__ __forceinline__ void rng_sync(Pkt& p) {
+  if (p.ctr & 1u) p.rnext = c2d_draw_s(p.key, p.sub, p.ctr);
+}
 
 __device__ __forceinline__ double clampd(double v, double lim) {
   if (v > lim) v = lim;
@@ -510,7 +523,7 @@ __device__ __forceinline__ void census_write(const KParams& P, const Tal& T, con
     P.cout.xnu[slot] = p.xnu;
     P.cout.jk[slot] = ((uint32_t)p.jph << 16) | (uint32_t)p.kph;
     P.cout.bins[slot] = (uint32_t)p.jgpsp | ((uint32_t)p.jgplc << 8) | ((uint32_t)p.jgpmu << 16);
-    P.cout.key[slot] = c2d_derive(p.key, C2D_TAG_CENSUS, p.ctr, 0u);
+    P.cout.key[slot] = c2d_derive_s(p.key, C2D_TAG_CENSUS, p.ctr, 0u, p.sub);
   } else {
     atomicOr(P.err, ERR_CENSUS);
   }
@@ -534,7 +547,7 @@ __device__ __forceinline__ ScatRec make_rec(const Pkt& p, uint64_t key, uint32_t
   r.ctr = ctr;
   r.key = key;
   r.kap = (uint32_t)p.kap;
-  r.pad = 0;
+  r.sub = p.sub;
   return r;
 }
 
@@ -589,13 +602,9 @@ struct ComCache {
 __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, ComCache& cc, LaneCnt& lc) {
   const double lim8 = 9.9999999e-1, lim9 = 0.999999999;
   const Geo* g = T.g;
-  double mb_ran;
-  if (p.mode == 0) {
-    mb_ran = 1.0e-10;
-  } else {
-    mb_ran = U(p);   /* Philox uniform is never 0: the `goto 100` redraw cannot trigger */
-  }
-  double colmfp = -c2d_log(mb_ran);
+  /* mode 0 uses mb_ran = 1e-10 (imctrk2d.f:150) but never reads colmfp (dcol below) */
+  double colmfp = 0.0;
+  if (p.mode != 0) colmfp = -c2d_log(U(p));   /* Philox uniform is never 0: no `goto 100` redraw */
   if (p.ew < 1.0e-40) return FL_END;
   if (++p.nflight > MAX_FLIGHTS) {
     LC_ADD(lc, C2D_CNT_ABORTED);
@@ -1018,6 +1027,7 @@ __device__ __forceinline__ void load_pk(Pkt& p, const PktSoA& s, int64_t i) {
   p.jgpmu = (int32_t)((bn >> 16) & 0xffu); p.kap = (int32_t)(bn >> 24);
   p.ctr = s.ctr[i];
   p.key = s.key[i];
+  p.sub = 0;
 }
 
 }  // namespace
@@ -1040,6 +1050,7 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_source_kernel)(const KPara
   for (int64_t it = (int64_t)blockIdx.x * SBLOCK + threadIdx.x; it < n; it += stride) {
     Pkt p;
     p.ctr = 0;
+    p.sub = 0;
     if (it < P.n_vol_items) {
       const int64_t gidx = it * P.world + P.rank;
       const int cell = upper_index(P.vol_prefix, P.ncell, gidx);
@@ -1059,7 +1070,7 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_source_kernel)(const KPara
       p.kap = 1;
       surf_source(P, g, p, side, s1, slot);
     }
-    p.ctr = 0;   /* a source's own draws are done: its copies use derived keys */
+    p.ctr = 0;   /* a source's own draws are done: its copies use sub-streams */
     store_pk(P.pk, it, p);
   }
 }
@@ -1105,7 +1116,8 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
     /* split2 copy: ew = ewcsv; split3 copy: ew = ewcsv / split3 (imctrk2d.f:611,636) */
     const double ewold = is2 ? ewcsv : ewcsv / P.split3;
     const double thr = ewold * P.split2 * P.split1 * P.spl3_trg;
-    p.key = c2d_derive(rec.key, is2 ? C2D_TAG_SCAT2 : C2D_TAG_SCAT3, ii, rec.ctr);
+    p.key = c2d_derive_s(rec.key, is2 ? C2D_TAG_SCAT2 : C2D_TAG_SCAT3, ii, rec.ctr, rec.sub);
+    p.sub = 0;
     p.ctr = 0;
     int i_gam = 0, guard = 0;
     bool third = false;
@@ -1124,6 +1136,7 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
       ScatRec r3 = rec;
       r3.key = p.key;
       r3.ctr = p.ctr;
+      r3.sub = 0;
       push_scat(P, A.q3_out, A.n3_out, r3);
     } else {
       const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
@@ -1156,6 +1169,7 @@ __device__ __forceinline__ void load_source(const KParams& P, Pkt& p, long long 
     p.jgpsp = (int32_t)(bn & 0xffu); p.jgplc = (int32_t)((bn >> 8) & 0xffu);
     p.jgpmu = (int32_t)((bn >> 16) & 0xffu);
     p.key = P.cin.key[i];
+    p.sub = 0;
     p.dcen = P.cdt;                                    /* imcfield2d.f:117 */
     p.kap = 0;
   } else {
@@ -1199,11 +1213,14 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
   const long long n_items = A.gen == 0 ? (long long)A.n_items : (long long)rfl64(*A.n_pk);
 
   Pkt p;
-  p.mode = 0; p.kap = 0; p.ctr = 0; p.key = 0; p.nflight = 0;
+  p.mode = 0; p.kap = 0; p.ctr = 0; p.key = 0; p.sub = 0; p.nflight = 0;
   /* The split1 loop (imctrk2d.f:106-123) restarts every copy from the source
    * record, which stays in memory (census store / packet store) for the whole
    * launch: it is re-read instead of being held in registers. */
   long long src_item = 0;
+#if C2D_TABLE_COMTOT
+  double s_eta = 1.0;     /* cos(phi) of the source, reused by every copy */
+#endif
   int32_t state = ST_IDLE, probe = 0, nscat = 0;
   ComCache cc = {-1, -1, 0.0, 0.0};
   LaneCnt lc = {0u, cnt_lds};
@@ -1246,7 +1263,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
         p.wtmin = 1.0e-10 * p.ew;
         p.ew = p.ew / P.split1;
         p.mode = -1;
-        p.key = c2d_derive(p.key, C2D_TAG_PROBE, 0u, 0u);
+        p.sub = 1u;
         p.ctr = 0;
         probe = 0;
         nscat = 0;
@@ -1254,6 +1271,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
       } else {
         /* a scatter secondary, tracked as imctrk2d(1) (imctrk2d.f:662-679) */
         load_pk(p, P.pk, item);
+        rng_sync(p);
         p.mode = 1;
         p.wtmin = 1.0e-10 * p.ew;
         state = ST_TRACK;
@@ -1262,6 +1280,9 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
       cc.cell0 = -1; cc.cell1 = -1;
       cache_energy(P, T.g, p);
       set_phi(p, p.phi);
+#if C2D_TABLE_COMTOT
+      s_eta = p.eta;
+#endif
     }
     if (exhausted && __ballot(state != ST_IDLE) == 0ull) break;
     if (state != ST_IDLE) {
@@ -1279,17 +1300,21 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
             const double s_ew = ew0 / P.split1;
             p.ctr = 0;
             p.nflight = 0;
-            set_phi(p, p.phi);   /* same xnu: the energy caches and ComCache stay valid */
+            /* same xnu and phi: the energy caches, ComCache and cos(phi) stay valid */
+#if C2D_TABLE_COMTOT
+            p.eta = s_eta;
+            p.esw = (p.phi <= PI_REF && p.phi >= 1.0e-10) ? 1 : -1;
+#endif
             if (probe < P.split1) {
               p.ew = s_ew;
               p.wtmin = 1.0e-10 * ew0;
-              p.key = c2d_derive(p.key, C2D_TAG_PROBE, (uint32_t)probe, 0u);
+              p.sub = 1u + (uint32_t)probe;
             } else {
               /* recombined unscattered copies, imctrk2d(0) (imctrk2d.f:690-704) */
               p.ew = (double)(P.split1 - nscat) * s_ew;
               p.wtmin = 1.0e-10 * p.ew;
               p.mode = 0;
-              p.key = c2d_derive(p.key, C2D_TAG_RECOMB, 0u, 0u);
+              p.sub = C2D_SUB_RECOMB;
               state = ST_TRACK;
             }
           } else {

@@ -92,6 +92,7 @@ typedef struct rng {
   uint64_t key;
   uint32_t ctr;
   fibstate* fs;
+  uint32_t sub;     /* lineage sub-stream (c2d_rng.h) */
 } rng_t;
 
 /* RNFARR (rand.f:230-255) */
@@ -208,7 +209,7 @@ static double fibran(fibstate* s) {
 }
 
 static double U(rng_t* g) {
-  if (g->mode == C2O_RNG_LINEAGE) return c2d_draw(g->key, g->ctr++);
+  if (g->mode == C2O_RNG_LINEAGE) return c2d_draw_s(g->key, g->sub, g->ctr++);
   if (g->mode == C2O_RNG_RAN1) return ran1(g->fs, &g_ran1_seed);
   return fibran(g->fs);
 }
@@ -216,8 +217,19 @@ static double U(rng_t* g) {
 static rng_t rng_child(const rng_t* g, uint32_t tag, uint32_t a, uint32_t b) {
   rng_t c = *g;
   if (g->mode == C2O_RNG_LINEAGE) {
-    c.key = c2d_derive(g->key, tag, a, b);
+    c.key = c2d_derive_s(g->key, tag, a, b, g->sub);
     c.ctr = 0;
+    c.sub = 0;
+  }
+  return c;
+}
+
+/* split1 copies: sub-streams of the source stream (c2d_rng.h) */
+static rng_t rng_sub(const rng_t* g, uint32_t sub) {
+  rng_t c = *g;
+  if (g->mode == C2O_RNG_LINEAGE) {
+    c.ctr = 0;
+    c.sub = sub;
   }
   return c;
 }
@@ -672,7 +684,7 @@ static void census_write(c2o_ctx* c, pkt_t* p, rng_t* g) {
   q->i[0] = p->jgpsp; q->i[1] = p->jgplc; q->i[2] = p->jgpmu;
   q->i[3] = p->jph; q->i[4] = p->kph;
   if (g->mode == C2O_RNG_LINEAGE)
-    q->key = c2d_derive(g->key, C2D_TAG_CENSUS, g->ctr, 0u);
+    q->key = c2d_derive_s(g->key, C2D_TAG_CENSUS, g->ctr, 0u, g->sub);
   else
     q->key = (uint64_t)(int64_t)(int32_t)(U(g) * 1.0e5);
   TALLY(c, counters + C2D_CNT_CENSUS) += 1.0;
@@ -901,7 +913,7 @@ static void imctrk2d(c2o_ctx* c, pkt_t* p, int scat_flag, rng_t* g) {
   for (int it = 0; it < niter; it++) {
     *p = sv;
     if (scat_flag == -1) {
-      rng_t gp = rng_child(g, C2D_TAG_PROBE, (uint32_t)it, 0u);
+      rng_t gp = rng_sub(g, 1u + (uint32_t)it);
       rng_t* gpp = (g->mode == C2O_RNG_LINEAGE) ? &gp : g;
       nscat += flight_loop(c, p, -1, gpp, wtmin);
     } else {
@@ -911,7 +923,7 @@ static void imctrk2d(c2o_ctx* c, pkt_t* p, int scat_flag, rng_t* g) {
   if (c->split1 - nscat > 0 && scat_flag == -1) {
     *p = sv;
     p->ew = (double)(c->split1 - nscat) * sv.ew;
-    rng_t gr = rng_child(g, C2D_TAG_RECOMB, 0u, 0u);
+    rng_t gr = rng_sub(g, C2D_SUB_RECOMB);
     imctrk2d(c, p, 0, (g->mode == C2O_RNG_LINEAGE) ? &gr : g);
   }
 }
@@ -1468,6 +1480,10 @@ double c2o_unit_planck(c2o_ctx* c, double tpl, double wmu, int32_t* bins) {
   return P.xnu;
 }
 double c2o_unit_philox_draw(uint64_t key, uint32_t n) { return c2d_draw(key, n); }
+double c2o_unit_philox_draw_s(uint64_t key, uint32_t sub, uint32_t n) { return c2d_draw_s(key, sub, n); }
+uint64_t c2o_unit_derive_s(uint64_t key, uint32_t tag, uint32_t a, uint32_t b, uint32_t sub) {
+  return c2d_derive_s(key, tag, a, b, sub);
+}
 uint64_t c2o_unit_derive(uint64_t key, uint32_t tag, uint32_t a, uint32_t b) {
   return c2d_derive(key, tag, a, b);
 }

@@ -76,6 +76,10 @@ def load(flavor: str = "ref") -> C.CDLL:
     lib.c2o_unit_planck.argtypes = [C.c_void_p, C.c_double, C.c_double, C.POINTER(C.c_int32)]
     lib.c2o_unit_philox_draw.restype = C.c_double
     lib.c2o_unit_philox_draw.argtypes = [C.c_uint64, C.c_uint32]
+    lib.c2o_unit_philox_draw_s.restype = C.c_double
+    lib.c2o_unit_philox_draw_s.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
+    lib.c2o_unit_derive_s.restype = C.c_uint64
+    lib.c2o_unit_derive_s.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
     lib.c2o_unit_derive.restype = C.c_uint64
     lib.c2o_unit_derive.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
     lib.c2o_is_detmath.restype = C.c_int

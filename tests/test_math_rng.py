@@ -60,12 +60,24 @@ def test_philox_known_answers():
             d = lib.c2o_unit_derive(key, tag, a, b)
             w = philox_py((a, b, tag, 0x9E3779B9), (key & 0xffffffff, key >> 32))
             assert d == (w[1] << 32) | w[0]
-        for n in (0, 1, 17, 1 << 20):
+        for n in (0, 1, 2, 17, 1 << 20, (1 << 20) + 1):
             u = lib.c2o_unit_philox_draw(key, n)
-            w = philox_py((n, 0, 0, 0x5EEDD1CE), (key & 0xffffffff, key >> 32))
-            x = (((w[0] << 32) | w[1]) >> 11)
+            # draws 2m, 2m+1 = low / high half of Philox block m
+            w = philox_py((n >> 1, 0, 0, 0x5EEDD1CE), (key & 0xffffffff, key >> 32))
+            hi, lo = (w[2], w[3]) if n & 1 else (w[0], w[1])
+            x = (((hi << 32) | lo) >> 11)
             assert u == (x + 0.5) * 2.0 ** -53
             assert 0.0 < u < 1.0
+        # sub-streams (split1 copies) and sub-stream derivations
+        for sub in (1, 7, 0xFFFFFF):
+            for n in (0, 1, 5):
+                u = lib.c2o_unit_philox_draw_s(key, sub, n)
+                w = philox_py((n >> 1, sub, 0, 0x5EEDD1CE), (key & 0xffffffff, key >> 32))
+                hi, lo = (w[2], w[3]) if n & 1 else (w[0], w[1])
+                assert u == ((((hi << 32) | lo) >> 11) + 0.5) * 2.0 ** -53
+            d = lib.c2o_unit_derive_s(key, 11, 5, 9, sub)
+            w = philox_py((5, 9, 11 | (sub << 8), 0x9E3779B9), (key & 0xffffffff, key >> 32))
+            assert d == (w[1] << 32) | w[0]
 
 
 def philox_py(ctr, key):

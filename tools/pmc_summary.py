@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Summarise tools/gpu_profile.sh output: generation-0 transport dispatches
+(the transport dispatch that follows each c2d_source_kernel dispatch), their
+durations, and the PMC counters of the timed (last) generation-0 dispatch.
+
+FETCH_SIZE / WRITE_SIZE are in KiB summed over the XCDs.  On gfx950
+FETCH_SIZE counts wide streaming reads at half their bytes
+(MI355X_MICROARCH.md §HBM); both raw and x2-corrected fetch bytes are
+reported.  hbm_bytes_per_step = (2*FETCH + WRITE) / packet-steps of that
+dispatch (packet-steps from the bench JSON of the same run)."""
+import csv
+import glob
+import json
+import os
+import sys
+from statistics import mean
+
+
+def find(d, suffix):
+    f = glob.glob(os.path.join(d, "**", "*" + suffix), recursive=True)
+    return f[0] if f else None
+
+
+def dispatches(kt_csv):
+    rows = list(csv.DictReader(open(kt_csv)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    return rows
+
+
+def gen0_ids(rows):
+    ids, after_src = [], False
+    for r in rows:
+        k = r["Kernel_Name"]
+        if "c2d_source_kernel" in k:
+            after_src = True
+        elif "c2d_transport_kernel" in k and after_src:
+            ids.append(r["Dispatch_Id"])
+            after_src = False
+    return ids
+
+
+def counters(d, did):
+    f = find(d, "counter_collection.csv")
+    out = {}
+    if not f:
+        return out
+    for r in csv.DictReader(open(f)):
+        if r["Dispatch_Id"] == did:
+            out[r["Counter_Name"]] = out.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return out
+
+
+def main(root):
+    res = {}
+    kt = find(os.path.join(root, "kt"), "kernel_trace.csv")
+    if kt:
+        rows = dispatches(kt)
+        by = {r["Dispatch_Id"]: r for r in rows}
+        g0 = gen0_ids(rows)
+        dur = [(int(by[i]["End_Timestamp"]) - int(by[i]["Start_Timestamp"])) / 1e6 for i in g0]
+        print("generation-0 transport dispatches: %d; ms: %s" % (len(dur), ", ".join("%.3f" % d for d in dur)))
+        if len(dur) >= 5:
+            print("mean of the last 5 (bench timed steps): %.3f ms" % mean(dur[-5:]))
+            res["gen0_ms_timed_mean"] = mean(dur[-5:])
+        names = {}
+        for r in rows:
+            n = r["Kernel_Name"].split("(")[0]
+            names.setdefault(n, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+        for n, v in sorted(names.items(), key=lambda kv: -sum(kv[1])):
+            print("  %-60s n=%4d total=%9.3f ms mean=%8.3f ms" % (n[:60], len(v), sum(v), mean(v)))
+        r0 = by[g0[-1]] if g0 else rows[0]
+        print("transport: VGPR=%s SGPR=%s scratch=%s LDS=%s grid=%s wg=%s" % (
+            r0.get("VGPR_Count"), r0.get("SGPR_Count"), r0.get("Scratch_Size"),
+            r0.get("LDS_Block_Size"), r0.get("Grid_Size_X"), r0.get("Workgroup_Size_X")))
+    for sub in ("fetch", "write", "sq"):
+        d = os.path.join(root, sub)
+        f = find(d, "kernel_trace.csv")
+        if not f:
+            continue
+        rows = dispatches(f)
+        g0 = gen0_ids(rows)
+        if not g0:
+            continue
+        did = g0[-1]
+        c = counters(d, did)
+        r = [x for x in rows if x["Dispatch_Id"] == did][0]
+        ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        bj = os.path.join(root, "bench_%s.json" % sub)
+        steps = None
+        if os.path.exists(bj):
+            try:
+                steps = json.load(open(bj))["roofline"]["steps_per_launch_avg"]
+            except Exception:
+                steps = None
+        print("[%s] dispatch %s: %.3f ms, packet-steps %s, counters %s" % (sub, did, ms, steps, c))
+        res[sub] = {"ms": ms, "steps": steps, "counters": c}
+    if "fetch" in res and "write" in res and res["fetch"]["steps"] and res["write"]["steps"]:
+        fk = res["fetch"]["counters"].get("FETCH_SIZE", 0.0)
+        wk = res["write"]["counters"].get("WRITE_SIZE", 0.0)
+        fb = fk * 1024.0 * 2.0 / res["fetch"]["steps"]
+        wb = wk * 1024.0 / res["write"]["steps"]
+        res["hbm_bytes_per_step"] = fb + wb
+        print("HBM bytes per packet-step: fetch(x2) %.2f + write %.2f = %.2f" % (fb, wb, fb + wb))
+    if "sq" in res:
+        c = res["sq"]["counters"]
+        w = c.get("SQ_WAVE_CYCLES", 0.0)
+        if w:
+            print("SQ: wait_any %.3f  wait_inst_any %.3f  active_inst_any %.3f  active_valu %.3f" % (
+                c.get("SQ_WAIT_ANY", 0) / w, c.get("SQ_WAIT_INST_ANY", 0) / w,
+                c.get("SQ_ACTIVE_INST_ANY", 0) / w, c.get("SQ_ACTIVE_INST_VALU", 0) / w))
+            st = res["sq"]["steps"]
+            if st:
+                print("per packet-step: VALU insts %.1f  SALU %.1f  VMEM %.2f (wave-instructions x64 / steps)" % (
+                    64 * c.get("SQ_INSTS_VALU", 0) / st, 64 * c.get("SQ_INSTS_SALU", 0) / st,
+                    64 * c.get("SQ_INSTS_VMEM", 0) / st))
+    json.dump(res, open(os.path.join(root, "summary.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
