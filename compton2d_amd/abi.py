@@ -302,3 +302,162 @@ class StepInputs:
         s.spectra = C.cast(arr, C.POINTER(Spectrum))
         s._keep = keep
         return s
+
+
+# ---------------------------------------------------------------------------
+# Fokker-Planck electron update (c2d_fp_config / c2d_fp_step_in / _out)
+# ---------------------------------------------------------------------------
+C2D_E_FP = -8
+ERRORS[C2D_E_FP] = "C2D_E_FP"
+FP_E_OLD, FP_E_NEW, FP_HR, FP_HR_ST, FP_DELTA_T, FP_STEPS, FP_SKIPPED = range(7)
+FP_NDIAG = 8
+
+_d, _i32, _i64 = C.c_double, C.c_int32, C.c_int64
+
+
+class MArray2(C.Structure):
+    _fields_ = [("data", PD), ("s_j", _i64), ("s_k", _i64)]
+
+
+class MArray3(C.Structure):
+    _fields_ = [("data", PD), ("s_i", _i64), ("s_j", _i64), ("s_k", _i64)]
+
+
+class FpConfig(C.Structure):
+    _fields_ = [
+        ("pair_switch", _i32), ("df_implicit", _d), ("df_T", _d), ("r_esc", _d), ("r_acc", _d),
+        ("cf_sentinel", _i32), ("r_flare", _d), ("z_flare", _d), ("t_flare", _d),
+        ("sigma_r", _d), ("sigma_z", _d), ("sigma_t", _d), ("flare_amp", _d),
+        ("inj_switch", _i32), ("inj_dis", _i32), ("g2var_switch", _i32), ("pick_sw", _i32),
+        ("inj_g1", _d), ("inj_g2", _d), ("inj_p", _d), ("inj_t", _d), ("inj_L", _d),
+        ("pick_rate", _d), ("inj_gg", _d), ("inj_sigma", _d), ("inj_v", _d),
+        ("F_IC", PD), ("F_IC_s_i", _i64), ("F_IC_s_ph", _i64),
+    ]
+
+
+class FpStepIn(C.Structure):
+    _fields_ = [
+        ("ncycle", _i32), ("time", _d), ("dt", _d),
+        ("tea", Array2), ("tna", Array2), ("n_e", Array2), ("B_field", Array2),
+        ("Eloss_sy", Array2), ("ec_old", Array2), ("turb_lev", Array2), ("vol", Array2),
+        ("f_pair", Array2), ("ecens", Array2), ("n_field", Array3),
+    ]
+
+
+class FpStepOut(C.Structure):
+    _fields_ = [
+        ("f_nt", MArray3), ("Pnt", MArray3), ("Te_new", MArray2), ("tea", MArray2),
+        ("n_e", MArray2), ("gmin", MArray2), ("gmax", MArray2), ("amxwl", MArray2),
+        ("p_nth", MArray2), ("zone_diag", PD),
+        ("E_tot_old", _d), ("E_tot_new", _d), ("hr_total", _d), ("hr_st_total", _d),
+        ("dT_max", _d),
+    ]
+
+
+@dataclass
+class FpConstants:
+    """FP_calc run constants (src/reader.f:512-559, general.pa:27-28)."""
+    F_IC: np.ndarray                 # [NUM_NT, NPHFIELD] (icloss2d.f)
+    pair_switch: int = 0
+    df_implicit: float = 1.0e-2
+    df_T: float = 2.5e-1
+    r_esc: float = 0.3
+    r_acc: float = 1.0
+    cf_sentinel: int = 0
+    r_flare: float = 0.0
+    z_flare: float = 0.0
+    t_flare: float = 1.0e6
+    sigma_r: float = 1.0e6
+    sigma_z: float = 1.0e6
+    sigma_t: float = 1.0e6
+    flare_amp: float = 0.0
+    inj_switch: int = 0
+    inj_dis: int = 2
+    g2var_switch: int = 0
+    pick_sw: int = 0
+    inj_g1: float = 1.0e2
+    inj_g2: float = 3.0e4
+    inj_p: float = 1.0
+    inj_t: float = 1.2e6
+    inj_L: float = 5.0e40
+    pick_rate: float = 0.8e-3
+    inj_gg: float = 1.0e2
+    inj_sigma: float = 1.0e1
+    g_bulk: float = 33.0
+
+    @property
+    def inj_v(self) -> float:
+        return float(np.sqrt(1.0 - 1.0 / self.g_bulk ** 2) * 2.9979245620e10)   # reader.f:559
+
+    def to_ctypes(self) -> FpConfig:
+        f = np.ascontiguousarray(self.F_IC, dtype=np.float64)
+        assert f.shape == (NUM_NT, NPHFIELD)
+        self._keep = f
+        c = FpConfig()
+        for name, _ in FpConfig._fields_:
+            if name in ("F_IC", "F_IC_s_i", "F_IC_s_ph", "inj_v"):
+                continue
+            setattr(c, name, getattr(self, name))
+        c.inj_v = self.inj_v
+        c.F_IC = _pd(f)
+        c.F_IC_s_i, c.F_IC_s_ph = NPHFIELD, 1
+        return c
+
+
+FP_STATE_KEYS = ("tea", "n_e", "gmin", "gmax", "amxwl", "p_nth")
+FP_INPUT_KEYS = ("tna", "B_field", "Eloss_sy", "ec_old", "turb_lev", "vol", "f_pair", "ecens")
+
+
+class FpCall:
+    """ctypes structs for one c2d_fp_step / c2o_fp_step call.
+
+    `inputs`: zone arrays [nz,nr] for FP_INPUT_KEYS (+ 'n_field' [nz,nr,NPHFIELD];
+    'ecens'/'n_field' may be None = the device tally buffer), plus 'tea' and 'n_e'.
+    `state`: f_nt/Pnt [nz,nr,NUM_NT] and FP_STATE_KEYS zone arrays; copied, the
+    copies are updated in place by the call and returned by result().
+    """
+
+    def __init__(self, ncycle: int, time: float, dt: float, inputs: dict, state: dict):
+        nz, nr = np.asarray(state["tea"]).shape
+        self.nz, self.nr = nz, nr
+        keep = []
+
+        def a2(a):
+            if a is None:
+                return Array2(None, 0, 0)
+            a = np.ascontiguousarray(a, dtype=np.float64)
+            assert a.shape == (nz, nr)
+            keep.append(a)
+            return Array2(_pd(a), nr, 1)
+
+        s = FpStepIn()
+        s.ncycle, s.time, s.dt = int(ncycle), float(time), float(dt)
+        s.tea, s.n_e = a2(state["tea"]), a2(state["n_e"])
+        for k in FP_INPUT_KEYS:
+            setattr(s, k, a2(inputs.get(k)))
+        nf = inputs.get("n_field")
+        if nf is None:
+            s.n_field = Array3(None, 0, 0, 0)
+        else:
+            nf = np.ascontiguousarray(nf, dtype=np.float64)
+            assert nf.shape == (nz, nr, NPHFIELD)
+            keep.append(nf)
+            s.n_field = Array3(_pd(nf), 1, nr * NPHFIELD, NPHFIELD)
+        self.st = {k: np.array(state[k], dtype=np.float64, copy=True) for k in
+                   ("f_nt", "Pnt") + FP_STATE_KEYS}
+        self.st["Te_new"] = np.zeros((nz, nr))
+        self.diag = np.zeros((nz, nr, FP_NDIAG))
+        o = FpStepOut()
+        for k in ("f_nt", "Pnt"):
+            setattr(o, k, MArray3(_pd(self.st[k]), 1, nr * NUM_NT, NUM_NT))
+        for k in FP_STATE_KEYS + ("Te_new",):
+            setattr(o, k, MArray2(_pd(self.st[k]), nr, 1))
+        o.zone_diag = _pd(self.diag)
+        self.sin, self.sout, self._keep = s, o, keep
+
+    def result(self) -> dict:
+        r = dict(self.st)
+        r["zone_diag"] = self.diag
+        for k in ("E_tot_old", "E_tot_new", "hr_total", "hr_st_total", "dT_max"):
+            r[k] = getattr(self.sout, k)
+        return r

@@ -144,6 +144,35 @@ struct GenArgs {
   int32_t gen;
 };
 
+/* ---- Fokker-Planck solve (fp.hip) ---- */
+/* per-zone input record [ncell][FZ_N], packed by the host */
+enum : int32_t {
+  FZ_VOL = 0, FZ_TEA, FZ_TNA, FZ_NE, FZ_B, FZ_ELSY, FZ_ECENS, FZ_ECOLD, FZ_TURB, FZ_FPAIR,
+  FZ_PNTH, FZ_N = 16
+};
+/* per-zone output record [ncell][FO_N]: state, then C2D_FP_NDIAG diagnostics */
+enum : int32_t { FO_TE = 0, FO_NE, FO_GMIN, FO_GMAX, FO_AMXWL, FO_PNTH, FO_DIAG = 8, FO_N = 16 };
+enum : int32_t { FPERR_STEPS = 1, FPERR_GUARD = 2 };
+
+struct FpParams {
+  int32_t nz, nr, pick_sw, inj_switch, inj_dis, g2var_switch, cf_sentinel, pad0;
+  double time, dt, df_implicit, df_T, r_esc, r_acc;
+  double r_flare, z_flare, t_flare, sigma_r, sigma_z, sigma_t, flare_amp;
+  double inj_g1, inj_g2, inj_p, inj_t, inj_L, pick_rate, inj_gg, inj_sigma, inj_v;
+  const Geo* geo;          /* grids: z[0]=zmin, r[0]=rmin, 1-based zones      */
+  const double* gnt;       /* [num_nt]                                         */
+  const double* FT;        /* [nphfield][num_nt]: F_IC transposed               */
+  const double* zin;       /* [ncell][FZ_N]                                    */
+  const double* f_in;      /* [ncell][num_nt]                                  */
+  const double* P_in;      /* [ncell][num_nt]                                  */
+  const double* nf;        /* n_field: nf[cell*nphfield + ph]                  */
+  const double* ecens;     /* [ncell] (tally buffer) or null: zin[FZ_ECENS]     */
+  double* f_out;           /* [ncell][num_nt]                                  */
+  double* P_out;
+  double* zout;            /* [ncell][FO_N]                                    */
+  int32_t* err;
+};
+
 }  // namespace c2d
 
 #endif

@@ -33,6 +33,7 @@ extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t s);
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
                                       double* tab, int ncell, hipStream_t s);
+extern "C" int c2d_launch_fp(const FpParams* P, int ncell, hipStream_t s);
 extern "C" int c2d_launch_tridag(const double* a, const double* b, const double* c,
                                  const double* r, double* x, int ncell, int nt, hipStream_t s);
 
@@ -124,6 +125,13 @@ struct c2d_ctx {
   float last_src_ms = 0.f;
   int64_t last_g0_steps = 0;
   int last_launches = 0;
+  /* Fokker-Planck */
+  bool fp_ready = false;
+  c2d_fp_config fpc;
+  double *fp_FT = nullptr, *fp_zin = nullptr, *fp_fin = nullptr, *fp_Pin = nullptr,
+         *fp_nf = nullptr, *fp_fout = nullptr, *fp_Pout = nullptr, *fp_zout = nullptr;
+  int32_t* fp_err = nullptr;
+  float last_fp_ms = 0.f;
 };
 
 static int fail(c2d_ctx* c, int code, const char* fmt, ...) {
@@ -283,6 +291,10 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
     if (c->cens[b].key) (void)hipFree(c->cens[b].key);
   }
   for (double* p : c->spec_bufs) (void)hipFree(p);
+  void* fptrs[] = {c->fp_FT, c->fp_zin, c->fp_fin, c->fp_Pin, c->fp_nf, c->fp_fout, c->fp_Pout,
+                   c->fp_zout, c->fp_err};
+  for (void* p : fptrs)
+    if (p) (void)hipFree(p);
   c->pk.release();
   if (c->ev_g0a) (void)hipEventDestroy(c->ev_g0a);
   if (c->ev_g0b) (void)hipEventDestroy(c->ev_g0b);
@@ -790,5 +802,172 @@ extern "C" int c2d_last_kernel_ms(c2d_ctx* c, double* gen0_ms, double* all_ms, i
   if (gen0_ms) *gen0_ms = c->last_g0_ms;
   if (all_ms) *all_ms = c->last_all_ms;
   if (launches) *launches = c->last_launches;
+  return C2D_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* Fokker-Planck (src/update2d.f:7-327, FP_calc :337-1739)             */
+/* ------------------------------------------------------------------ */
+extern "C" int c2d_fp_set_config(c2d_ctx* c, const c2d_fp_config* fc) {
+  if (!c || !fc || !fc->F_IC) return C2D_E_ARG;
+  if (fc->pair_switch != 0)
+    return fail(c, C2D_E_ARG, "pair_switch=1 in the FP solve (pa_calc/trid_p) is not supported");
+  if (fc->inj_switch != 0 && fc->inj_dis != 1 && fc->inj_dis != 2)
+    return fail(c, C2D_E_ARG, "inj_dis must be 1 or 2 when inj_switch is on (got %d)", fc->inj_dis);
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const size_t nc = (size_t)c->ncell;
+  if (!c->fp_FT) {
+    HIPCHK(c, dalloc(&c->fp_FT, (size_t)C2D_NPHFIELD * C2D_NUM_NT));
+    HIPCHK(c, dalloc(&c->fp_zin, nc * FZ_N));
+    HIPCHK(c, dalloc(&c->fp_fin, nc * C2D_NUM_NT));
+    HIPCHK(c, dalloc(&c->fp_Pin, nc * C2D_NUM_NT));
+    HIPCHK(c, dalloc(&c->fp_nf, nc * C2D_NPHFIELD));
+    HIPCHK(c, dalloc(&c->fp_fout, nc * C2D_NUM_NT));
+    HIPCHK(c, dalloc(&c->fp_Pout, nc * C2D_NUM_NT));
+    HIPCHK(c, dalloc(&c->fp_zout, nc * FO_N));
+    HIPCHK(c, dalloc(&c->fp_err, 1));
+  }
+  /* F_IC(i, ph) -> FT[ph][i]: lanes (bins i) read consecutive addresses */
+  std::vector<double> ft((size_t)C2D_NPHFIELD * C2D_NUM_NT);
+  for (int ph = 0; ph < C2D_NPHFIELD; ph++)
+    for (int i = 0; i < C2D_NUM_NT; i++)
+      ft[(size_t)ph * C2D_NUM_NT + i] = fc->F_IC[i * fc->F_IC_s_i + ph * fc->F_IC_s_ph];
+  HIPCHK(c, hipMemcpy(c->fp_FT, ft.data(), ft.size() * sizeof(double), hipMemcpyHostToDevice));
+  c->fpc = *fc;
+  c->fpc.F_IC = nullptr;
+  c->fp_ready = true;
+  return C2D_OK;
+}
+
+extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out* out) {
+  if (!c || !in || !out) return C2D_E_ARG;
+  if (!c->fp_ready) return fail(c, C2D_E_STATE, "c2d_fp_set_config must precede c2d_fp_step");
+  if (!out->f_nt.data || !out->Pnt.data)
+    return fail(c, C2D_E_ARG, "c2d_fp_step: f_nt and Pnt (in/out) are required");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const int nz = c->nz, nr = c->nr, nc = c->ncell;
+  const bool nf_dev = in->n_field.data == nullptr, ecens_dev = in->ecens.data == nullptr;
+  auto a2 = [](const c2d_array2& a, int j, int k, double d) {
+    return a.data ? a.data[j * a.s_j + k * a.s_k] : d;
+  };
+  auto m2 = [](const c2d_marray2& a, int j, int k) -> double* {
+    return a.data ? &a.data[j * a.s_j + k * a.s_k] : nullptr;
+  };
+  std::vector<double> zin((size_t)nc * FZ_N, 0.0), fin((size_t)nc * C2D_NUM_NT),
+      pin((size_t)nc * C2D_NUM_NT), nf(nf_dev ? 0 : (size_t)nc * C2D_NPHFIELD);
+  for (int j = 0; j < nz; j++)
+    for (int k = 0; k < nr; k++) {
+      const int cell = j * nr + k;
+      double* z = &zin[(size_t)cell * FZ_N];
+      z[FZ_VOL] = a2(in->vol, j, k, 0.0);
+      z[FZ_TEA] = a2(in->tea, j, k, 0.0);
+      z[FZ_TNA] = a2(in->tna, j, k, 0.0);
+      z[FZ_NE] = a2(in->n_e, j, k, 0.0);
+      z[FZ_B] = a2(in->B_field, j, k, 0.0);
+      z[FZ_ELSY] = a2(in->Eloss_sy, j, k, 0.0);
+      z[FZ_ECENS] = a2(in->ecens, j, k, 0.0);
+      z[FZ_ECOLD] = a2(in->ec_old, j, k, 0.0);
+      z[FZ_TURB] = a2(in->turb_lev, j, k, 0.0);
+      z[FZ_FPAIR] = a2(in->f_pair, j, k, 0.0);
+      const double* pp = m2(out->p_nth, j, k);
+      z[FZ_PNTH] = pp ? *pp : 0.0;
+      for (int i = 0; i < C2D_NUM_NT; i++) {
+        fin[(size_t)cell * C2D_NUM_NT + i] =
+            out->f_nt.data[i * out->f_nt.s_i + j * out->f_nt.s_j + k * out->f_nt.s_k];
+        pin[(size_t)cell * C2D_NUM_NT + i] =
+            out->Pnt.data[i * out->Pnt.s_i + j * out->Pnt.s_j + k * out->Pnt.s_k];
+      }
+      if (!nf_dev)
+        for (int ph = 0; ph < C2D_NPHFIELD; ph++)
+          nf[(size_t)cell * C2D_NPHFIELD + ph] =
+              in->n_field.data[ph * in->n_field.s_i + j * in->n_field.s_j + k * in->n_field.s_k];
+    }
+  const hipStream_t st = c->stream;
+  HIPCHK(c, hipMemcpyAsync(c->fp_zin, zin.data(), zin.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->fp_fin, fin.data(), fin.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->fp_Pin, pin.data(), pin.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  if (!nf_dev)
+    HIPCHK(c, hipMemcpyAsync(c->fp_nf, nf.data(), nf.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemsetAsync(c->fp_err, 0, sizeof(int32_t), st));
+  FpParams P;
+  memset(&P, 0, sizeof P);
+  const c2d_fp_config& f = c->fpc;
+  P.nz = nz; P.nr = nr; P.pick_sw = f.pick_sw; P.inj_switch = f.inj_switch; P.inj_dis = f.inj_dis;
+  P.g2var_switch = f.g2var_switch; P.cf_sentinel = f.cf_sentinel;
+  P.time = in->time; P.dt = in->dt; P.df_implicit = f.df_implicit; P.df_T = f.df_T;
+  P.r_esc = f.r_esc; P.r_acc = f.r_acc; P.r_flare = f.r_flare; P.z_flare = f.z_flare;
+  P.t_flare = f.t_flare; P.sigma_r = f.sigma_r; P.sigma_z = f.sigma_z; P.sigma_t = f.sigma_t;
+  P.flare_amp = f.flare_amp; P.inj_g1 = f.inj_g1; P.inj_g2 = f.inj_g2; P.inj_p = f.inj_p;
+  P.inj_t = f.inj_t; P.inj_L = f.inj_L; P.pick_rate = f.pick_rate; P.inj_gg = f.inj_gg;
+  P.inj_sigma = f.inj_sigma; P.inj_v = f.inj_v;
+  P.geo = c->geo; P.gnt = c->gnt; P.FT = c->fp_FT; P.zin = c->fp_zin; P.f_in = c->fp_fin;
+  P.P_in = c->fp_Pin;
+  P.nf = nf_dev ? c->T + c->L.n_field : c->fp_nf;    /* tally layout: [cell][nphfield] */
+  P.ecens = ecens_dev ? c->T + c->L.ecens : nullptr;
+  P.f_out = c->fp_fout; P.P_out = c->fp_Pout; P.zout = c->fp_zout; P.err = c->fp_err;
+  HIPCHK(c, hipEventRecord(c->ev_g0a, st));
+  int rc = c2d_launch_fp(&P, nc, st);
+  if (rc) return fail(c, C2D_E_HIP, "fp launch: %s", hipGetErrorString((hipError_t)rc));
+  HIPCHK(c, hipEventRecord(c->ev_g0b, st));
+  std::vector<double> zout((size_t)nc * FO_N), fout((size_t)nc * C2D_NUM_NT), pout((size_t)nc * C2D_NUM_NT);
+  std::vector<double> ecd(ecens_dev ? nc : 0);
+  int32_t herr = 0;
+  HIPCHK(c, hipMemcpyAsync(zout.data(), c->fp_zout, zout.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(fout.data(), c->fp_fout, fout.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(pout.data(), c->fp_Pout, pout.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(&herr, c->fp_err, sizeof herr, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  (void)hipEventElapsedTime(&c->last_fp_ms, c->ev_g0a, c->ev_g0b);
+  if (herr & FPERR_STEPS)
+    return fail(c, C2D_E_FP, "FP sub-step limit exceeded (reference stops, update2d.f:585-599)");
+  if (herr & FPERR_GUARD) return fail(c, C2D_E_FP, "FP temperature/McDonald iteration guard tripped");
+  /* scatter back in zone order; E_add_up sums, dT_max, tea (update2d.f:266-276) */
+  double E_old = 0.0, E_new = 0.0, hr = 0.0, hr_st = 0.0;
+  double dT_max = (in->ncycle <= 1) ? f.df_T : 0.0;   /* photon_fill, update2d.f:1912 */
+  for (int j = 0; j < nz; j++)
+    for (int k = 0; k < nr; k++) {
+      const int cell = j * nr + k;
+      const double* zo = &zout[(size_t)cell * FO_N];
+      const double* dg = zo + FO_DIAG;
+      double* p;
+      if ((p = m2(out->Te_new, j, k))) *p = zo[FO_TE];
+      if (dg[C2D_FP_SKIPPED] == 0.0) {
+        for (int i = 0; i < C2D_NUM_NT; i++) {
+          out->f_nt.data[i * out->f_nt.s_i + j * out->f_nt.s_j + k * out->f_nt.s_k] =
+              fout[(size_t)cell * C2D_NUM_NT + i];
+          out->Pnt.data[i * out->Pnt.s_i + j * out->Pnt.s_j + k * out->Pnt.s_k] =
+              pout[(size_t)cell * C2D_NUM_NT + i];
+        }
+        if ((p = m2(out->n_e, j, k))) *p = zo[FO_NE];
+        if ((p = m2(out->gmin, j, k))) *p = zo[FO_GMIN];
+        if ((p = m2(out->gmax, j, k))) *p = zo[FO_GMAX];
+        if ((p = m2(out->amxwl, j, k))) *p = zo[FO_AMXWL];
+        if ((p = m2(out->p_nth, j, k))) *p = zo[FO_PNTH];
+        E_old = E_old + dg[C2D_FP_E_OLD];
+        E_new = E_new + dg[C2D_FP_E_NEW];
+        hr = hr + dg[C2D_FP_HR];
+        hr_st = hr_st + dg[C2D_FP_HR_ST];
+        if (dg[C2D_FP_DELTA_T] > dT_max) dT_max = dg[C2D_FP_DELTA_T];
+      }
+      if ((p = m2(out->tea, j, k)) && a2(in->tna, j, k, 0.0) > 1.) {
+        double t = zo[FO_TE];
+        t = (1.0e3 < t) ? 1.0e3 : t;
+        t = (5.0 > t) ? 5.0 : t;
+        *p = t;
+      }
+      if (out->zone_diag)
+        memcpy(out->zone_diag + (size_t)cell * C2D_FP_NDIAG, dg, sizeof(double) * C2D_FP_NDIAG);
+    }
+  out->E_tot_old = E_old;
+  out->E_tot_new = E_new;
+  out->hr_total = hr;
+  out->hr_st_total = hr_st;
+  out->dT_max = dT_max;
+  return C2D_OK;
+}
+
+extern "C" int c2d_last_fp_ms(c2d_ctx* c, double* ms) {
+  if (!c || !ms) return C2D_E_ARG;
+  *ms = c->last_fp_ms;
   return C2D_OK;
 }

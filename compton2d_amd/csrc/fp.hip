@@ -1,17 +1,41 @@
 /*
- * fp.hip — Fokker-Planck electron-solve kernels (gfx950).
+ * fp.hip — Fokker-Planck electron update on gfx950.
  *
- * Batched Chang-Cooper tridiagonal solve of src/update2d.f:2476-2518
- * (`tridag`, called from FP_calc :1398 once per zone and sub-step) with the
- * reference's semantics kept exactly: the |b(1)| <= 1e-100 early return
- * (x left untouched), the |bet| <= 1e-100 zeroing, and the clipping of
- * negative values during back-substitution (every entry but x(1)).
- * The Thomas recurrence is sequential in the energy index, so one zone is
- * one lane (the zone count, <= 9801, is far below one wave per CU: this
- * solve is latency-bound and tiny next to transport).
+ * c2d_fp_kernel: the reference's FP_calc (src/update2d.f:337-1739) for one
+ * zone per 64-lane wavefront (one workgroup = one wave).  The zone's
+ * 200-bin state (f_old, f_new, Chang-Cooper coefficients, rates) and its
+ * 400-bin photon field live in LDS for all implicit sub-steps (thousands
+ * per MC step in optically thin zones).  Work is split by what parity
+ * allows:
+ *   - element-wise stages (rates dg_sy with its exp, the Chang-Cooper
+ *     smw/bigW/bigC coefficients with their 3 exps per bin, injection
+ *     profiles, the n_field x F_IC contraction, power-law fit terms) run
+ *     one energy bin per lane;
+ *   - reductions and recurrences whose order fixes the result bit for bit
+ *     (the reference's sequential sums, the Thomas solve tridag
+ *     :2476-2518, the temperature search :1440-1468) are evaluated by every
+ *     lane in the reference order from LDS (broadcast reads), so no
+ *     cross-lane exchange is needed;
+ *   - McDonald's series (src/volume2d.f:598-626), thousands of terms per
+ *     call inside the temperature search, computes 64 terms per pass in
+ *     parallel: the abscissa chain t <- t*1.001 is replayed per lane in
+ *     the reference's multiplication order, the expensive pow/exp terms are
+ *     lane-parallel, and the terms are accumulated in order through
+ *     readlane, up to the reference's stopping term.
+ * Arithmetic is c2d_math.h with -ffp-contract=off, so results equal the
+ * det-math build of the oracle (oracle/c2d_fp_oracle.c) bit for bit.
+ * Branches of FP_calc that never reach an output (Coulomb/Moeller rates
+ * and their rate-file cache, dg_br, loop 300's dg_A/disp_A) are not
+ * computed; see the oracle's header for the argument.
+ *
+ * c2d_tridag_kernel: the batched Thomas solve alone (one zone per lane),
+ * exported as c2d_fp_tridag for unit parity against tridag.
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "c2d_device.hpp"
+#include "c2d_math.h"
 
 namespace c2d {
 
@@ -51,6 +75,499 @@ __global__ void __launch_bounds__(TRI_BLOCK) c2d_tridag_kernel(const double* __r
   for (int i = 0; i < nt; i++) x[o + i] = f[i];
 }
 
+namespace {
+
+constexpr int FPB = 64;
+constexpr int NT = C2D_NUM_NT;
+constexpr int NPH = C2D_NPHFIELD;
+constexpr double PI_REF = 3.1415926536;       /* general.pa:24 */
+constexpr double C_LIGHT = 2.9979245620e10;   /* general.pa:25 */
+constexpr double LNL = 20.0;                  /* update2d.f:143 */
+constexpr int MAX_FP_STEPS = 1000000;         /* update2d.f:585-599 */
+constexpr long long GUARD_MAX = 1ll << 34;    /* never reached by valid input */
+#define F32(x) ((double)(float)(x))
+
+__device__ __forceinline__ double rl(double v, int m) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), m);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), m);
+  return __hiloint2double(hi, lo);
+}
+
+/* gammln (volume2d.f:647-668) */
+__device__ double gammln(double xx) {
+  const double cof[6] = {76.18009172947146, -86.50532032941677, 24.01409824083091,
+                         -1.231739572450155, .1208650973866179e-2, -.5395239384953e-5};
+  const double stp = 2.5066282746310005;
+  double x = xx, y = x, tmp = x + 5.5;
+  tmp = (x + 0.5) * c2d_log(tmp) - tmp;
+  double ser = 1.000000000190015;
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    y = y + 1.0;
+    ser = ser + cof[j] / y;
+  }
+  return tmp + c2d_log(stp * ser / x);
+}
+
+/* McDonald (volume2d.f:598-626), 64 series terms per pass (wave-uniform call) */
+__device__ double mcdonald_w(double nu, double z, int lane, long long& guard) {
+  const double dt = 1.001, d = dt - 1.0, s = 5.0e-1 * (1.0 + dt), a = nu - 5.0e-1;
+  double sum = 0.0, t0 = 1.0;
+  for (;;) {
+    double t = t0;
+    for (int m = 0; m < lane; m++) t = t * dt;   /* the reference's t after `lane` terms */
+    const double ts = t * s;
+    const double y = z * ts;
+    double sd = 0.0;
+    if (y < 2.25e2) sd = c2d_pow(ts * ts - 1.0, a) / c2d_exp(y);
+    const double term = d * t * sd;
+    const double tn = t * dt;
+    const unsigned long long stop = __ballot(!(tn < 2.0 || sd > 1.0e-8));
+    const int nterm = stop ? __ffsll((long long)stop) : FPB;
+    for (int m = 0; m < nterm; m++) sum = sum + rl(term, m);
+    guard += nterm;
+    if (stop || guard > GUARD_MAX) break;
+    t0 = rl(tn, FPB - 1);
+  }
+  return __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, nu) * sum / c2d_exp(gammln(5.0e-1 + nu));
+}
+
+/* gamma_bar (volume2d.f:572-594) */
+__device__ double gamma_bar_w(double Theta, int lane, long long& guard) {
+  double g;
+  if (Theta < F32(0.2)) {
+    g = (1. + F32(4.375) * Theta + F32(7.383) * (Theta * Theta) +
+         F32(3.384) * (Theta * Theta * Theta)) /
+            (1. + F32(1.875) * Theta + F32(.8203) * (Theta * Theta)) -
+        Theta;
+  } else {
+    const double K2 = mcdonald_w(2.0, 1.0 / Theta, lane, guard);
+    const double K3 = mcdonald_w(3.0, 1.0 / Theta, lane, guard);
+    g = K3 / K2 - Theta;
+  }
+  if (g < 1.0) g = 1.0;
+  return g;
+}
+
+}  // namespace
+
+/* One zone per workgroup (= one wave).  Line numbers: src/update2d.f. */
+__global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
+  __shared__ double s_gnt[NT + 2], s_gam[NT + 2], s_fold[NT + 2], s_fnew[NT + 2];
+  __shared__ double s_dgic[NT + 2], s_dgdt[NT + 2], s_disp[NT + 2];
+  __shared__ double s_a[NT + 2], s_b[NT + 2], s_c[NT + 2];
+  __shared__ double s_smw[NT + 2], s_bigW[NT + 2], s_bigC[NT + 2], s_em[NT + 2], s_inj[NT + 2];
+  __shared__ double s_Pnt[NT + 2], s_nf[NPH];
+
+  const int cell = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int j = cell / P.nr + 1, k = cell % P.nr + 1;
+  const Geo* G = P.geo;
+  const double* zin = P.zin + (size_t)cell * FZ_N;
+  double* zo = P.zout + (size_t)cell * FO_N;
+  long long guard = 0;
+
+  const double volume = zin[FZ_VOL], tea = zin[FZ_TEA], tna = zin[FZ_TNA];
+  const double B = zin[FZ_B], Eloss_sy = zin[FZ_ELSY], f_pair = zin[FZ_FPAIR];
+  const double ecens = P.ecens ? P.ecens[cell] : zin[FZ_ECENS];
+  const double zmax = G->z[P.nz], rmax = G->r[P.nr];
+
+  const double t_esc = P.r_esc * zmax / C_LIGHT;   /* :460-461 */
+  const double t_acc = P.r_acc * zmax / C_LIGHT;
+  double Te_new = tea;
+  double n_p = zin[FZ_NE];
+  double ne = n_p * (1. + f_pair);
+  double n_positron = n_p * f_pair;
+  double n_lept = ne + n_positron;
+  if (n_lept < 1.0e-11) {                           /* :478 */
+    if (lane == 0) {
+      zo[FO_TE] = Te_new;
+      for (int q = 0; q < C2D_FP_NDIAG; q++) zo[FO_DIAG + q] = 0.0;
+      zo[FO_DIAG + C2D_FP_SKIPPED] = 1.0;
+    }
+    return;
+  }
+  for (int i = lane; i < NT; i += FPB) {
+    s_gnt[i + 1] = P.gnt[i];
+    s_gam[i + 1] = P.gnt[i] + 1.0;
+    s_fold[i + 1] = P.f_in[(size_t)cell * NT + i];
+    s_Pnt[i + 1] = P.P_in[(size_t)cell * NT + i];
+  }
+  for (int i = lane; i < NPH; i += FPB) s_nf[i] = P.nf[(size_t)cell * NPH + i];
+  __syncthreads();
+
+  /* E_el, normalisation (:482-509) */
+  double E_el = 0.0, E_pos = 0.0;
+  for (int i = 2; i <= NT; i++) E_el = E_el + (s_gnt[i] - s_gnt[i - 1]) * s_gam[i] * s_fold[i];
+  E_el = E_el * ne * 8.176e-7 * volume;
+  double e_old = 0.0 + E_el + E_pos + zin[FZ_ECOLD];
+  double e_new = 0.0 + ecens;
+  double sum_p = 0.;
+  for (int i = 1; i <= NT - 1; i++) sum_p = sum_p + (s_gnt[i + 1] - s_gnt[i]) * s_fold[i];
+  __syncthreads();
+  for (int i = lane + 1; i <= NT; i += FPB) s_fold[i] = s_fold[i] / sum_p;
+  __syncthreads();
+  if (lane == 0) s_fold[NT] = 0.0;
+
+  /* flare (:532-562) */
+  const double rmid = 5.0e-1 * (G->r[k] + G->r[k - 1]);   /* r[0] = rmin */
+  const double zmid = 5.0e-1 * (G->z[j] + G->z[j - 1]);   /* z[0] = zmin */
+  double tl_flare = 0.0;
+  if (P.cf_sentinel == 1) {
+    const double ar = (rmid - P.r_flare) / P.sigma_r;
+    const double az = (zmid - P.z_flare) / P.sigma_z;
+    const double at = (P.time - P.t_flare) / P.sigma_t;
+    const double y = 5.0e-1 * (ar * ar + az * az + at * at);
+    tl_flare = (y < 1.0e2) ? P.flare_amp / c2d_exp(y) : 0.0;
+  }
+  const double tlev = zin[FZ_TURB] + tl_flare;
+  const double Tp_flare = tna * (1.0 + tl_flare);
+  const double Th_p = Tp_flare / 9.382e5;
+  double Th_e = tea / 5.11e2;
+  const double f_th = 1.5 * volume * n_lept;
+  /* dg_ic(i) = -sum_ph n_field(ph) F_IC(i,ph) / volume (:568-574), bin per lane */
+  for (int i = lane + 1; i <= NT - 1; i += FPB) {
+    double s = 0.0;
+    const double* ft = P.FT + (i - 1);
+    for (int ph = 0; ph < NPH; ph++) s = s - s_nf[ph] * ft[(size_t)ph * NT] / volume;
+    s_dgic[i] = s;
+  }
+  if (lane == 0) s_dgic[NT] = 0.0;   /* hazard H10 */
+  const double dz = G->z[j] - G->z[j - 1];          /* :628-632 */
+  __syncthreads();
+
+  double hr = 0.0, hr_st = 0.0, sum_E = 0.0, t_fp = 0.0;
+  int fp_steps = 0;
+  for (;;) {
+    /* label 200 (:577) */
+    double g_av = gamma_bar_w(Th_e, lane, guard);
+    double hr_th_c = 0.0;
+    for (int i = 1; i <= NT - 1; i++)
+      hr_th_c = hr_th_c - 8.176e-7 * s_dgic[i] * s_fold[i] * (s_gnt[i + 1] - s_gnt[i]) * volume * n_lept;
+    if (fp_steps > MAX_FP_STEPS) {
+      if (lane == 0) atomicOr(P.err, FPERR_STEPS);
+      return;
+    }
+    const double gamma_R = 2.1e-3 * __builtin_sqrt(n_lept) / (B * __builtin_sqrt(g_av));
+    const double sT = Th_e + Th_p;
+    const double h_T = F32(.79788) * (2. * (sT * sT) + 2.0 * sT + 1.0) /
+                       (c2d_pow(sT, 1.5) * (1.0 + 1.875 * Th_e + .8203 * (Th_e * Th_e)));
+    const double hr_th_Coul = f_th * 1.7386e-26 * n_p * LNL * h_T * (Tp_flare - Te_new);
+    const double yR = gamma_R / g_av;
+    const double hr_th_sy = (yR < 100.0) ? -Eloss_sy / (P.dt * c2d_exp(yR)) : 0.0;
+    double hr_th_A = tlev * hr_th_Coul;
+    if (hr_th_A < 1.0e-20) hr_th_A = 1.0e-20;
+    const double hr_th_total = hr_th_sy + hr_th_c + hr_th_A;
+    const double dT_total = 6.25e8 * P.dt * hr_th_total / f_th;
+    double f_t_implicit = P.df_implicit * Te_new / fabs(dT_total);
+    if (f_t_implicit > P.df_T) f_t_implicit = P.df_T;
+    const double f_sy = 1.058e-15 * (B * B) / 8.176e-7;
+    const double g_thr = 1.0 + 4.0 * Th_e;
+    /* dgdt, disp (:880-889, :1035-1049): bin per lane */
+    for (int i = lane + 1; i <= NT; i += FPB) {
+      const double gi = s_gam[i];
+      const double y = gamma_R / gi;
+      const double dg_sy = (y < 100.0) ? -(f_sy * (gi * gi - 1.0) / c2d_exp(y)) : -1.0e-50;
+      const double dg_A = gi / t_acc;
+      s_disp[i] = gi * gi / t_acc / 2.0;
+      s_dgdt[i] = dg_sy + s_dgic[i] + dg_A;
+    }
+    double hr_nt_A = 0.0, hr_st_A = 0.0;
+    for (int i = 1; i <= NT - 1; i++) {
+      const double gi = s_gam[i];
+      const double dg_A = gi / t_acc;
+      hr_nt_A = hr_nt_A + dg_A * s_fold[i] * (s_gam[i + 1] - gi);
+      if (gi > g_thr) hr_st_A = hr_st_A + dg_A * s_fold[i] * (s_gam[i + 1] - gi);
+    }
+    hr_st_A = hr_st_A * 8.176e-7 * n_lept * volume;
+    hr_nt_A = hr_nt_A * 8.176e-7 * n_lept * volume;
+    const double heat_total = hr_th_Coul + hr_nt_A;
+    e_old = e_old + heat_total * f_t_implicit * P.dt;
+    if (fp_steps == 0) {
+      hr = hr + heat_total;
+      hr_st = hr_st + hr_st_A;
+    }
+    double d_t = f_t_implicit * P.dt;                  /* :1142-1146 */
+    if (d_t > (P.dt - t_fp)) d_t = 1.00001 * (P.dt - t_fp);
+    n_positron = 0.0;                                  /* pairs off (:1164-1167) */
+    ne = n_p + n_positron;
+    /* injection (:1226-1306) */
+    double n_inject = 0.0;
+    bool inj_any = false;
+    double inj_rho = 0.0, inj_sum = 0.0;
+    if (P.pick_sw == 1) {
+      for (int i = lane + 1; i <= NT - 1; i += FPB) {
+        const double x = s_gam[i] - P.inj_gg;
+        s_inj[i] = 1.0e2 * c2d_exp(-((x * x) / 2.0 / (P.inj_sigma * P.inj_sigma))) /
+                   (P.inj_sigma * __builtin_sqrt(2.0 * PI_REF));
+      }
+      __syncthreads();
+      inj_sum = 0.0;
+      for (int i = 1; i <= NT - 1; i++) inj_sum = inj_sum + s_inj[i] * (s_gnt[i + 1] - s_gnt[i]);
+      inj_rho = P.pick_rate * d_t;
+      inj_any = true;
+    }
+    if (inj_any) {
+      __syncthreads();
+      for (int i = lane + 1; i <= NT - 1; i += FPB) {
+        const double v = inj_rho * s_inj[i] / inj_sum;
+        s_inj[i] = v;
+        s_fold[i] = s_fold[i] + v / ne;
+      }
+      __syncthreads();
+      for (int i = 1; i <= NT - 1; i++) n_inject = n_inject + s_inj[i] * (s_gnt[i + 1] - s_gnt[i]);
+    }
+    if (P.inj_switch != 0) {
+      const double tt = P.time + t_fp - P.inj_t;
+      if (tt > dz / P.inj_v * (double)(j - 1) && tt < dz / P.inj_v * (double)j && k <= P.nr) {
+        __syncthreads();
+        for (int i = lane + 1; i <= NT - 1; i += FPB) {
+          const double gi = s_gam[i];
+          double v;
+          if (P.inj_dis == 1) {
+            const double x = gi - P.inj_gg;
+            v = 1.0e2 * c2d_exp(-((x * x) / 2.0 / (P.inj_sigma * P.inj_sigma))) /
+                (P.inj_sigma * __builtin_sqrt(2.0 * PI_REF));
+          } else {
+            const double inj_g2var =
+                P.inj_g2 * c2d_pow(10.0, (P.time + t_fp - P.inj_t) * P.inj_v / zmax);
+            if (gi > P.inj_g1) {
+              const double inj_y = (P.g2var_switch == 1) ? gi / inj_g2var : gi / P.inj_g2;
+              v = (inj_y < 1.0e2) ? 1.0e2 / (c2d_pow(gi, P.inj_p) * c2d_exp(inj_y)) : 0.0;
+            } else {
+              v = 0.0;
+            }
+          }
+          s_inj[i] = v;
+        }
+        __syncthreads();
+        double isum = 0.0, inj_E = 0.0;
+        for (int i = 1; i <= NT - 1; i++) {
+          isum = isum + s_inj[i] * (s_gnt[i + 1] - s_gnt[i]);
+          inj_E = inj_E + s_inj[i] * (s_gnt[i + 1] - s_gnt[i]) * s_gam[i];
+        }
+        inj_E = inj_E / isum;
+        const double inj_rate = P.inj_L / 8.186e-7 / inj_E / (PI_REF * (rmax * rmax) * dz);
+        const double rho = inj_rate * d_t;
+        __syncthreads();
+        for (int i = lane + 1; i <= NT - 1; i += FPB) {
+          const double v = rho * s_inj[i] / isum;
+          s_inj[i] = v;
+          s_fold[i] = s_fold[i] + v / ne;
+        }
+        __syncthreads();
+        for (int i = 1; i <= NT - 1; i++) n_inject = n_inject + s_inj[i] * (s_gnt[i + 1] - s_gnt[i]);
+      }
+    }
+    ne = ne + n_inject;
+    n_p = n_p + n_inject;
+    n_lept = n_lept + n_inject;
+    ne = ne * t_esc / (t_esc + d_t);                  /* escape (:1309-1313) */
+    n_p = n_p * t_esc / (t_esc + d_t);
+    n_lept = n_lept * t_esc / (t_esc + d_t);
+    __syncthreads();
+    /* Chang-Cooper coefficients (:1363-1390): smw, bigW, bigC and the
+     * exp(-smw) factor for i = 1..NT-1, then a, b, c for i = 2..NT-1 */
+    for (int i = lane + 1; i <= NT - 1; i += FPB) {
+      double bigB, Dg;
+      if (i == 1) {
+        bigB = -(s_dgdt[1] + s_dgdt[2]);
+        Dg = s_gnt[2] - s_gnt[1];
+      } else {
+        bigB = -(s_dgdt[i] + s_dgdt[i + 1]) / 2.0;
+        Dg = s_gnt[i + 1] - s_gnt[i];
+      }
+      const double bigC = (s_disp[i] + s_disp[i + 1]) / 2.0;
+      const double smw = Dg * bigB / bigC;
+      s_smw[i] = smw;
+      s_bigW[i] = smw / (c2d_exp(smw) - 1.0);
+      s_em[i] = bigC * smw / (1.0 - c2d_exp(-smw));   /* bigC*smw/(1-exp(-smw)) */
+      s_bigC[i] = bigC;
+    }
+    __syncthreads();
+    for (int i = lane + 2; i <= NT - 1; i += FPB) {
+      const double D_gminus = s_gnt[i] - s_gnt[i - 1];
+      const double D_gplus = s_gnt[i + 1] - s_gnt[i];
+      const double Delta_g = __builtin_sqrt(s_gnt[i] / s_gnt[i - 1]) * D_gminus;
+      s_c[i] = -d_t * (s_em[i] / Delta_g / D_gplus);
+      s_b[i] = 1.0 + d_t / Delta_g * (s_bigC[i] * s_bigW[i] / D_gplus + s_em[i - 1] / D_gminus) +
+               d_t / t_esc;
+      s_a[i] = -d_t / Delta_g * s_bigC[i - 1] * s_bigW[i - 1] / D_gminus;
+    }
+    if (lane == 0) {
+      s_a[1] = 0.0; s_b[1] = 1.0; s_c[1] = 0.0;
+      s_a[NT] = 0.0; s_b[NT] = 1.0; s_c[NT] = 0.0;
+    }
+    __syncthreads();
+    /* tridag (:2476-2518) in the reference order; gam kept in s_smw */
+    {
+      double bet = s_b[1];
+      double u = s_fold[1] / bet;
+      bool zero = false;
+      if (lane == 0) s_fnew[1] = u;
+      for (int i = 2; i <= NT; i++) {
+        const double gam = s_c[i - 1] / bet;
+        bet = s_b[i] - s_a[i] * gam;
+        if (fabs(bet) <= 1.0e-100) {
+          zero = true;
+          break;
+        }
+        u = (s_fold[i] - s_a[i] * u) / bet;
+        if (lane == 0) {
+          s_smw[i] = gam;
+          s_fnew[i] = u;
+        }
+      }
+      __syncthreads();
+      if (zero) {
+        for (int i = lane + 1; i <= NT; i += FPB) s_fnew[i] = 0.0;
+      } else if (lane == 0) {
+        double up = s_fnew[NT];
+        for (int i = NT - 1; i >= 1; i--) {
+          double ui = s_fnew[i] - s_smw[i + 1] * up;
+          if (up < 0.0) s_fnew[i + 1] = 0.0;
+          s_fnew[i] = ui;
+          up = ui;
+        }
+      }
+      __syncthreads();
+    }
+    if (lane == 0) {
+      s_fnew[NT] = 0.0;
+      s_fnew[1] = 0.0;
+    }
+    __syncthreads();
+    sum_p = 0.;
+    double sE = 0.;
+    for (int i = 1; i <= NT - 1; i++) {              /* :1415-1419 */
+      const double fi = s_fnew[i];
+      sum_p = sum_p + (s_gnt[i + 1] - s_gnt[i]) * fi;
+      sE = sE + (s_gnt[i + 1] - s_gnt[i]) * s_gam[i] * fi;
+      if (lane == 0) s_Pnt[i] = sum_p;
+    }
+    sum_E = sE / sum_p;
+    t_fp = t_fp + d_t;
+    fp_steps = fp_steps + 1;
+    __syncthreads();
+    for (int i = lane + 1; i <= NT; i += FPB) {
+      const double v = s_fnew[i] / sum_p;
+      s_fnew[i] = v;
+      s_fold[i] = v;
+    }
+    __syncthreads();
+    /* new temperature (:1440-1468) */
+    double gbar = 0.0;
+    for (int i = 1; i <= NT - 1; i++) gbar = gbar + s_gam[i] * s_fnew[i] * (s_gnt[i + 1] - s_gnt[i]);
+    double The_new = Th_e;
+    if (gbar > g_av) {
+      while (gbar > g_av) {
+        The_new = The_new * F32(1.005);
+        g_av = gamma_bar_w(The_new, lane, guard);
+        if (guard > GUARD_MAX) break;
+      }
+    } else {
+      while (gbar < g_av) {
+        The_new = The_new / F32(1.005);
+        g_av = gamma_bar_w(The_new, lane, guard);
+        if (The_new < 1.0e-2) break;
+        if (guard > GUARD_MAX) break;
+      }
+    }
+    if (guard > GUARD_MAX) {
+      if (lane == 0) atomicOr(P.err, FPERR_GUARD);
+      return;
+    }
+    Te_new = 5.11e2 * The_new;
+    Th_e = The_new;
+    if (!(t_fp < P.dt)) break;                         /* :1473 */
+  }
+
+  /* outputs (:1481-1500) */
+  E_el = 0.0;
+  E_pos = 0.0;
+  for (int i = 2; i <= NT; i++) E_el = E_el + s_fnew[i] * s_gam[i] * (s_gnt[i] - s_gnt[i - 1]);
+  E_el = E_el * ne * 8.176e-7 * volume;
+  e_new = e_new + E_el + E_pos;
+  for (int i = lane; i < NT; i += FPB) {
+    P.f_out[(size_t)cell * NT + i] = s_fnew[i + 1];
+    P.P_out[(size_t)cell * NT + i] = s_Pnt[i + 1] / sum_p;
+  }
+  /* nonthermal parameters (:1654-1736) */
+  int i;
+  for (i = 5; i <= NT - 5; i++)
+    if (s_fnew[i] > 1.0e-10) break;
+  const double gmin = s_gam[i];
+  const int i_nt = i;
+  for (i = NT - 5; i >= 5; i--)
+    if (s_fnew[i] > 1.0e-15) break;
+  const double gmax = s_gam[i];
+  double sum_nt = 0.0, sum_th = 0.0;
+  for (i = 1; i <= NT - 1; i++) {
+    if (i < i_nt)
+      sum_th = sum_th + (s_gam[i + 1] - s_gam[i]) * s_fnew[i];
+    else
+      sum_nt = sum_nt + (s_gam[i + 1] - s_gam[i]) * s_fnew[i];
+  }
+  double amxwl = sum_th / (sum_nt + sum_th);
+  double p_nth = zin[FZ_PNTH];
+  if (amxwl > 9.999e-1) {
+    amxwl = 1.0;
+  } else {
+    p_nth = F32(0.1);
+    double sum_g = 1.0e50, sumg_old;
+    /* first bin with gamma/gmax >= 100 ends the fit sum (:1707-1717) */
+    int i_end = NT - 1;
+    for (i = i_nt; i <= NT - 2; i++)
+      if (!(s_gam[i] / gmax < 100.0)) {
+        i_end = i;
+        break;
+      }
+    for (;;) {
+      sumg_old = sum_g;
+      sum_g = 0.0;
+      double sum_gg = 0.0;
+      const double p_1 = 1.0 - p_nth;
+      double N_nt;
+      if (fabs(p_1) > 1.0e-4)
+        N_nt = (1. - amxwl) * p_1 / (c2d_pow(gmax, p_1) - c2d_pow(gmin, p_1));
+      else
+        N_nt = (1.0 - amxwl) / c2d_log(gmax / gmin);
+      __syncthreads();
+      for (int q = i_nt + lane; q < i_end; q += FPB)
+        s_inj[q] = N_nt / (c2d_pow(s_gam[q], p_nth) * c2d_exp(s_gam[q] / gmax));
+      __syncthreads();
+      for (int q = i_nt; q < i_end; q++) {
+        const double f_pl = s_inj[q];
+        sum_g = sum_g + f_pl * s_gam[q] * (s_gnt[q + 1] - s_gnt[q]);
+        sum_gg = sum_gg + f_pl * (s_gnt[q + 1] - s_gnt[q]);
+      }
+      sum_g = sum_g / sum_gg;
+      sum_g = fabs(sum_g - sum_E);
+      if (sum_g < sumg_old && p_nth < 10.) {
+        p_nth = p_nth + 0.5e-1;
+        continue;
+      }
+      break;
+    }
+  }
+  if (lane == 0) {
+    zo[FO_TE] = Te_new;
+    zo[FO_NE] = n_p;
+    zo[FO_GMIN] = gmin;
+    zo[FO_GMAX] = gmax;
+    zo[FO_AMXWL] = amxwl;
+    zo[FO_PNTH] = p_nth;
+    zo[FO_DIAG + C2D_FP_E_OLD] = e_old;
+    zo[FO_DIAG + C2D_FP_E_NEW] = e_new;
+    zo[FO_DIAG + C2D_FP_HR] = hr;
+    zo[FO_DIAG + C2D_FP_HR_ST] = hr_st;
+    zo[FO_DIAG + C2D_FP_DELTA_T] = fabs(Te_new - tea) / Te_new;
+    zo[FO_DIAG + C2D_FP_STEPS] = (double)fp_steps;
+    zo[FO_DIAG + C2D_FP_SKIPPED] = 0.0;
+    zo[FO_DIAG + 7] = 0.0;
+  }
+}
+
 }  // namespace c2d
 
 extern "C" int c2d_launch_tridag(const double* a, const double* b, const double* c,
@@ -60,5 +577,11 @@ extern "C" int c2d_launch_tridag(const double* a, const double* b, const double*
   const int grid = (ncell + c2d::TRI_BLOCK - 1) / c2d::TRI_BLOCK;
   hipLaunchKernelGGL(c2d::c2d_tridag_kernel, dim3(grid), dim3(c2d::TRI_BLOCK), 0, stream, a, b, c,
                      r, x, ncell, nt);
+  return (int)hipGetLastError();
+}
+
+extern "C" int c2d_launch_fp(const c2d::FpParams* P, int ncell, hipStream_t stream) {
+  if (ncell <= 0) return 0;
+  hipLaunchKernelGGL(c2d::c2d_fp_kernel, dim3(ncell), dim3(64), 0, stream, *P);
   return (int)hipGetLastError();
 }

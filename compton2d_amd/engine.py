@@ -90,6 +90,12 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_last_kernel_ms.restype = C.c_int
     lib.c2d_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                        C.POINTER(C.c_int32)]
+    lib.c2d_fp_set_config.restype = C.c_int
+    lib.c2d_fp_set_config.argtypes = [vp, C.POINTER(abi.FpConfig)]
+    lib.c2d_fp_step.restype = C.c_int
+    lib.c2d_fp_step.argtypes = [vp, C.POINTER(abi.FpStepIn), C.POINTER(abi.FpStepOut)]
+    lib.c2d_last_fp_ms.restype = C.c_int
+    lib.c2d_last_fp_ms.argtypes = [vp, C.POINTER(C.c_double)]
     if path is None:
         _lib = lib
     return lib
@@ -217,6 +223,25 @@ class Engine:
         return n.value
 
     # -- Fokker-Planck -------------------------------------------------------
+    def fp_set_config(self, const: abi.FpConstants) -> None:
+        """FP_calc run constants + F_IC (replaces setup_bcast / FP_bcast)."""
+        self._fpc = const.to_ctypes()
+        self._check(self.lib.c2d_fp_set_config(self.ctx, C.byref(self._fpc)))
+
+    def fp_step(self, ncycle: int, time: float, dt: float, inputs: dict, state: dict) -> dict:
+        """One `update` (src/update2d.f:7-327) on the GPU; returns the new state.
+
+        inputs['n_field'] / inputs['ecens'] set to None read the context's
+        (all-reduced) tally buffer on the device instead of host arrays."""
+        call = abi.FpCall(ncycle, time, dt, inputs, state)
+        self._check(self.lib.c2d_fp_step(self.ctx, C.byref(call.sin), C.byref(call.sout)))
+        return call.result()
+
+    def last_fp_ms(self) -> float:
+        ms = C.c_double()
+        self._check(self.lib.c2d_last_fp_ms(self.ctx, C.byref(ms)))
+        return ms.value
+
     def fp_tridag(self, a, b, c, r, x0=None) -> np.ndarray:
         """Batched tridag (src/update2d.f:2476-2518); arrays [ncell, nt]."""
         a, b, c, r = (np.ascontiguousarray(x, np.float64) for x in (a, b, c, r))

@@ -14,7 +14,8 @@
  *   src/update2d.f:1929  cens_add_up (REDUCE)      c2d_tally_device_ptr + one all-reduce
  *   src/imcleak2d.f:171  event-file writes         c2d_events
  *   src/census2d.f:1-76  write_cens/read_cens      c2d_census_export / c2d_census_import
- *   src/update2d.f:337   FP_calc + tridag          c2d_fp_step
+ *   src/update2d.f:7     update (FP_calc, tridag,  c2d_fp_set_config + c2d_fp_step
+ *     E_add_up, FP_send_job/recv_result)
  *
  * Every array argument is (pointer, strides) so Fortran COMMON arrays with
  * their fixed leading extents (general.pa: n_vol=400, jmax=kmax=99,
@@ -59,6 +60,8 @@ extern "C" {
 #define C2D_E_QUEUE_OVERFLOW   -5   /* scatter-secondary queue full               */
 #define C2D_E_NOMEM            -6
 #define C2D_E_STATE            -7   /* call order violated                        */
+#define C2D_E_FP               -8   /* FP sub-step limit (reference `stop`,
+                                       src/update2d.f:585-599) or a solver guard  */
 
 /* comtot (src/comtot2d.f:1-334, icoms=6) evaluation mode. */
 #define C2D_COMTOT_EXACT  0   /* 199-term electron-spectrum sum per call (reference)   */
@@ -207,6 +210,63 @@ typedef struct c2d_fp_in {
   int32_t nt;                     /* unknowns per zone (num_nt-1 = 199 in ref)  */
 } c2d_fp_in;
 
+/* ------------------------------------------------------------------------
+ * Fokker-Planck electron update of one MC step (src/update2d.f:7-327
+ * `update` + :337-1739 `FP_calc` for every zone, tridag :2476-2518).
+ * Mutable (pointer, strides) views bind the caller's COMMON arrays, which
+ * are updated in place exactly where the reference's FP_recv_result /
+ * update write them (src/fp_mpi.f:972-1003, src/update2d.f:266-276).
+ * ---------------------------------------------------------------------- */
+typedef struct c2d_marray3 { double* data; int64_t s_i, s_j, s_k; } c2d_marray3;
+typedef struct c2d_marray2 { double* data; int64_t s_j, s_k; } c2d_marray2;
+
+/* Run constants of FP_calc (src/reader.f:512-559, broadcast once by
+ * setup_bcast src/fp_mpi.f:12-324; df_implicit/df_T general.pa:27-28;
+ * F_IC from IC_loss src/icloss2d.f:1-64, broadcast by FP_bcast
+ * src/fp_mpi.f:596). */
+typedef struct c2d_fp_config {
+  int32_t pair_switch;            /* pairs in the FP solve: only 0 supported    */
+  double  df_implicit, df_T;      /* 1e-2, 0.25 in the reference               */
+  double  r_esc, r_acc;           /* escape / acceleration time [z(nz)/c]      */
+  int32_t cf_sentinel;            /* coronal flare on/off                      */
+  double  r_flare, z_flare, t_flare, sigma_r, sigma_z, sigma_t, flare_amp;
+  int32_t inj_switch, inj_dis, g2var_switch, pick_sw;
+  double  inj_g1, inj_g2, inj_p, inj_t, inj_L, pick_rate, inj_gg, inj_sigma;
+  double  inj_v;                  /* sqrt(1-1/g_bulk**2)*c_light (reader.f:559) */
+  const double* F_IC;             /* F_IC(i<num_nt, i_ph<nphfield)             */
+  int64_t F_IC_s_i, F_IC_s_ph;    /* Fortran F_IC(200,400): s_i=1, s_ph=200    */
+} c2d_fp_config;
+
+/* Per-step inputs of `update` (what FP_send_job packs, src/fp_mpi.f:632-686). */
+typedef struct c2d_fp_step_in {
+  int32_t ncycle;                 /* photon_fill (ncycle <= 1) sets dT_max=df_T */
+  double time, dt;                /* time, dt(1)                               */
+  c2d_array2 tea, tna, n_e, B_field, Eloss_sy, ec_old, turb_lev, vol;
+  c2d_array2 f_pair;              /* NULL data = 0                             */
+  c2d_array2 ecens;               /* NULL data: the context's tally buffer     */
+  c2d_array3 n_field;             /* (i_ph, j, k); NULL data: tally buffer     */
+} c2d_fp_step_in;
+
+/* Per-zone diagnostics (optional output, [ncell][C2D_FP_NDIAG]). */
+#define C2D_FP_E_OLD    0   /* zone's share of E_tot_old                       */
+#define C2D_FP_E_NEW    1   /* zone's share of E_tot_new                       */
+#define C2D_FP_HR       2   /* zone's share of hr_total                        */
+#define C2D_FP_HR_ST    3   /* zone's share of hr_st_total                     */
+#define C2D_FP_DELTA_T  4   /* |Te_new - tea| / Te_new                         */
+#define C2D_FP_STEPS    5   /* implicit FP sub-steps taken                     */
+#define C2D_FP_SKIPPED  6   /* 1: n_lept < 1e-11, zone left untouched          */
+#define C2D_FP_NDIAG    8
+
+/* In/out state.  f_nt, Pnt, n_e, gmin, gmax, amxwl, p_nth and tea are read
+ * and updated in place; Te_new is written.  Views with NULL data are
+ * skipped (tea: the update2d.f:266-276 clamp is then left to the caller). */
+typedef struct c2d_fp_step_out {
+  c2d_marray3 f_nt, Pnt;          /* (i<num_nt, j, k)                          */
+  c2d_marray2 Te_new, tea, n_e, gmin, gmax, amxwl, p_nth;
+  double* zone_diag;              /* optional [ncell][C2D_FP_NDIAG], cell=j*nr+k */
+  double  E_tot_old, E_tot_new, hr_total, hr_st_total, dT_max;  /* E_add_up */
+} c2d_fp_step_out;
+
 const char* c2d_version(void);
 int  c2d_init(const c2d_config* cfg, c2d_ctx** out);
 void c2d_finalize(c2d_ctx* ctx);
@@ -250,10 +310,22 @@ int  c2d_census_import(c2d_ctx* ctx, const double* d6, const int32_t* i5,
  * zone per wavefront.  x is [ncell][nt] on the host. */
 int  c2d_fp_tridag(c2d_ctx* ctx, const c2d_fp_in* in, double* x);
 
+/* Fokker-Planck run constants (once per run; replaces setup_bcast and the
+ * F_IC part of FP_bcast). */
+int  c2d_fp_set_config(c2d_ctx* ctx, const c2d_fp_config* cfg);
+/* One `update` (src/update2d.f:7-327) over all nz*nr zones: FP_calc for
+ * every zone on the GPU (one wavefront per zone, state in LDS), the
+ * E_add_up sums (zone order), the dT_max reduction and the tea update.
+ * Replaces FP_send_job / FP_calc / FP_send_result / E_add_up /
+ * FP_end_bcast.  Synchronous. */
+int  c2d_fp_step(c2d_ctx* ctx, const c2d_fp_step_in* in, c2d_fp_step_out* out);
+
 /* Device timing of the last step's dominant kernel (transport generation 0):
  * milliseconds and launches, measured with HIP events on the library's
  * own stream. */
 int  c2d_last_kernel_ms(c2d_ctx* ctx, double* gen0_ms, double* all_ms, int32_t* launches);
+/* Device time of the last c2d_fp_step's FP kernel (HIP events, ms). */
+int  c2d_last_fp_ms(c2d_ctx* ctx, double* ms);
 /* Packet-steps executed by that generation-0 launch (roofline numerator). */
 int  c2d_last_gen0_steps(c2d_ctx* ctx, int64_t* steps);
 

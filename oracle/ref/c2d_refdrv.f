@@ -71,6 +71,11 @@ c     static configuration (after setup)
       write(u) (Elcmax(j), j=1,nph_lc)
       write(u) (mu(j), j=1,nmu)
       close(u)
+c     IC loss kernel of setup (icloss2d.f:1-64), input of FP_calc
+      open(unit=u, file='fic.bin', access='stream',
+     1     form='unformatted', status='replace')
+      write(u) ((F_IC(j,k), j=1,num_nt), k=1,nphfield)
+      close(u)
 c
       do 500 n = 0, nsteps-1
 c        master part of the step
@@ -172,6 +177,77 @@ c        worker tallies of this step
          write(u) (P_file(j), j=1,nfmax)
          close(u)
          close(nunit_evt)
+c
+c        Fokker-Planck update (src/xec2d.f:86-87 -> update2d.f:7-327):
+c        the master/worker job exchange of update collapses to calling
+c        FP_calc for every zone in this one process.
+         if ((T_const.eq.0).and.(ncycle.gt.0)) then
+            write(fn, '(a,i3.3,a)') 'fpin_', n, '.bin'
+            open(unit=u, file=fn, access='stream',
+     1           form='unformatted', status='replace')
+            write(u) ncycle
+            write(u) time, dt(1)
+            write(u) ((tea(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((tna(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((n_e(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((B_field(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((Eloss_sy(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((ecens(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((ec_old(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((turb_lev(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((vol(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((f_pair(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((gmin(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((gmax(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((amxwl(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((p_nth(js,ks), ks=1,nr), js=1,nz)
+            write(u) (((f_nt(js,ks,j), j=1,num_nt), ks=1,nr), js=1,nz)
+            write(u) (((Pnt(js,ks,j), j=1,num_nt), ks=1,nr), js=1,nz)
+            write(u) (((n_field(j,js,ks), j=1,nphfield), ks=1,nr),
+     1                js=1,nz)
+            close(u)
+c           update, master part (update2d.f:142-151, :174-177), the
+c           dT_max of photon_fill (:1912) and FP_bcast (:185)
+            lnL = 20.d0
+            dT_max = 0.d0
+            if (ncycle.le.1) dT_max = df_T
+            hr_st_total = 0.d0
+            hr_total = 0.d0
+            E_tot_old = 0.d0
+            E_tot_new = 0.d0
+            do 62 js = 1, nz
+               do 61 ks = 1, nr
+                  Te_new(js,ks) = tea(js,ks)
+ 61            continue
+ 62         continue
+            do 70 zone = 1, nz*nr
+               call FP_calc(zone)
+ 70         continue
+c           store results for the next step (update2d.f:266-276)
+            do 82 js = 1, nz
+               do 81 ks = 1, nr
+                  if (tna(js,ks).gt.1.) then
+                     tea(js,ks) = Te_new(js,ks)
+                     tea(js,ks) = dmin1(1.d3, tea(js,ks))
+                     tea(js,ks) = dmax1(5.d0, tea(js,ks))
+                  endif
+ 81            continue
+ 82         continue
+            write(fn, '(a,i3.3,a)') 'fpout_', n, '.bin'
+            open(unit=u, file=fn, access='stream',
+     1           form='unformatted', status='replace')
+            write(u) E_tot_old, E_tot_new, hr_total, hr_st_total, dT_max
+            write(u) ((Te_new(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((tea(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((n_e(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((gmin(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((gmax(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((amxwl(js,ks), ks=1,nr), js=1,nz)
+            write(u) ((p_nth(js,ks), ks=1,nr), js=1,nz)
+            write(u) (((f_nt(js,ks,j), j=1,num_nt), ks=1,nr), js=1,nz)
+            write(u) (((Pnt(js,ks,j), j=1,num_nt), ks=1,nr), js=1,nz)
+            close(u)
+         endif
 c
 c        advance in time (src/xec2d.f:100-107)
          dt(2) = dt(1)

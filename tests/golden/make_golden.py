@@ -43,6 +43,23 @@ CASES = {
     "grid3x4": dict(case=dict(nz=3, nr=4, n_e=1.0e6, nst=1500, nmu=2), nsteps=2),
 }
 
+# Fokker-Planck cases (T_const=0): the reference's update/FP_calc after each
+# transport step with ncycle > 0 (refdrv dumps fpin_/fpout_NNN.bin)
+FP_CASES = {
+    # constant Gaussian pick-up + turbulence heating (src_20121026/input.dat:97-105)
+    "fp_pick": dict(case=dict(nz=2, nr=2, n_e=4.0e6, nst=400, T_const=0, pick_sw=1,
+                              turb_lev=1.0e-2), nsteps=3),
+    # shock injection (power law with moving cut-off) + coronal flare
+    "fp_inj": dict(case=dict(nz=2, nr=2, n_e=4.0e6, nst=400, T_const=0, inj_switch=1, inj_dis=2,
+                             g2var_switch=1, inj_t=0.0, inj_L=5e40, cf_sentinel=1,
+                             flare_amp=10.0, t_flare=1.0e5, sigma_t=1.0e6, sigma_r=1.0e16,
+                             sigma_z=1.0e16), nsteps=3),
+}
+FP_CONST_KEYS = ("cf_sentinel", "r_flare", "z_flare", "t_flare", "sigma_r", "sigma_z", "sigma_t",
+                 "flare_amp", "r_esc", "r_acc", "inj_switch", "inj_dis", "g2var_switch", "pick_sw",
+                 "inj_g1", "inj_g2", "inj_p", "inj_t", "inj_L", "pick_rate", "inj_gg", "inj_sigma",
+                 "g_bulk")
+
 TALLY_KEYS = ("edep", "prdep", "ecens", "npcen", "n_field", "E_IC", "nelectron", "fout", "edout",
               "erlki", "erlko", "erlku", "erlkl", "Ed_in", "census_d", "census_i", "events")
 IN_KEYS = ("kappa_tot", "eps_tot", "eps_th", "f_nt", "Pnt", "n_e", "Eloss_th", "Eloss_tot",
@@ -85,6 +102,46 @@ def run_case(name: str, spec: dict, out_dir: Path, work: Path) -> Path:
     return path
 
 
+def run_fp_case(name: str, spec: dict, out_dir: Path, work: Path) -> Path:
+    """FP inputs/outputs of the reference's update (update2d.f:7-327) per step."""
+    d = work / name
+    if d.exists():
+        shutil.rmtree(d)
+    refcase.write_input_deck(d, spec["case"])
+    refcase.run_reference(d, spec["nsteps"], klag=1, timeout=3600)
+    cfg = refcase.read_config(d)
+    full = dict(refcase.BASE_CASE)
+    full.update(spec["case"])
+    meta = {k: v for k, v in cfg.items() if not isinstance(v, np.ndarray)}
+    meta["case"] = spec["case"]
+    meta["fp_const"] = {k: full[k] for k in FP_CONST_KEYS}
+    arrays = {"cfg_" + k: v for k, v in cfg.items() if isinstance(v, np.ndarray)}
+    arrays["E_ph"] = refcase.read_step_in(d, 0, cfg)["E_ph"]
+    steps = []
+    for n in range(spec["nsteps"]):
+        if not refcase.has_fp(d, n):
+            continue
+        fi, fo = refcase.read_fp_in(d, n, cfg), refcase.read_fp_out(d, n, cfg)
+        steps.append(n)
+        meta["fp%d" % n] = dict(ncycle=fi["ncycle"], time=fi["time"], dt=fi["dt"],
+                                **{k: fo[k] for k in ("E_tot_old", "E_tot_new", "hr_total",
+                                                      "hr_st_total", "dT_max")})
+        for k, v in fi.items():
+            if isinstance(v, np.ndarray):
+                arrays["fpin%d_%s" % (n, k)] = v
+        for k, v in fo.items():
+            if isinstance(v, np.ndarray):
+                arrays["fpout%d_%s" % (n, k)] = v
+    meta["fp_steps"] = steps
+    arrays["meta_json"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    path = out_dir / (name + ".npz")
+    np.savez_compressed(path, **arrays)
+    fic = out_dir / "fp_fic.npz"
+    np.savez_compressed(fic, F_IC=refcase.read_fic(d),
+                        source="F_IC(num_nt, nphfield) of the reference setup (icloss2d.f:1-64)")
+    return path
+
+
 def make_medium(out_path: Path, work: Path) -> None:
     """Per-cell tables of the inputm.dat medium (n_e=80, B=0.13 G, p=2.3)."""
     d = work / "medium"
@@ -116,6 +173,11 @@ def main() -> None:
             if args.only and name != args.only:
                 continue
             p = run_case(name, spec, out, work)
+            print("wrote", p, p.stat().st_size, "bytes")
+        for name, spec in FP_CASES.items():
+            if args.only and name != args.only:
+                continue
+            p = run_fp_case(name, spec, out, work)
             print("wrote", p, p.stat().st_size, "bytes")
         if not args.only:
             mp = ROOT / "compton2d_amd" / "data" / "medium_inputm.npz"

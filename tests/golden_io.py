@@ -48,3 +48,48 @@ class GoldenCase:
 
     def out(self, n: int, key: str) -> np.ndarray:
         return self.a["out%d_%s" % (n, key)]
+
+
+FP_CASES = ("fp_pick", "fp_inj")
+
+
+def fp_fic() -> np.ndarray:
+    """F_IC(num_nt, nphfield) of the reference setup, [NUM_NT, NPHFIELD]."""
+    return np.load(GOLDEN / "fp_fic.npz", allow_pickle=False)["F_IC"]
+
+
+class FpGoldenCase:
+    """Inputs and outputs of the reference's `update` (FP_calc for every zone)
+    per MC step, dumped by oracle/ref/c2d_refdrv.f (tests/golden/make_golden.py)."""
+
+    def __init__(self, name: str):
+        self.name = name
+        z = np.load(GOLDEN / (name + ".npz"), allow_pickle=False)
+        self.a = {k: z[k] for k in z.files}
+        self.meta = json.loads(bytes(self.a.pop("meta_json")).decode())
+        self.steps = list(self.meta["fp_steps"])
+        self.nz, self.nr = self.meta["nz"], self.meta["nr"]
+
+    def grid(self, **over) -> abi.GridConfig:
+        m, a = self.meta, self.a
+        g = abi.GridConfig(
+            nz=m["nz"], nr=m["nr"], rmin=m["rmin"], zmin=m["zmin"], z=a["cfg_z"], r=a["cfg_r"],
+            E_ph=a["E_ph"], E_field=a["cfg_E_field"], gnt=a["cfg_gnt"], hu=a["cfg_hu"],
+            Elcmin=a["cfg_Elcmin"], Elcmax=a["cfg_Elcmax"], mu=a["cfg_mu"])
+        for k, v in over.items():
+            setattr(g, k, v)
+        return g
+
+    def constants(self) -> abi.FpConstants:
+        return abi.FpConstants(F_IC=fp_fic(), **self.meta["fp_const"])
+
+    def fp_in(self, n: int) -> dict:
+        d = {k[len("fpin%d_" % n):]: v for k, v in self.a.items() if k.startswith("fpin%d_" % n)}
+        d.update({k: self.meta["fp%d" % n][k] for k in ("ncycle", "time", "dt")})
+        return d
+
+    def fp_out(self, n: int) -> dict:
+        d = {k[len("fpout%d_" % n):]: v for k, v in self.a.items() if k.startswith("fpout%d_" % n)}
+        d.update({k: self.meta["fp%d" % n][k] for k in ("E_tot_old", "E_tot_new", "hr_total",
+                                                       "hr_st_total", "dT_max")})
+        return d

@@ -31,8 +31,8 @@ def load(flavor: str = "ref") -> C.CDLL:
     if flavor in _libs:
         return _libs[flavor]
     path = ORACLE_DIR / "_build" / ("liboracle_%s.so" % flavor)
-    src = ORACLE_DIR / "c2d_oracle.c"
-    if not path.exists() or path.stat().st_mtime < src.stat().st_mtime:
+    srcs = (ORACLE_DIR / "c2d_oracle.c", ORACLE_DIR / "c2d_fp_oracle.c")
+    if not path.exists() or any(path.stat().st_mtime < s.stat().st_mtime for s in srcs):
         build()
     lib = C.CDLL(str(path))
     lib.c2o_create.restype = C.c_void_p
@@ -83,6 +83,11 @@ def load(flavor: str = "ref") -> C.CDLL:
     lib.c2o_unit_derive.restype = C.c_uint64
     lib.c2o_unit_derive.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
     lib.c2o_is_detmath.restype = C.c_int
+    lib.c2o_fp_step.restype = C.c_int
+    lib.c2o_fp_step.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.FpConfig),
+                                C.POINTER(abi.FpStepIn), C.POINTER(abi.FpStepOut)]
+    lib.c2o_gamma_bar.restype = C.c_double
+    lib.c2o_gamma_bar.argtypes = [C.c_double]
     _libs[flavor] = lib
     return lib
 
@@ -142,3 +147,15 @@ class Oracle:
         return self.lib.c2o_census_import(self.ctx, d6.ctypes.data_as(C.POINTER(C.c_double)),
                                           i5.ctypes.data_as(C.POINTER(C.c_int32)),
                                           keys.ctypes.data_as(C.POINTER(C.c_uint64)), len(keys))
+
+
+def fp_step(grid: abi.GridConfig, const: abi.FpConstants, ncycle: int, time: float, dt: float,
+            inputs: dict, state: dict, flavor: str = "det") -> dict:
+    """The oracle's `update` (oracle/c2d_fp_oracle.c): returns the new state."""
+    lib = load(flavor)
+    g, fc = grid.to_ctypes(), const.to_ctypes()
+    call = abi.FpCall(ncycle, time, dt, inputs, state)
+    rc = lib.c2o_fp_step(C.byref(g), C.byref(fc), C.byref(call.sin), C.byref(call.sout))
+    if rc != 0:
+        raise RuntimeError("c2o_fp_step failed: %d" % rc)
+    return call.result()

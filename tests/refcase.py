@@ -33,6 +33,12 @@ BASE_CASE = dict(
     g_bulk=33.0, split1=10, split2=10, split3=3, spl3_trg=10,
     # zone medium (src_20121026/inputm.dat:1-11)
     tea=100.0, tna=100.0, n_e=80.0, B=0.13, amxwl=0.0, gmin=1.0e2, gmax=1.0e5, p_nth=2.3,
+    q_turb=1.666667, turb_lev=1.0e-20,
+    # Fokker-Planck run constants (reader.f:512-557; src_20121026/input.dat:84-105)
+    cf_sentinel=0, r_flare=0.0, z_flare=0.0, t_flare=1.0e6, sigma_r=1.0e6, sigma_z=1.0e6,
+    sigma_t=1.0e6, flare_amp=0.0, r_esc=0.3, r_acc=1.0, inj_switch=0, inj_dis=2,
+    g2var_switch=0, pick_sw=0, inj_g1=1e2, inj_g2=3e4, inj_p=1.0, inj_t=1.2e6, inj_L=5e40,
+    pick_rate=0.8e-3, inj_gg=1e2, inj_sigma=1e1,
 )
 
 
@@ -92,17 +98,16 @@ def write_input_deck(case_dir: Path, case: dict) -> None:
     L.append(_line("dh_sentinel", 0))
     L.append(_line("pair_switch", c["pair_switch"]))
     L.append(_line("T_const", c["T_const"]))
-    L.append(_line("cf_sentinel", 0))
+    L.append(_line("cf_sentinel", c["cf_sentinel"]))
     for nm in ("r_flare", "z_flare", "t_flare", "sigma_r", "sigma_z", "sigma_t", "flare_amp"):
-        L.append(_line(nm, 0.0 if nm in ("r_flare", "z_flare", "flare_amp") else 1.0e6))
-    L.append(_line("r_esc", 0.3))
-    L.append(_line("r_acc", 1.0))
-    for nm, v in (("inj_switch", 0), ("inj_dis", 2), ("g2var_switch", 0), ("pick_sw", 0)):
-        L.append(_line(nm, v))
-    for nm, v in (("inj_g1", 1e2), ("inj_g2", 3e4), ("inj_p", 1.0), ("inj_t", 1.2e6),
-                  ("inj_L", 5e40), ("pick_rate", 0.8e-3), ("inj_gg", 1e2), ("inj_sigma", 1e1),
-                  ("g_bulk", float(c["g_bulk"]))):
-        L.append(_line(nm, float(v)))
+        L.append(_line(nm, float(c[nm])))
+    L.append(_line("r_esc", float(c["r_esc"])))
+    L.append(_line("r_acc", float(c["r_acc"])))
+    for nm in ("inj_switch", "inj_dis", "g2var_switch", "pick_sw"):
+        L.append(_line(nm, int(c[nm])))
+    for nm in ("inj_g1", "inj_g2", "inj_p", "inj_t", "inj_L", "pick_rate", "inj_gg", "inj_sigma",
+               "g_bulk"):
+        L.append(_line(nm, float(c[nm])))
     for nm, v in (("R_blr", 2.18e38), ("fr_blr", 0.1), ("R_ir", 0.78e19), ("fr_ir", 0.5),
                   ("R_disk", 1e17), ("d_jet", 0.5e17)):
         L.append(_line(nm, float(v)))
@@ -116,8 +121,8 @@ def write_input_deck(case_dir: Path, case: dict) -> None:
                 Z.append(_line(nm, float(v)))
             Z.append(_line("ep_switch", 0))
             for nm, v in (("B_field", c["B"]), ("amxwl", c["amxwl"]), ("gmin", c["gmin"]),
-                          ("gmax", c["gmax"]), ("p_nth", c["p_nth"]), ("q_turb", 1.666667),
-                          ("turb_lev", 1.0e-20)):
+                          ("gmax", c["gmax"]), ("p_nth", c["p_nth"]), ("q_turb", c["q_turb"]),
+                          ("turb_lev", c["turb_lev"])):
                 Z.append(_line(nm, float(v)))
             (d / "input" / ("input_%02d_%02d.dat" % (j, k))).write_text("".join(Z))
     src = REFERENCE / "disk" / c["spec_file"]
@@ -221,6 +226,46 @@ def read_step_out(case_dir: Path, n: int, cfg: dict) -> dict:
     txt = ev.read_text().split() if ev.exists() else []
     o["events"] = (np.array([float(x.replace("D", "E")) for x in txt]).reshape(-1, 7)
                    if txt else np.zeros((0, 7)))
+    return o
+
+
+FP_IN_ZONE = ("tea", "tna", "n_e", "B_field", "Eloss_sy", "ecens", "ec_old", "turb_lev", "vol",
+              "f_pair", "gmin", "gmax", "amxwl", "p_nth")
+FP_OUT_ZONE = ("Te_new", "tea", "n_e", "gmin", "gmax", "amxwl", "p_nth")
+
+
+def read_fic(case_dir: Path) -> np.ndarray:
+    """F_IC(num_nt, nphfield) of setup (icloss2d.f), as [NUM_NT, NPHFIELD]."""
+    R = _Reader(Path(case_dir) / "fic.bin")
+    return R.f8(abi.NUM_NT * abi.NPHFIELD).reshape(abi.NPHFIELD, abi.NUM_NT).T.copy()
+
+
+def has_fp(case_dir: Path, n: int) -> bool:
+    return (Path(case_dir) / ("fpin_%03d.bin" % n)).exists()
+
+
+def read_fp_in(case_dir: Path, n: int, cfg: dict) -> dict:
+    nz, nr = cfg["nz"], cfg["nr"]
+    R = _Reader(Path(case_dir) / ("fpin_%03d.bin" % n))
+    d = {"ncycle": int(R.i4(1)[0])}
+    d["time"], d["dt"] = (float(x) for x in R.f8(2))
+    for nm in FP_IN_ZONE:
+        d[nm] = R.f8(nz * nr).reshape(nz, nr)
+    for nm in ("f_nt", "Pnt"):
+        d[nm] = R.f8(nz * nr * abi.NUM_NT).reshape(nz, nr, abi.NUM_NT)
+    d["n_field"] = R.f8(nz * nr * abi.NPHFIELD).reshape(nz, nr, abi.NPHFIELD)
+    return d
+
+
+def read_fp_out(case_dir: Path, n: int, cfg: dict) -> dict:
+    nz, nr = cfg["nz"], cfg["nr"]
+    R = _Reader(Path(case_dir) / ("fpout_%03d.bin" % n))
+    o = dict(zip(("E_tot_old", "E_tot_new", "hr_total", "hr_st_total", "dT_max"),
+                 (float(x) for x in R.f8(5))))
+    for nm in FP_OUT_ZONE:
+        o[nm] = R.f8(nz * nr).reshape(nz, nr)
+    for nm in ("f_nt", "Pnt"):
+        o[nm] = R.f8(nz * nr * abi.NUM_NT).reshape(nz, nr, abi.NUM_NT)
     return o
 
 

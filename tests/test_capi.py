@@ -42,6 +42,11 @@ int main(void) {
   printf("c2d_config %zu\nc2d_step_in %zu\nc2d_tally_layout %zu\nc2d_fp_in %zu\nc2d_spectrum %zu\n",
          sizeof(c2d_config), sizeof(c2d_step_in), sizeof(c2d_tally_layout), sizeof(c2d_fp_in),
          sizeof(c2d_spectrum));
+  printf("c2d_fp_config %zu\nc2d_fp_step_in %zu\nc2d_fp_step_out %zu\n", sizeof(c2d_fp_config),
+         sizeof(c2d_fp_step_in), sizeof(c2d_fp_step_out));
+  P(c2d_fp_config, inj_v) P(c2d_fp_config, F_IC_s_ph) P(c2d_fp_config, pick_sw)
+  P(c2d_fp_step_in, n_field) P(c2d_fp_step_in, ecens) P(c2d_fp_step_in, dt)
+  P(c2d_fp_step_out, zone_diag) P(c2d_fp_step_out, dT_max) P(c2d_fp_step_out, p_nth)
   P(c2d_config, seed) P(c2d_config, rank) P(c2d_config, queue_capacity) P(c2d_config, mu)
   P(c2d_step_in, kappa_tot) P(c2d_step_in, nsv) P(c2d_step_in, tbbl) P(c2d_step_in, spectra)
   P(c2d_step_in, n_spectra) P(c2d_step_in, dt)
@@ -60,10 +65,15 @@ int main(void) {
     assert int(got["c2d_tally_layout"]) == C.sizeof(abi.TallyLayout)
     assert int(got["c2d_fp_in"]) == C.sizeof(abi.FpIn)
     assert int(got["c2d_spectrum"]) == C.sizeof(abi.Spectrum)
+    assert int(got["c2d_fp_config"]) == C.sizeof(abi.FpConfig)
+    assert int(got["c2d_fp_step_in"]) == C.sizeof(abi.FpStepIn)
+    assert int(got["c2d_fp_step_out"]) == C.sizeof(abi.FpStepOut)
+    classes = {"c2d_config": abi.Config, "c2d_step_in": abi.StepIn, "c2d_fp_config": abi.FpConfig,
+               "c2d_fp_step_in": abi.FpStepIn, "c2d_fp_step_out": abi.FpStepOut}
     for key, val in got.items():
         if "." in key:
             t, f = key.split(".")
-            cls = abi.Config if t == "c2d_config" else abi.StepIn
+            cls = classes[t]
             assert getattr(cls, f).offset == int(val), key
 
 

@@ -1,0 +1,71 @@
+"""GPU Fokker-Planck update (c2d_fp_step, compton2d_amd/csrc/fp.hip) against the
+oracle (oracle/c2d_fp_oracle.c, det-math build) on the reference's own FP inputs
+(tests/golden/fp_*.npz): every zone output bit-identical; E_add_up sums equal
+(both sum the per-zone shares in zone order).  The oracle's glibc build is
+pinned bit-exactly to the reference in tests/test_fp_oracle.py."""
+import numpy as np
+import pytest
+
+import oracle_lib as OL
+from compton2d_amd import abi
+from compton2d_amd.engine import Engine
+from golden_io import FP_CASES, FpGoldenCase, GoldenCase
+
+pytestmark = pytest.mark.gpu
+
+ZONE_KEYS = ("Te_new", "tea", "n_e", "gmin", "gmax", "amxwl", "p_nth", "f_nt", "Pnt", "zone_diag")
+
+
+@pytest.mark.parametrize("name", FP_CASES)
+def test_gpu_fp_bitwise_equals_oracle(name):
+    case = FpGoldenCase(name)
+    eng = Engine(case.grid(device=0))
+    eng.fp_set_config(case.constants())
+    for n in case.steps:
+        fi = case.fp_in(n)
+        g = eng.fp_step(fi["ncycle"], fi["time"], fi["dt"], fi, fi)
+        o = OL.fp_step(case.grid(), case.constants(), fi["ncycle"], fi["time"], fi["dt"], fi, fi,
+                       flavor="det")
+        for k in ZONE_KEYS:
+            np.testing.assert_array_equal(g[k], o[k], err_msg="%s step %d %s" % (name, n, k))
+        for k in ("E_tot_old", "E_tot_new", "hr_total", "hr_st_total", "dT_max"):
+            assert g[k] == o[k], (name, n, k, g[k], o[k])
+        ref = case.fp_out(n)       # and close to the reference itself
+        np.testing.assert_array_equal(g["Te_new"], ref["Te_new"])
+        assert np.max(np.abs(g["f_nt"] - ref["f_nt"])) <= 1e-10 * np.max(np.abs(ref["f_nt"]))
+    assert eng.last_fp_ms() > 0
+    eng.close()
+
+
+def test_gpu_fp_reads_photon_field_from_device_tallies():
+    """n_field / ecens = None: the kernel reads the fused tally buffer of the
+    preceding transport step directly (no host round trip)."""
+    tc = GoldenCase("ssc_tau")
+    fc = FpGoldenCase("fp_pick")
+    eng = Engine(tc.grid(comtot_mode=abi.COMTOT_EXACT, device=0))
+    eng.fp_set_config(fc.constants())
+    eng.transport_step(tc.step_inputs(0))
+    eng.transport_step(tc.step_inputs(1))
+    t = eng.tallies()
+    fi = fc.fp_in(fc.steps[0])
+    host = dict(fi, n_field=t["n_field"], ecens=t["ecens"])
+    dev = dict(fi, n_field=None, ecens=None)
+    a = eng.fp_step(2, fi["time"], fi["dt"], host, fi)
+    b = eng.fp_step(2, fi["time"], fi["dt"], dev, fi)
+    for k in ZONE_KEYS:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert a["E_tot_new"] == b["E_tot_new"]
+    eng.close()
+
+
+def test_gpu_fp_rejects_pairs_and_requires_config():
+    case = FpGoldenCase("fp_pick")
+    eng = Engine(case.grid(device=0))
+    fi = case.fp_in(case.steps[0])
+    with pytest.raises(Exception, match="C2D_E_STATE"):
+        eng.fp_step(fi["ncycle"], fi["time"], fi["dt"], fi, fi)
+    c = case.constants()
+    c.pair_switch = 1
+    with pytest.raises(Exception, match="C2D_E_ARG"):
+        eng.fp_set_config(c)
+    eng.close()
