@@ -154,6 +154,9 @@ enum : int32_t {
 enum : int32_t { FO_TE = 0, FO_NE, FO_GMIN, FO_GMAX, FO_AMXWL, FO_PNTH, FO_DIAG = 8, FO_N = 16 };
 enum : int32_t { FPERR_STEPS = 1, FPERR_GUARD = 2 };
 
+/* McDonald abscissa table: n < C2D_FP_MCD_N -> {t_n, ts_n, (ts_n^2-1)^1.5, (ts_n^2-1)^2.5} */
+#define C2D_FP_MCD_N 16384
+
 struct FpParams {
   int32_t nz, nr, pick_sw, inj_switch, inj_dis, g2var_switch, cf_sentinel, pad0;
   double time, dt, df_implicit, df_T, r_esc, r_acc;
@@ -162,6 +165,7 @@ struct FpParams {
   const Geo* geo;          /* grids: z[0]=zmin, r[0]=rmin, 1-based zones      */
   const double* gnt;       /* [num_nt]                                         */
   const double* FT;        /* [nphfield][num_nt]: F_IC transposed               */
+  const double* mcd;       /* [C2D_FP_MCD_N][4] McDonald table                 */
   const double* zin;       /* [ncell][FZ_N]                                    */
   const double* f_in;      /* [ncell][num_nt]                                  */
   const double* P_in;      /* [ncell][num_nt]                                  */

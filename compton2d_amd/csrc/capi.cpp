@@ -16,6 +16,7 @@
 
 #include "../../include/compton2d.h"
 #include "c2d_device.hpp"
+#include "c2d_math.h"
 #include "c2d_rng.h"
 
 using namespace c2d;
@@ -128,7 +129,7 @@ struct c2d_ctx {
   /* Fokker-Planck */
   bool fp_ready = false;
   c2d_fp_config fpc;
-  double *fp_FT = nullptr, *fp_zin = nullptr, *fp_fin = nullptr, *fp_Pin = nullptr,
+  double *fp_FT = nullptr, *fp_mcd = nullptr, *fp_zin = nullptr, *fp_fin = nullptr, *fp_Pin = nullptr,
          *fp_nf = nullptr, *fp_fout = nullptr, *fp_Pout = nullptr, *fp_zout = nullptr;
   int32_t* fp_err = nullptr;
   float last_fp_ms = 0.f;
@@ -291,7 +292,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
     if (c->cens[b].key) (void)hipFree(c->cens[b].key);
   }
   for (double* p : c->spec_bufs) (void)hipFree(p);
-  void* fptrs[] = {c->fp_FT, c->fp_zin, c->fp_fin, c->fp_Pin, c->fp_nf, c->fp_fout, c->fp_Pout,
+  void* fptrs[] = {c->fp_FT, c->fp_mcd, c->fp_zin, c->fp_fin, c->fp_Pin, c->fp_nf, c->fp_fout, c->fp_Pout,
                    c->fp_zout, c->fp_err};
   for (void* p : fptrs)
     if (p) (void)hipFree(p);
@@ -826,6 +827,23 @@ extern "C" int c2d_fp_set_config(c2d_ctx* c, const c2d_fp_config* fc) {
     HIPCHK(c, dalloc(&c->fp_Pout, nc * C2D_NUM_NT));
     HIPCHK(c, dalloc(&c->fp_zout, nc * FO_N));
     HIPCHK(c, dalloc(&c->fp_err, 1));
+    /* McDonald series abscissae (volume2d.f:604-620): t_n by repeated
+     * multiplication exactly as the reference loop forms it, with the
+     * argument-independent factors of each term (same c2d_math code and
+     * rounding as the kernel) */
+    std::vector<double> mt((size_t)C2D_FP_MCD_N * 4);
+    const double dtm = 1.001, sm = 5.0e-1 * (1.0 + dtm);
+    double t = 1.0;
+    for (int n = 0; n < C2D_FP_MCD_N; n++) {
+      const double ts = t * sm;
+      mt[(size_t)n * 4 + 0] = t;
+      mt[(size_t)n * 4 + 1] = ts;
+      mt[(size_t)n * 4 + 2] = c2d_pow(ts * ts - 1.0, 1.5);
+      mt[(size_t)n * 4 + 3] = c2d_pow(ts * ts - 1.0, 2.5);
+      t = t * dtm;
+    }
+    HIPCHK(c, dalloc(&c->fp_mcd, mt.size()));
+    HIPCHK(c, hipMemcpy(c->fp_mcd, mt.data(), mt.size() * sizeof(double), hipMemcpyHostToDevice));
   }
   /* F_IC(i, ph) -> FT[ph][i]: lanes (bins i) read consecutive addresses */
   std::vector<double> ft((size_t)C2D_NPHFIELD * C2D_NUM_NT);
@@ -900,7 +918,7 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   P.flare_amp = f.flare_amp; P.inj_g1 = f.inj_g1; P.inj_g2 = f.inj_g2; P.inj_p = f.inj_p;
   P.inj_t = f.inj_t; P.inj_L = f.inj_L; P.pick_rate = f.pick_rate; P.inj_gg = f.inj_gg;
   P.inj_sigma = f.inj_sigma; P.inj_v = f.inj_v;
-  P.geo = c->geo; P.gnt = c->gnt; P.FT = c->fp_FT; P.zin = c->fp_zin; P.f_in = c->fp_fin;
+  P.geo = c->geo; P.gnt = c->gnt; P.FT = c->fp_FT; P.mcd = c->fp_mcd; P.zin = c->fp_zin; P.f_in = c->fp_fin;
   P.P_in = c->fp_Pin;
   P.nf = nf_dev ? c->T + c->L.n_field : c->fp_nf;    /* tally layout: [cell][nphfield] */
   P.ecens = ecens_dev ? c->T + c->L.ecens : nullptr;

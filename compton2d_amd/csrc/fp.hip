@@ -17,11 +17,11 @@
  *     lane in the reference order from LDS (broadcast reads), so no
  *     cross-lane exchange is needed;
  *   - McDonald's series (src/volume2d.f:598-626), thousands of terms per
- *     call inside the temperature search, computes 64 terms per pass in
- *     parallel: the abscissa chain t <- t*1.001 is replayed per lane in
- *     the reference's multiplication order, the expensive pow/exp terms are
- *     lane-parallel, and the terms are accumulated in order through
- *     readlane, up to the reference's stopping term.
+ *     call inside the temperature search, evaluates K2 and K3 together, 64
+ *     terms per pass: the argument-independent parts of each term come from
+ *     a table (see mcdonald23_w), exp(z*ts) is lane-parallel, and the terms
+ *     are accumulated in order through readlane up to the reference's
+ *     stopping term.
  * Arithmetic is c2d_math.h with -ffp-contract=off, so results equal the
  * det-math build of the oracle (oracle/c2d_fp_oracle.c) bit for bit.
  * Branches of FP_calc that never reach an output (Coulomb/Moeller rates
@@ -93,6 +93,36 @@ __device__ __forceinline__ double rl(double v, int m) {
   return __hiloint2double(hi, lo);
 }
 
+/* acc = acc + f(i) for i = lo..hi, in this order: f is evaluated lane-parallel
+ * (bin i = c0 + lane of each 64-bin chunk), the additions run in sequence on
+ * wave-uniform values fetched with readlane, so the rounding is that of the
+ * reference's serial loop while no LDS load sits on the dependency chain. */
+template <class F>
+__device__ __forceinline__ double seq_sum(double acc, int lo, int hi, int lane, F f) {
+  for (int c0 = lo; c0 <= hi; c0 += FPB) {
+    const int i = c0 + lane;
+    const double v = (i <= hi) ? f(i) : 0.0;
+    const int mn = (hi - c0 + 1) < FPB ? (hi - c0 + 1) : FPB;
+    for (int m = 0; m < mn; m++) acc = acc + rl(v, m);
+  }
+  return acc;
+}
+/* two independent serial sums over the same bins, interleaved */
+template <class F, class G>
+__device__ __forceinline__ void seq_sum2(double& a1, double& a2, int lo, int hi, int lane, F f,
+                                         G g) {
+  for (int c0 = lo; c0 <= hi; c0 += FPB) {
+    const int i = c0 + lane;
+    const double v1 = (i <= hi) ? f(i) : 0.0;
+    const double v2 = (i <= hi) ? g(i) : 0.0;
+    const int mn = (hi - c0 + 1) < FPB ? (hi - c0 + 1) : FPB;
+    for (int m = 0; m < mn; m++) {
+      a1 = a1 + rl(v1, m);
+      a2 = a2 + rl(v2, m);
+    }
+  }
+}
+
 /* gammln (volume2d.f:647-668) */
 __device__ double gammln(double xx) {
   const double cof[6] = {76.18009172947146, -86.50532032941677, 24.01409824083091,
@@ -109,31 +139,68 @@ __device__ double gammln(double xx) {
   return tmp + c2d_log(stp * ser / x);
 }
 
-/* McDonald (volume2d.f:598-626), 64 series terms per pass (wave-uniform call) */
-__device__ double mcdonald_w(double nu, double z, int lane, long long& guard) {
-  const double dt = 1.001, d = dt - 1.0, s = 5.0e-1 * (1.0 + dt), a = nu - 5.0e-1;
-  double sum = 0.0, t0 = 1.0;
-  for (;;) {
-    double t = t0;
-    for (int m = 0; m < lane; m++) t = t * dt;   /* the reference's t after `lane` terms */
-    const double ts = t * s;
+/* McDonald (volume2d.f:598-626) for nu = 2 and 3 together, 64 series terms per
+ * pass (wave-uniform call).  Both series run over the same abscissae
+ * t_n = 1.001^n (by repeated multiplication), ts_n = t_n*s, and
+ * (ts_n^2 - 1)^a: those depend on n only, so the first C2D_FP_MCD_N of them
+ * come from a table built once on the host with the same c2d_math code
+ * (c2d_fp_set_config); only exp(z*ts) depends on the argument.  Beyond the
+ * table the abscissa chain is replayed per lane from the last value.  Terms
+ * are added in the reference's order up to each series' own stopping term,
+ * so K2 and K3 equal two sequential McDonald calls bit for bit. */
+__device__ void mcdonald23_w(double z, int lane, const double* __restrict__ tab, double& K2,
+                             double& K3, long long& guard) {
+  const double dt = 1.001, d = dt - 1.0, s = 5.0e-1 * (1.0 + dt);
+  double sum2 = 0.0, sum3 = 0.0, t0 = 1.0;
+  bool run2 = true, run3 = true;
+  for (int n0 = 0; run2 || run3; n0 += FPB) {
+    const int n = n0 + lane;
+    double t, ts, p2, p3;
+    if (n0 + FPB <= C2D_FP_MCD_N) {
+      const double* e = tab + (size_t)n * 4;
+      t = e[0]; ts = e[1]; p2 = e[2]; p3 = e[3];
+    } else {
+      t = t0;
+      for (int m = 0; m < lane; m++) t = t * dt;
+      ts = t * s;
+      p2 = c2d_pow(ts * ts - 1.0, 1.5);
+      p3 = c2d_pow(ts * ts - 1.0, 2.5);
+    }
     const double y = z * ts;
-    double sd = 0.0;
-    if (y < 2.25e2) sd = c2d_pow(ts * ts - 1.0, a) / c2d_exp(y);
-    const double term = d * t * sd;
+    double sd2 = 0.0, sd3 = 0.0;
+    if (y < 2.25e2) {
+      const double ey = c2d_exp(y);
+      sd2 = p2 / ey;
+      sd3 = p3 / ey;
+    }
+    const double term2 = d * t * sd2, term3 = d * t * sd3;
     const double tn = t * dt;
-    const unsigned long long stop = __ballot(!(tn < 2.0 || sd > 1.0e-8));
-    const int nterm = stop ? __ffsll((long long)stop) : FPB;
-    for (int m = 0; m < nterm; m++) sum = sum + rl(term, m);
-    guard += nterm;
-    if (stop || guard > GUARD_MAX) break;
+    const unsigned long long st2 = __ballot(!(tn < 2.0 || sd2 > 1.0e-8));
+    const unsigned long long st3 = __ballot(!(tn < 2.0 || sd3 > 1.0e-8));
+    const int n2 = run2 ? (st2 ? __ffsll((long long)st2) : FPB) : 0;
+    const int n3 = run3 ? (st3 ? __ffsll((long long)st3) : FPB) : 0;
+    const int nm = n2 > n3 ? n2 : n3;
+    if (n2 == FPB && n3 == FPB) {
+      for (int m = 0; m < FPB; m++) {
+        sum2 = sum2 + rl(term2, m);
+        sum3 = sum3 + rl(term3, m);
+      }
+    } else {
+      for (int m = 0; m < n2; m++) sum2 = sum2 + rl(term2, m);
+      for (int m = 0; m < n3; m++) sum3 = sum3 + rl(term3, m);
+    }
+    if (st2) run2 = false;
+    if (st3) run3 = false;
+    guard += nm;
+    if (guard > GUARD_MAX) break;
     t0 = rl(tn, FPB - 1);
   }
-  return __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, nu) * sum / c2d_exp(gammln(5.0e-1 + nu));
+  K2 = __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, 2.0) * sum2 / c2d_exp(gammln(5.0e-1 + 2.0));
+  K3 = __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, 3.0) * sum3 / c2d_exp(gammln(5.0e-1 + 3.0));
 }
 
 /* gamma_bar (volume2d.f:572-594) */
-__device__ double gamma_bar_w(double Theta, int lane, long long& guard) {
+__device__ double gamma_bar_w(double Theta, int lane, const double* tab, long long& guard) {
   double g;
   if (Theta < F32(0.2)) {
     g = (1. + F32(4.375) * Theta + F32(7.383) * (Theta * Theta) +
@@ -141,8 +208,8 @@ __device__ double gamma_bar_w(double Theta, int lane, long long& guard) {
             (1. + F32(1.875) * Theta + F32(.8203) * (Theta * Theta)) -
         Theta;
   } else {
-    const double K2 = mcdonald_w(2.0, 1.0 / Theta, lane, guard);
-    const double K3 = mcdonald_w(3.0, 1.0 / Theta, lane, guard);
+    double K2, K3;
+    mcdonald23_w(1.0 / Theta, lane, tab, K2, K3, guard);
     g = K3 / K2 - Theta;
   }
   if (g < 1.0) g = 1.0;
@@ -198,12 +265,13 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
 
   /* E_el, normalisation (:482-509) */
   double E_el = 0.0, E_pos = 0.0;
-  for (int i = 2; i <= NT; i++) E_el = E_el + (s_gnt[i] - s_gnt[i - 1]) * s_gam[i] * s_fold[i];
+  E_el = seq_sum(E_el, 2, NT, lane,
+                 [&](int i) { return (s_gnt[i] - s_gnt[i - 1]) * s_gam[i] * s_fold[i]; });
   E_el = E_el * ne * 8.176e-7 * volume;
   double e_old = 0.0 + E_el + E_pos + zin[FZ_ECOLD];
   double e_new = 0.0 + ecens;
-  double sum_p = 0.;
-  for (int i = 1; i <= NT - 1; i++) sum_p = sum_p + (s_gnt[i + 1] - s_gnt[i]) * s_fold[i];
+  double sum_p = seq_sum(0., 1, NT - 1, lane,
+                         [&](int i) { return (s_gnt[i + 1] - s_gnt[i]) * s_fold[i]; });
   __syncthreads();
   for (int i = lane + 1; i <= NT; i += FPB) s_fold[i] = s_fold[i] / sum_p;
   __syncthreads();
@@ -240,10 +308,11 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
   int fp_steps = 0;
   for (;;) {
     /* label 200 (:577) */
-    double g_av = gamma_bar_w(Th_e, lane, guard);
-    double hr_th_c = 0.0;
-    for (int i = 1; i <= NT - 1; i++)
-      hr_th_c = hr_th_c - 8.176e-7 * s_dgic[i] * s_fold[i] * (s_gnt[i + 1] - s_gnt[i]) * volume * n_lept;
+    double g_av = gamma_bar_w(Th_e, lane, P.mcd, guard);
+    /* hr_th_c = hr_th_c - x_i, i.e. + (-x_i) bit for bit */
+    const double hr_th_c = seq_sum(0.0, 1, NT - 1, lane, [&](int i) {
+      return -(8.176e-7 * s_dgic[i] * s_fold[i] * (s_gnt[i + 1] - s_gnt[i]) * volume * n_lept);
+    });
     if (fp_steps > MAX_FP_STEPS) {
       if (lane == 0) atomicOr(P.err, FPERR_STEPS);
       return;
@@ -273,11 +342,22 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
       s_dgdt[i] = dg_sy + s_dgic[i] + dg_A;
     }
     double hr_nt_A = 0.0, hr_st_A = 0.0;
-    for (int i = 1; i <= NT - 1; i++) {
-      const double gi = s_gam[i];
-      const double dg_A = gi / t_acc;
-      hr_nt_A = hr_nt_A + dg_A * s_fold[i] * (s_gam[i + 1] - gi);
-      if (gi > g_thr) hr_st_A = hr_st_A + dg_A * s_fold[i] * (s_gam[i + 1] - gi);
+    for (int c0 = 1; c0 <= NT - 1; c0 += FPB) {        /* loop 350 sums, in order */
+      const int i = c0 + lane;
+      double v = 0.0;
+      bool st = false;
+      if (i <= NT - 1) {
+        const double gi = s_gam[i];
+        v = gi / t_acc * s_fold[i] * (s_gam[i + 1] - gi);
+        st = gi > g_thr;
+      }
+      const unsigned long long stm = __ballot(st);
+      const int mn = (NT - c0) < FPB ? (NT - c0) : FPB;
+      for (int m = 0; m < mn; m++) {
+        const double x = rl(v, m);
+        hr_nt_A = hr_nt_A + x;
+        if ((stm >> m) & 1ull) hr_st_A = hr_st_A + x;
+      }
     }
     hr_st_A = hr_st_A * 8.176e-7 * n_lept * volume;
     hr_nt_A = hr_nt_A * 8.176e-7 * n_lept * volume;
@@ -302,8 +382,8 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
                    (P.inj_sigma * __builtin_sqrt(2.0 * PI_REF));
       }
       __syncthreads();
-      inj_sum = 0.0;
-      for (int i = 1; i <= NT - 1; i++) inj_sum = inj_sum + s_inj[i] * (s_gnt[i + 1] - s_gnt[i]);
+      inj_sum = seq_sum(0.0, 1, NT - 1, lane,
+                        [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); });
       inj_rho = P.pick_rate * d_t;
       inj_any = true;
     }
@@ -315,7 +395,8 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
         s_fold[i] = s_fold[i] + v / ne;
       }
       __syncthreads();
-      for (int i = 1; i <= NT - 1; i++) n_inject = n_inject + s_inj[i] * (s_gnt[i + 1] - s_gnt[i]);
+      n_inject = seq_sum(n_inject, 1, NT - 1, lane,
+                         [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); });
     }
     if (P.inj_switch != 0) {
       const double tt = P.time + t_fp - P.inj_t;
@@ -342,10 +423,9 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
         }
         __syncthreads();
         double isum = 0.0, inj_E = 0.0;
-        for (int i = 1; i <= NT - 1; i++) {
-          isum = isum + s_inj[i] * (s_gnt[i + 1] - s_gnt[i]);
-          inj_E = inj_E + s_inj[i] * (s_gnt[i + 1] - s_gnt[i]) * s_gam[i];
-        }
+        seq_sum2(isum, inj_E, 1, NT - 1, lane,
+                 [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); },
+                 [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]) * s_gam[i]; });
         inj_E = inj_E / isum;
         const double inj_rate = P.inj_L / 8.186e-7 / inj_E / (PI_REF * (rmax * rmax) * dz);
         const double rho = inj_rate * d_t;
@@ -356,7 +436,8 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
           s_fold[i] = s_fold[i] + v / ne;
         }
         __syncthreads();
-        for (int i = 1; i <= NT - 1; i++) n_inject = n_inject + s_inj[i] * (s_gnt[i + 1] - s_gnt[i]);
+        n_inject = seq_sum(n_inject, 1, NT - 1, lane,
+                           [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); });
       }
     }
     ne = ne + n_inject;
@@ -399,36 +480,62 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
       s_a[NT] = 0.0; s_b[NT] = 1.0; s_c[NT] = 0.0;
     }
     __syncthreads();
-    /* tridag (:2476-2518) in the reference order; gam kept in s_smw */
+    /* tridag (:2476-2518): the recurrences run in the reference order on
+     * wave-uniform values (readlane) with each 64-bin chunk's operands staged
+     * in registers; gam is kept in s_smw */
     {
       double bet = s_b[1];
       double u = s_fold[1] / bet;
       bool zero = false;
       if (lane == 0) s_fnew[1] = u;
-      for (int i = 2; i <= NT; i++) {
-        const double gam = s_c[i - 1] / bet;
-        bet = s_b[i] - s_a[i] * gam;
-        if (fabs(bet) <= 1.0e-100) {
-          zero = true;
-          break;
+      for (int c0 = 2; c0 <= NT && !zero; c0 += FPB) {
+        const int i = c0 + lane;
+        const bool in = i <= NT;
+        const double av = in ? s_a[i] : 0.0, bv = in ? s_b[i] : 0.0;
+        const double cv = in ? s_c[i - 1] : 0.0, rv = in ? s_fold[i] : 0.0;
+        double gmine = 0.0, umine = 0.0;
+        const int mn = (NT - c0 + 1) < FPB ? (NT - c0 + 1) : FPB;
+        for (int m = 0; m < mn; m++) {
+          const double am = rl(av, m);
+          const double gam = rl(cv, m) / bet;
+          bet = rl(bv, m) - am * gam;
+          if (fabs(bet) <= 1.0e-100) {
+            zero = true;
+            break;
+          }
+          u = (rl(rv, m) - am * u) / bet;
+          if (lane == m) {
+            gmine = gam;
+            umine = u;
+          }
         }
-        u = (s_fold[i] - s_a[i] * u) / bet;
-        if (lane == 0) {
-          s_smw[i] = gam;
-          s_fnew[i] = u;
+        if (!zero && in) {
+          s_smw[i] = gmine;
+          s_fnew[i] = umine;
         }
       }
       __syncthreads();
       if (zero) {
         for (int i = lane + 1; i <= NT; i += FPB) s_fnew[i] = 0.0;
-      } else if (lane == 0) {
+      } else {
+        /* back substitution on the unclipped values, then the reference's
+         * clipping of u(2..num_nt) (each u(i+1) is clipped after u(i) used it) */
         double up = s_fnew[NT];
-        for (int i = NT - 1; i >= 1; i--) {
-          double ui = s_fnew[i] - s_smw[i + 1] * up;
-          if (up < 0.0) s_fnew[i + 1] = 0.0;
-          s_fnew[i] = ui;
-          up = ui;
+        for (int c1 = NT - 1; c1 >= 1; c1 -= FPB) {
+          const int i = c1 - lane;
+          const bool in = i >= 1;
+          const double fv = in ? s_fnew[i] : 0.0, gv = in ? s_smw[i + 1] : 0.0;
+          double mine = 0.0;
+          const int mn = c1 < FPB ? c1 : FPB;
+          for (int m = 0; m < mn; m++) {
+            up = rl(fv, m) - rl(gv, m) * up;
+            if (lane == m) mine = up;
+          }
+          if (in) s_fnew[i] = mine;
         }
+        __syncthreads();
+        for (int i = lane + 2; i <= NT; i += FPB)
+          if (s_fnew[i] < 0.0) s_fnew[i] = 0.0;
       }
       __syncthreads();
     }
@@ -439,11 +546,22 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
     __syncthreads();
     sum_p = 0.;
     double sE = 0.;
-    for (int i = 1; i <= NT - 1; i++) {              /* :1415-1419 */
-      const double fi = s_fnew[i];
-      sum_p = sum_p + (s_gnt[i + 1] - s_gnt[i]) * fi;
-      sE = sE + (s_gnt[i + 1] - s_gnt[i]) * s_gam[i] * fi;
-      if (lane == 0) s_Pnt[i] = sum_p;
+    for (int c0 = 1; c0 <= NT - 1; c0 += FPB) {       /* :1415-1419 */
+      const int i = c0 + lane;
+      double av = 0.0, bv = 0.0;
+      if (i <= NT - 1) {
+        const double fi = s_fnew[i], dg = s_gnt[i + 1] - s_gnt[i];
+        av = dg * fi;
+        bv = dg * s_gam[i] * fi;
+      }
+      double mine = 0.0;
+      const int mn = (NT - c0) < FPB ? (NT - c0) : FPB;
+      for (int m = 0; m < mn; m++) {
+        sum_p = sum_p + rl(av, m);
+        sE = sE + rl(bv, m);
+        if (lane == m) mine = sum_p;
+      }
+      if (i <= NT - 1) s_Pnt[i] = mine;
     }
     sum_E = sE / sum_p;
     t_fp = t_fp + d_t;
@@ -456,19 +574,20 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
     }
     __syncthreads();
     /* new temperature (:1440-1468) */
-    double gbar = 0.0;
-    for (int i = 1; i <= NT - 1; i++) gbar = gbar + s_gam[i] * s_fnew[i] * (s_gnt[i + 1] - s_gnt[i]);
+    const double gbar = seq_sum(0.0, 1, NT - 1, lane, [&](int i) {
+      return s_gam[i] * s_fnew[i] * (s_gnt[i + 1] - s_gnt[i]);
+    });
     double The_new = Th_e;
     if (gbar > g_av) {
       while (gbar > g_av) {
         The_new = The_new * F32(1.005);
-        g_av = gamma_bar_w(The_new, lane, guard);
+        g_av = gamma_bar_w(The_new, lane, P.mcd, guard);
         if (guard > GUARD_MAX) break;
       }
     } else {
       while (gbar < g_av) {
         The_new = The_new / F32(1.005);
-        g_av = gamma_bar_w(The_new, lane, guard);
+        g_av = gamma_bar_w(The_new, lane, P.mcd, guard);
         if (The_new < 1.0e-2) break;
         if (guard > GUARD_MAX) break;
       }
@@ -485,7 +604,8 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
   /* outputs (:1481-1500) */
   E_el = 0.0;
   E_pos = 0.0;
-  for (int i = 2; i <= NT; i++) E_el = E_el + s_fnew[i] * s_gam[i] * (s_gnt[i] - s_gnt[i - 1]);
+  E_el = seq_sum(E_el, 2, NT, lane,
+                 [&](int i) { return s_fnew[i] * s_gam[i] * (s_gnt[i] - s_gnt[i - 1]); });
   E_el = E_el * ne * 8.176e-7 * volume;
   e_new = e_new + E_el + E_pos;
   for (int i = lane; i < NT; i += FPB) {
@@ -501,13 +621,9 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
   for (i = NT - 5; i >= 5; i--)
     if (s_fnew[i] > 1.0e-15) break;
   const double gmax = s_gam[i];
-  double sum_nt = 0.0, sum_th = 0.0;
-  for (i = 1; i <= NT - 1; i++) {
-    if (i < i_nt)
-      sum_th = sum_th + (s_gam[i + 1] - s_gam[i]) * s_fnew[i];
-    else
-      sum_nt = sum_nt + (s_gam[i + 1] - s_gam[i]) * s_fnew[i];
-  }
+  const auto dfn = [&](int q) { return (s_gam[q + 1] - s_gam[q]) * s_fnew[q]; };
+  const double sum_th = seq_sum(0.0, 1, i_nt - 1, lane, dfn);
+  const double sum_nt = seq_sum(0.0, i_nt, NT - 1, lane, dfn);
   double amxwl = sum_th / (sum_nt + sum_th);
   double p_nth = zin[FZ_PNTH];
   if (amxwl > 9.999e-1) {
@@ -532,14 +648,19 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
         N_nt = (1. - amxwl) * p_1 / (c2d_pow(gmax, p_1) - c2d_pow(gmin, p_1));
       else
         N_nt = (1.0 - amxwl) / c2d_log(gmax / gmin);
-      __syncthreads();
-      for (int q = i_nt + lane; q < i_end; q += FPB)
-        s_inj[q] = N_nt / (c2d_pow(s_gam[q], p_nth) * c2d_exp(s_gam[q] / gmax));
-      __syncthreads();
-      for (int q = i_nt; q < i_end; q++) {
-        const double f_pl = s_inj[q];
-        sum_g = sum_g + f_pl * s_gam[q] * (s_gnt[q + 1] - s_gnt[q]);
-        sum_gg = sum_gg + f_pl * (s_gnt[q + 1] - s_gnt[q]);
+      for (int c0 = i_nt; c0 < i_end; c0 += FPB) {
+        const int q = c0 + lane;
+        double v1 = 0.0, v2 = 0.0;
+        if (q < i_end) {
+          const double f_pl = N_nt / (c2d_pow(s_gam[q], p_nth) * c2d_exp(s_gam[q] / gmax));
+          v1 = f_pl * s_gam[q] * (s_gnt[q + 1] - s_gnt[q]);
+          v2 = f_pl * (s_gnt[q + 1] - s_gnt[q]);
+        }
+        const int mn = (i_end - c0) < FPB ? (i_end - c0) : FPB;
+        for (int m = 0; m < mn; m++) {
+          sum_g = sum_g + rl(v1, m);
+          sum_gg = sum_gg + rl(v2, m);
+        }
       }
       sum_g = sum_g / sum_gg;
       sum_g = fabs(sum_g - sum_E);
