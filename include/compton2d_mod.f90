@@ -3,14 +3,16 @@
 ! This is the binding a maintainer adds to the reference's Fortran host
 ! (bbw7561135/Compton2d src/) so that the worker-side calls
 !     call imcfield2d ; call imcvol2d ; call imcsurf2d      (src/xec2d.f:167-176)
-! become one c2d_transport_step() per GPU, with the COMMON tables passed in
-! place through (c_loc, strides).  See INTEGRATION.md.
+! become one c2d_transport_step() per GPU, and `call update`
+! (src/xec2d.f:86-87, src/update2d.f:7-327) one c2d_fp_step(), with the COMMON
+! tables passed in place through (c_loc, strides).  See INTEGRATION.md.
 module compton2d
   use iso_c_binding
   implicit none
 
   integer(c_int), parameter :: C2D_OK = 0, C2D_E_ARG = -1, C2D_E_HIP = -2, &
-       C2D_E_CENSUS_OVERFLOW = -3, C2D_E_EVENT_OVERFLOW = -4, C2D_E_QUEUE_OVERFLOW = -5
+       C2D_E_CENSUS_OVERFLOW = -3, C2D_E_EVENT_OVERFLOW = -4, C2D_E_QUEUE_OVERFLOW = -5, &
+       C2D_E_NOMEM = -6, C2D_E_STATE = -7, C2D_E_FP = -8
   integer(c_int32_t), parameter :: C2D_COMTOT_EXACT = 0, C2D_COMTOT_TABLE = 1
   integer, parameter :: C2D_NCOUNTERS = 16, C2D_CNT_STEPS = 0, C2D_CNT_ESCAPES = 1, &
        C2D_CNT_CENSUS = 2
@@ -66,6 +68,47 @@ module compton2d
      integer(c_int32_t) :: n_spectra = 0
      type(c_ptr) :: spectra = c_null_ptr
   end type c2d_step_in
+
+  ! ---- Fokker-Planck update (c2d_fp_set_config / c2d_fp_step) ----
+  integer, parameter :: C2D_FP_NDIAG = 8, C2D_FP_STEPS = 5, C2D_FP_SKIPPED = 6
+
+  type, bind(C) :: c2d_marray3
+     type(c_ptr) :: data = c_null_ptr
+     integer(c_int64_t) :: s_i = 0, s_j = 0, s_k = 0
+  end type c2d_marray3
+
+  type, bind(C) :: c2d_marray2
+     type(c_ptr) :: data = c_null_ptr
+     integer(c_int64_t) :: s_j = 0, s_k = 0
+  end type c2d_marray2
+
+  type, bind(C) :: c2d_fp_config              ! reader.f:512-559, general.pa:27-28
+     integer(c_int32_t) :: pair_switch = 0
+     real(c_double) :: df_implicit = 1.d-2, df_T = 2.5d-1, r_esc = 0.3d0, r_acc = 1.d0
+     integer(c_int32_t) :: cf_sentinel = 0
+     real(c_double) :: r_flare = 0, z_flare = 0, t_flare = 0, sigma_r = 1, sigma_z = 1, &
+          sigma_t = 1, flare_amp = 0
+     integer(c_int32_t) :: inj_switch = 0, inj_dis = 2, g2var_switch = 0, pick_sw = 0
+     real(c_double) :: inj_g1 = 0, inj_g2 = 0, inj_p = 0, inj_t = 0, inj_L = 0, &
+          pick_rate = 0, inj_gg = 0, inj_sigma = 1, inj_v = 0
+     type(c_ptr) :: F_IC = c_null_ptr             ! F_IC(num_nt, nphfield), COMMON /fic/
+     integer(c_int64_t) :: F_IC_s_i = 1, F_IC_s_ph = 200
+  end type c2d_fp_config
+
+  type, bind(C) :: c2d_fp_step_in              ! what FP_send_job packs (fp_mpi.f:632-686)
+     integer(c_int32_t) :: ncycle = 0
+     real(c_double) :: time = 0, dt = 0
+     type(c2d_array2) :: tea, tna, n_e, B_field, Eloss_sy, ec_old, turb_lev, vol
+     type(c2d_array2) :: f_pair, ecens           ! ecens: null data = device tallies
+     type(c2d_array3) :: n_field                 ! null data = device tallies
+  end type c2d_fp_step_in
+
+  type, bind(C) :: c2d_fp_step_out             ! updated in place (fp_mpi.f:972-1003)
+     type(c2d_marray3) :: f_nt, Pnt
+     type(c2d_marray2) :: Te_new, tea, n_e, gmin, gmax, amxwl, p_nth
+     type(c_ptr) :: zone_diag = c_null_ptr
+     real(c_double) :: E_tot_old = 0, E_tot_new = 0, hr_total = 0, hr_st_total = 0, dT_max = 0
+  end type c2d_fp_step_out
 
   type, bind(C) :: c2d_tally_layout
      integer(c_int64_t) :: edep, prdep, ecens, npcen, n_field, E_IC, nelectron, fout, &
@@ -160,5 +203,18 @@ module compton2d
        integer(c_int64_t), intent(in) :: keys(*)
        integer(c_int64_t), value :: n
      end function c2d_census_import
+
+     integer(c_int) function c2d_fp_set_config(ctx, fcfg) bind(C, name='c2d_fp_set_config')
+       import :: c_int, c_ptr, c2d_fp_config
+       type(c_ptr), value :: ctx
+       type(c2d_fp_config), intent(in) :: fcfg
+     end function c2d_fp_set_config
+
+     integer(c_int) function c2d_fp_step(ctx, fin, fout) bind(C, name='c2d_fp_step')
+       import :: c_int, c_ptr, c2d_fp_step_in, c2d_fp_step_out
+       type(c_ptr), value :: ctx
+       type(c2d_fp_step_in), intent(in) :: fin
+       type(c2d_fp_step_out), intent(inout) :: fout
+     end function c2d_fp_step
   end interface
 end module compton2d
