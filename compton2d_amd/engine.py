@@ -211,6 +211,21 @@ class Engine:
             i5.ctypes.data_as(C.POINTER(C.c_int32)), keys.ctypes.data_as(C.POINTER(C.c_uint64)),
             len(keys)))
 
+    def save_census(self, path) -> int:
+        """Checkpoint the device census as a reference record file
+        (write_cens, src/census2d.f:1-36) + `<path>.keys`; returns the count."""
+        from . import census_io
+        d6, i5, keys = self.census()
+        census_io.write_census(path, d6, i5, keys)
+        return len(keys)
+
+    def load_census(self, path) -> int:
+        """Restart from a census record file (read_cens, src/census2d.f:40-76)."""
+        from . import census_io
+        d6, i5, keys = census_io.read_census(path)
+        self.import_census(d6, i5, keys)
+        return len(keys)
+
     def last_kernel_ms(self):
         """(generation-0 kernel ms, all launches ms, launches) of the last step (HIP events)."""
         g0, al, nl = C.c_double(), C.c_double(), C.c_int32()

@@ -48,4 +48,8 @@ objs=""
 for f in $OBJS; do objs="$objs $OUT/obj/$f.o"; done
 "$FC" -o "$OUT/c2d_refdrv" "$OUT/obj/c2d_refdrv.o" $objs \
   -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
-echo "build_ref: $OUT/c2d_refdrv"
+"$FC" -c $FFLAGS -I"$MPI_INC" -I"$SRC" -module-dir "$OUT/mod" \
+  "$HERE/c2d_censdrv.f" -o "$OUT/obj/c2d_censdrv.o"
+"$FC" -o "$OUT/c2d_censdrv" "$OUT/obj/c2d_censdrv.o" "$OUT/obj/census2d.o" \
+  -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
+echo "build_ref: $OUT/c2d_refdrv $OUT/c2d_censdrv"

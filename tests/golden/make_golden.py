@@ -142,6 +142,38 @@ def run_fp_case(name: str, spec: dict, out_dir: Path, work: Path) -> Path:
     return path
 
 
+def make_census_format(out_dir: Path, work: Path) -> Path:
+    """The reference's own write_cens/read_cens (src/census2d.f) on a set of
+    records covering the e14.7 edge cases; pins compton2d_amd/census_io.py."""
+    import subprocess
+    drv = ROOT / "oracle" / "_ref" / "c2d_censdrv"
+    rng = np.random.default_rng(5)
+    n = 200
+    d = np.column_stack([rng.uniform(0, 7.5e15, n), rng.uniform(0, 1e16, n), rng.uniform(-1, 1, n),
+                         rng.uniform(0, 6.3, n), 10 ** rng.uniform(30, 46, n),
+                         10 ** rng.uniform(-7, 11, n)])
+    d[0] = [0.0, -1.5e-5, -0.99999999, 6.2831853072, 9.999999951e45, 1.234567850e-7]
+    d[1] = [1e-120, 5e120, 0.5, 1.0, 123456789.0, 0.099999995]
+    i6 = np.column_stack([rng.integers(0, 129, n), rng.integers(0, 6, n), rng.integers(1, 33, n),
+                          rng.integers(1, 100, n), rng.integers(1, 100, n),
+                          rng.integers(0, 100000, n)]).astype(np.int32)
+    w = work / "census"
+    w.mkdir(parents=True, exist_ok=True)
+    with open(w / "in.bin", "wb") as f:
+        f.write(np.array([n], "<i4").tobytes())
+        f.write(d.astype("<f8").tobytes())
+        f.write(i6.astype("<i4").tobytes())
+    subprocess.run([str(drv), "w", str(w / "in.bin"), str(w / "ref.txt")], check=True)
+    subprocess.run([str(drv), "r", str(w / "ref.txt"), str(n), str(w / "back.bin")], check=True)
+    back = np.fromfile(w / "back.bin", "<f8", count=6 * n).reshape(n, 6)
+    iback = np.fromfile(w / "back.bin", "<i4", offset=48 * n).reshape(n, 6)
+    text = (w / "ref.txt").read_bytes()
+    path = out_dir / "census_fmt.npz"
+    np.savez_compressed(path, d=d, i6=i6, text=np.frombuffer(text, np.uint8), read_d=back,
+                        read_i=iback)
+    return path
+
+
 def make_medium(out_path: Path, work: Path) -> None:
     """Per-cell tables of the inputm.dat medium (n_e=80, B=0.13 G, p=2.3)."""
     d = work / "medium"
@@ -178,6 +210,9 @@ def main() -> None:
             if args.only and name != args.only:
                 continue
             p = run_fp_case(name, spec, out, work)
+            print("wrote", p, p.stat().st_size, "bytes")
+        if not args.only or args.only == "census_fmt":
+            p = make_census_format(out, work)
             print("wrote", p, p.stat().st_size, "bytes")
         if not args.only:
             mp = ROOT / "compton2d_amd" / "data" / "medium_inputm.npz"
