@@ -461,3 +461,19 @@ class FpCall:
         for k in ("E_tot_old", "E_tot_new", "hr_total", "hr_st_total", "dT_max"):
             r[k] = getattr(self.sout, k)
         return r
+
+
+# ---------------------------------------------------------------------------
+# Observer-frame binning (c2d_obs_bins; postprocessing/pspt.c, plcm.c)
+# ---------------------------------------------------------------------------
+OBS_SED, OBS_LC = 0, 1
+OBS_MAX_T, OBS_MAX_MU, OBS_MAX_E = 1024, 32, 256
+
+
+class ObsBins(C.Structure):
+    _fields_ = [
+        ("mode", _i32), ("gam_bulk", _d), ("rmax", _d), ("t_offset", _d),
+        ("n_t", _i32), ("t0", PD), ("t1", PD),
+        ("n_mu", _i32), ("mu0", PD), ("mu1", PD),
+        ("n_e", _i32), ("E0", PD), ("E1", PD),
+    ]

@@ -177,6 +177,20 @@ struct FpParams {
   int32_t* err;
 };
 
+/* ---- observer-frame binning (observe.hip) ---- */
+struct ObsDev {
+  double gam_bulk, rmax, t_offset;
+  int32_t mode, n_t, n_mu, n_e;
+  const double* t0; const double* t1;
+  const double* mu0; const double* mu1;
+  const double* E0; const double* E1;
+  double* F;                 /* [n_t][n_mu][n_e] sum of ew       */
+  double* F2;                /* sum of ew^2                        */
+  double* cnt;               /* particle counts (exact integers)  */
+  int32_t lds_rows;          /* leading time rows privatised in LDS (0..n_t) */
+  int32_t sorted_t, sorted_mu, sorted_e;   /* lo[] and hi[] non-decreasing: binary search */
+};
+
 }  // namespace c2d
 
 #endif

@@ -35,6 +35,10 @@ extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
                                       double* tab, int ncell, hipStream_t s);
 extern "C" int c2d_launch_fp(const FpParams* P, int ncell, hipStream_t s);
+extern "C" int c2d_launch_obs(const ObsDev* O, const double* ev, int64_t n, int grid,
+                              hipStream_t s);
+extern "C" size_t c2d_obs_lds_bytes(int n_t, int n_mu, int n_e, int lds_rows);
+extern "C" int c2d_obs_block(void);
 extern "C" int c2d_launch_tridag(const double* a, const double* b, const double* c,
                                  const double* r, double* x, int ncell, int nt, hipStream_t s);
 
@@ -91,6 +95,7 @@ struct c2d_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev_g0a = nullptr, ev_g0t = nullptr, ev_g0b = nullptr, ev_end = nullptr;
   int n_cu = 0, max_grid = 0, lds_cells = 0;
+  size_t lds_max = 64 * 1024;   /* LDS bytes a workgroup may allocate */
   size_t lds_bytes = 0;
   c2d_tally_layout L;
   /* device buffers */
@@ -133,6 +138,13 @@ struct c2d_ctx {
          *fp_nf = nullptr, *fp_fout = nullptr, *fp_Pout = nullptr, *fp_zout = nullptr;
   int32_t* fp_err = nullptr;
   float last_fp_ms = 0.f;
+  /* observer-frame binning */
+  bool obs_ready = false;
+  ObsDev obs;
+  double *obs_edges = nullptr, *obs_hist = nullptr, *obs_ev = nullptr;
+  int64_t obs_ev_cap = 0;
+  int obs_wg_per_cu = 1;
+  double obs_ms = 0.0;
 };
 
 static int fail(c2d_ctx* c, int code, const char* fmt, ...) {
@@ -194,6 +206,7 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   hipDeviceProp_t prop;
   HIPCHK(c, hipGetDeviceProperties(&prop, cfg->device));
   c->n_cu = prop.multiProcessorCount;
+  c->lds_max = std::max<size_t>(prop.sharedMemPerBlock, 64 * 1024);
 
   /* grids (1-based like the reference COMMON) */
   Geo g;
@@ -292,6 +305,9 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
     if (c->cens[b].key) (void)hipFree(c->cens[b].key);
   }
   for (double* p : c->spec_bufs) (void)hipFree(p);
+  void* optrs[] = {c->obs_edges, c->obs_hist, c->obs_ev};
+  for (void* p : optrs)
+    if (p) (void)hipFree(p);
   void* fptrs[] = {c->fp_FT, c->fp_mcd, c->fp_zin, c->fp_fin, c->fp_Pin, c->fp_nf, c->fp_fout, c->fp_Pout,
                    c->fp_zout, c->fp_err};
   for (void* p : fptrs)
@@ -987,5 +1003,117 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
 extern "C" int c2d_last_fp_ms(c2d_ctx* c, double* ms) {
   if (!c || !ms) return C2D_E_ARG;
   *ms = c->last_fp_ms;
+  return C2D_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* observer-frame binning (postprocessing/pspt.c, plcm.c)               */
+/* ------------------------------------------------------------------ */
+extern "C" int c2d_obs_begin(c2d_ctx* c, const c2d_obs_bins* b) {
+  if (!c || !b) return C2D_E_ARG;
+  if ((b->mode != C2D_OBS_SED && b->mode != C2D_OBS_LC) || b->n_t < 1 || b->n_t > C2D_OBS_MAX_T ||
+      b->n_mu < 1 || b->n_mu > C2D_OBS_MAX_MU || b->n_e < 1 || b->n_e > C2D_OBS_MAX_E ||
+      !b->t0 || !b->t1 || !b->mu0 || !b->mu1 || !b->E0 || !b->E1 || !(b->gam_bulk >= 1.0))
+    return fail(c, C2D_E_ARG, "c2d_obs_begin: bad binning");
+  if (b->mode == C2D_OBS_SED && b->n_mu != 1)
+    return fail(c, C2D_E_ARG, "c2d_obs_begin: the SED mode has one angular window");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (c->obs_edges) (void)hipFree(c->obs_edges);
+  if (c->obs_hist) (void)hipFree(c->obs_hist);
+  c->obs_edges = c->obs_hist = nullptr;
+  const int ne = 2 * (b->n_t + b->n_mu + b->n_e);
+  std::vector<double> h;
+  h.reserve(ne);
+  h.insert(h.end(), b->t0, b->t0 + b->n_t);
+  h.insert(h.end(), b->t1, b->t1 + b->n_t);
+  h.insert(h.end(), b->mu0, b->mu0 + b->n_mu);
+  h.insert(h.end(), b->mu1, b->mu1 + b->n_mu);
+  h.insert(h.end(), b->E0, b->E0 + b->n_e);
+  h.insert(h.end(), b->E1, b->E1 + b->n_e);
+  HIPCHK(c, dalloc(&c->obs_edges, (size_t)ne));
+  HIPCHK(c, hipMemcpy(c->obs_edges, h.data(), ne * sizeof(double), hipMemcpyHostToDevice));
+  const size_t nh = (size_t)b->n_t * b->n_mu * b->n_e;
+  HIPCHK(c, dalloc(&c->obs_hist, 3 * nh));
+  HIPCHK(c, hipMemset(c->obs_hist, 0, 3 * nh * sizeof(double)));
+  ObsDev& O = c->obs;
+  O.gam_bulk = b->gam_bulk; O.rmax = b->rmax; O.t_offset = b->t_offset;
+  O.mode = b->mode; O.n_t = b->n_t; O.n_mu = b->n_mu; O.n_e = b->n_e;
+  O.t0 = c->obs_edges; O.t1 = O.t0 + b->n_t; O.mu0 = O.t1 + b->n_t; O.mu1 = O.mu0 + b->n_mu;
+  O.E0 = O.mu1 + b->n_mu; O.E1 = O.E0 + b->n_e;
+  O.F = c->obs_hist; O.F2 = O.F + nh; O.cnt = O.F2 + nh;
+  /* privatise in LDS when the three histograms fit next to the edges */
+  /* privatise as many leading time rows in LDS as fit (all of them for the
+   * usual SED); later rows go to wave-aggregated global atomics */
+  {
+    const size_t edges = c2d_obs_lds_bytes(b->n_t, b->n_mu, b->n_e, 0);
+    const size_t row = c2d_obs_lds_bytes(0, b->n_mu, b->n_e, 1) - c2d_obs_lds_bytes(0, b->n_mu, b->n_e, 0);
+    const size_t avail = c->lds_max > edges ? c->lds_max - edges : 0;
+    O.lds_rows = (int)std::min<size_t>((size_t)b->n_t, avail / row);
+    const size_t bytes = c2d_obs_lds_bytes(b->n_t, b->n_mu, b->n_e, O.lds_rows);
+    /* workgroups per CU that fit the CU's 160 KiB of LDS, at most 4 */
+    c->obs_wg_per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / std::max<size_t>(bytes, 1)));
+  }
+  auto sorted = [](const double* lo, const double* hi, int n) {
+    for (int i = 1; i < n; i++)
+      if (!(lo[i] >= lo[i - 1]) || !(hi[i] >= hi[i - 1])) return 0;
+    return 1;
+  };
+  O.sorted_t = sorted(b->t0, b->t1, b->n_t);
+  O.sorted_mu = sorted(b->mu0, b->mu1, b->n_mu);
+  O.sorted_e = sorted(b->E0, b->E1, b->n_e);
+  c->obs_ms = 0.0;
+  c->obs_ready = true;
+  return C2D_OK;
+}
+
+static int obs_launch(c2d_ctx* c, const double* ev, int64_t m) {
+  if (m == 0) return C2D_OK;
+  /* enough blocks to fill the chip, each privatising its own histogram */
+  const int64_t bs = c2d_obs_block();
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * c->obs_wg_per_cu, (m + bs - 1) / bs));
+  HIPCHK(c, hipEventRecord(c->ev_g0a, c->stream));
+  int rc = c2d_launch_obs(&c->obs, ev, m, grid, c->stream);
+  if (rc) return fail(c, C2D_E_HIP, "obs launch: %s", hipGetErrorString((hipError_t)rc));
+  HIPCHK(c, hipEventRecord(c->ev_g0b, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, c->ev_g0a, c->ev_g0b);
+  c->obs_ms += ms;
+  return C2D_OK;
+}
+
+extern "C" int c2d_obs_accumulate(c2d_ctx* c, const double* events, int64_t n) {
+  if (!c) return C2D_E_ARG;
+  if (!c->obs_ready) return fail(c, C2D_E_STATE, "c2d_obs_begin must precede c2d_obs_accumulate");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (!events) return obs_launch(c, c->ev, c->n_ev);
+  if (n < 0) return C2D_E_ARG;
+  if (n > c->obs_ev_cap) {
+    if (c->obs_ev) (void)hipFree(c->obs_ev);
+    c->obs_ev = nullptr;
+    HIPCHK(c, dalloc(&c->obs_ev, (size_t)n * C2D_EVENT_WORDS));
+    c->obs_ev_cap = n;
+  }
+  if (n) HIPCHK(c, hipMemcpy(c->obs_ev, events, (size_t)n * C2D_EVENT_WORDS * sizeof(double),
+                             hipMemcpyHostToDevice));
+  return obs_launch(c, c->obs_ev, n);
+}
+
+extern "C" int c2d_obs_accumulate_device(c2d_ctx* c, const double* d_events, int64_t n) {
+  if (!c || !d_events || n < 0) return C2D_E_ARG;
+  if (!c->obs_ready) return fail(c, C2D_E_STATE, "c2d_obs_begin must precede c2d_obs_accumulate_device");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  return obs_launch(c, d_events, n);
+}
+
+extern "C" int c2d_obs_result(c2d_ctx* c, double* F, double* F2, double* count, double* kernel_ms) {
+  if (!c) return C2D_E_ARG;
+  if (!c->obs_ready) return fail(c, C2D_E_STATE, "c2d_obs_begin must precede c2d_obs_result");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const size_t nh = (size_t)c->obs.n_t * c->obs.n_mu * c->obs.n_e;
+  if (F) HIPCHK(c, hipMemcpy(F, c->obs.F, nh * sizeof(double), hipMemcpyDeviceToHost));
+  if (F2) HIPCHK(c, hipMemcpy(F2, c->obs.F2, nh * sizeof(double), hipMemcpyDeviceToHost));
+  if (count) HIPCHK(c, hipMemcpy(count, c->obs.cnt, nh * sizeof(double), hipMemcpyDeviceToHost));
+  if (kernel_ms) *kernel_ms = c->obs_ms;
   return C2D_OK;
 }

@@ -96,6 +96,14 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_fp_step.argtypes = [vp, C.POINTER(abi.FpStepIn), C.POINTER(abi.FpStepOut)]
     lib.c2d_last_fp_ms.restype = C.c_int
     lib.c2d_last_fp_ms.argtypes = [vp, C.POINTER(C.c_double)]
+    lib.c2d_obs_begin.restype = C.c_int
+    lib.c2d_obs_begin.argtypes = [vp, C.POINTER(abi.ObsBins)]
+    lib.c2d_obs_accumulate.restype = C.c_int
+    lib.c2d_obs_accumulate.argtypes = [vp, C.POINTER(C.c_double), C.c_int64]
+    lib.c2d_obs_accumulate_device.restype = C.c_int
+    lib.c2d_obs_accumulate_device.argtypes = [vp, C.c_void_p, C.c_int64]
+    lib.c2d_obs_result.restype = C.c_int
+    lib.c2d_obs_result.argtypes = [vp] + [C.POINTER(C.c_double)] * 4
     if path is None:
         _lib = lib
     return lib
@@ -257,6 +265,39 @@ class Engine:
         self._check(self.lib.c2d_last_fp_ms(self.ctx, C.byref(ms)))
         return ms.value
 
+    # -- observer-frame binning (postprocessing/pspt.c, plcm.c) ---------------
+    def obs_begin(self, binning) -> None:
+        """Zero a device histogram for `binning` (observer.Binning)."""
+        self._obs = binning
+        self._obs_c = binning.to_ctypes()
+        self._check(self.lib.c2d_obs_begin(self.ctx, C.byref(self._obs_c)))
+
+    def obs_accumulate(self, events=None) -> None:
+        """Bin host events [n, 7] (t_bound, xnu, ew, rpre, zpre, wmu, phi), or
+        with None the last transport step's device event buffer."""
+        if events is None:
+            self._check(self.lib.c2d_obs_accumulate(self.ctx, None, 0))
+            return
+        ev = np.ascontiguousarray(events, np.float64).reshape(-1, abi.EVENT_WORDS)
+        self._check(self.lib.c2d_obs_accumulate(self.ctx, ev.ctypes.data_as(abi.PD), len(ev)))
+
+    def obs_accumulate_device(self, ptr: int, n: int) -> None:
+        """Bin n events at device address `ptr` (e.g. tensor.data_ptr() of a
+        cuda float64 [n, 7] tensor on this context's GPU)."""
+        self._check(self.lib.c2d_obs_accumulate_device(self.ctx, C.c_void_p(ptr), n))
+
+    def obs_result(self):
+        """Raw sums (F = sum ew, F2 = sum ew^2, count), each [n_t, n_mu, n_e],
+        and the device milliseconds of the binning launches so far."""
+        b = self._obs
+        shape = (b.n_t, b.n_mu, b.n_e)
+        F, F2, cnt = (np.zeros(shape) for _ in range(3))
+        ms = C.c_double()
+        self._check(self.lib.c2d_obs_result(self.ctx, F.ctypes.data_as(abi.PD),
+                                            F2.ctypes.data_as(abi.PD),
+                                            cnt.ctypes.data_as(abi.PD), C.byref(ms)))
+        return F, F2, cnt, ms.value
+
     def fp_tridag(self, a, b, c, r, x0=None) -> np.ndarray:
         """Batched tridag (src/update2d.f:2476-2518); arrays [ncell, nt]."""
         a, b, c, r = (np.ascontiguousarray(x, np.float64) for x in (a, b, c, r))
@@ -266,6 +307,15 @@ class Engine:
                        c.ctypes.data_as(abi.PD), r.ctypes.data_as(abi.PD), nt)
         self._check(self.lib.c2d_fp_tridag(self.ctx, C.byref(fin), x.ctypes.data_as(abi.PD)))
         return x
+
+
+def obs_engine(device: int = 0) -> Engine:
+    """A context for observer-frame binning only (no transport tables used)."""
+    from . import synth
+    g = synth.c2_workload(nz=1, nr=1, sources=1, device=device, census_capacity=1024,
+                          event_capacity=1024).grid
+    g.queue_capacity = 1024
+    return Engine(g)
 
 
 def device_math(fn: int, x: np.ndarray, device: int = 0) -> np.ndarray:

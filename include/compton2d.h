@@ -267,6 +267,28 @@ typedef struct c2d_fp_step_out {
   double  E_tot_old, E_tot_new, hr_total, hr_st_total, dT_max;  /* E_add_up */
 } c2d_fp_step_out;
 
+/* ------------------------------------------------------------------------
+ * Observer-frame binning of escape events on the device (replaces running
+ * postprocessing/pspt.c:245-322 and plcm.c:382-456 over p###_evb.dat).
+ * Bin edges are explicit arrays so each tool's own edge arithmetic is kept
+ * (pspt: t0[n] = t0[0] + n*dt; plcm: t1[k] = t0[k+1] = t0[k] + dt).
+ * ---------------------------------------------------------------------- */
+#define C2D_OBS_SED 0   /* pspt.c: one closed mu window [mu0,mu1], first energy bin  */
+#define C2D_OBS_LC  1   /* plcm.c: time - t_offset >= 0, half-open mu bins, every
+                           energy band containing E                                 */
+#define C2D_OBS_MAX_T   1024
+#define C2D_OBS_MAX_MU  32
+#define C2D_OBS_MAX_E   256
+
+typedef struct c2d_obs_bins {
+  int32_t mode;                   /* C2D_OBS_SED | C2D_OBS_LC                  */
+  double  gam_bulk, rmax;         /* bulk Lorentz factor, r_max [cm]           */
+  double  t_offset;               /* LC only                                   */
+  int32_t n_t;  const double* t0; const double* t1;    /* observer time bins [s] */
+  int32_t n_mu; const double* mu0; const double* mu1;  /* observer-frame cos   */
+  int32_t n_e;  const double* E0; const double* E1;    /* observer energy [keV] */
+} c2d_obs_bins;
+
 const char* c2d_version(void);
 int  c2d_init(const c2d_config* cfg, c2d_ctx** out);
 void c2d_finalize(c2d_ctx* ctx);
@@ -324,6 +346,20 @@ int  c2d_fp_step(c2d_ctx* ctx, const c2d_fp_step_in* in, c2d_fp_step_out* out);
  * milliseconds and launches, measured with HIP events on the library's
  * own stream. */
 int  c2d_last_kernel_ms(c2d_ctx* ctx, double* gen0_ms, double* all_ms, int32_t* launches);
+/* Start an observer-frame histogram (zeroed on the device): sums of ew, of
+ * ew^2 and counts per [n_t][n_mu][n_e] bin. */
+int  c2d_obs_begin(c2d_ctx* ctx, const c2d_obs_bins* bins);
+/* Bin escape events into it: events == NULL bins the last transport step's
+ * device event buffer (c2d_events layout); otherwise n host events of 7 f64
+ * (t_bound, xnu, ew, rpre, zpre, wmu, phi). */
+int  c2d_obs_accumulate(c2d_ctx* ctx, const double* events, int64_t n);
+/* Same for n events already in device memory on the context's GPU (e.g. a
+ * gathered event buffer or a torch tensor); no copy. */
+int  c2d_obs_accumulate_device(c2d_ctx* ctx, const double* d_events, int64_t n);
+/* Download the raw sums ([n_t][n_mu][n_e] each; any pointer may be NULL)
+ * and the device time of the binning launches so far (ms). */
+int  c2d_obs_result(c2d_ctx* ctx, double* F, double* F2, double* count, double* kernel_ms);
+
 /* Device time of the last c2d_fp_step's FP kernel (HIP events, ms). */
 int  c2d_last_fp_ms(c2d_ctx* ctx, double* ms);
 /* Packet-steps executed by that generation-0 launch (roofline numerator). */

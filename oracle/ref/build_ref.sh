@@ -53,3 +53,11 @@ for f in $OBJS; do objs="$objs $OUT/obj/$f.o"; done
 "$FC" -o "$OUT/c2d_censdrv" "$OUT/obj/c2d_censdrv.o" "$OUT/obj/census2d.o" \
   -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
 echo "build_ref: $OUT/c2d_refdrv $OUT/c2d_censdrv"
+
+# The post-processing tools (postprocessing/pspt.c, plcm.c: K&R C reading an
+# input deck on stdin) for the observer-frame binning fixtures.
+PP="${C2D_REFERENCE_PP:-$(dirname "$SRC")/postprocessing}"
+for t in pspt plcm; do
+  gcc -O2 -std=gnu89 -w "$PP/$t.c" -o "$OUT/$t" -lm 2>/dev/null
+done
+echo "build_ref: $OUT/pspt $OUT/plcm"

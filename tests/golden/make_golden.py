@@ -174,6 +174,62 @@ def make_census_format(out_dir: Path, work: Path) -> Path:
     return path
 
 
+OBS_DECKS = {
+    # the reference's own decks (postprocessing/mrk421_*.input)
+    "sed_mrk421": ("pspt", "mrk421_sed.input"),
+    "lc_mrk421": ("plcm", "mrk421_lc.input"),
+    # decks that put most of the fixture's events into bins: several time and
+    # energy bins, linear + log regions, three angular bins with defaulted
+    # lower edges, overlapping bands, a time offset
+    "sed_wide": ("pspt", "p001_evb.dat\n33\n1e16\nsed_w.dat\n12\n-4000\n2e4\n0.999\n1.0\n2\n"
+                         "1e-4\n1e2\n24\n0\n1e2\n1e6\n8\n1\ny\n"),
+    "lc_wide": ("plcm", "p001_evb.dat\n15\n1e17\nlc07_ev0.dat\n3\nlc07_ev0.dat\n0.97\n0.995\n"
+                        "lc07_ev1.dat\n\n0.9995\nlc07_ev2.dat\n\n1.0001\n2e4\n4e4\n1.5e6\n4\n"
+                        "1e-3\n1e1\n1\n0\n1\n1e3\n3\n0\n1e2\n1e6\n2\n1\n1e-4\n1e7\n1\n0\n"),
+}
+
+
+def make_observer(out_dir: Path, work: Path) -> Path:
+    """The reference's post-processing tools (postprocessing/pspt.c, plcm.c,
+    compiled by oracle/ref/build_ref.sh) run over the escape events the
+    reference itself wrote in the golden transport cases, split over two
+    event files (p001_evb.dat, p002_evb.dat) so the tools' file walk is
+    exercised.  Stores events, decks and every output file."""
+    import resource
+    import subprocess
+    from compton2d_amd import observer
+    ev = []
+    for case, steps in (("ssc_tau", (1, 2)), ("grid3x4", (1,)), ("ec_lower", (1, 2))):
+        g = np.load(out_dir / ("%s.npz" % case))
+        ev += [g["out%d_events" % s] for s in steps]
+    ev = np.concatenate(ev)
+    pp = Path("/root/reference/postprocessing")
+    arrays = dict(events=ev, n_file1=np.array(len(ev) // 2))
+    for name, (tool, deck) in OBS_DECKS.items():
+        text = (pp / deck).read_text() if deck.endswith(".input") else deck
+        d = work / "obs" / name
+        if d.exists():
+            shutil.rmtree(d)
+        d.mkdir(parents=True)
+        observer.write_events(d / "p001_evb.dat", ev[: len(ev) // 2])
+        observer.write_events(d / "p002_evb.dat", ev[len(ev) // 2:])
+        before = set(p.name for p in d.iterdir())
+
+        def big_stack():
+            resource.setrlimit(resource.RLIMIT_STACK, (resource.RLIM_INFINITY, resource.RLIM_INFINITY))
+        subprocess.run([str(ROOT / "oracle" / "_ref" / tool)], input=text.encode(), cwd=d,
+                       stdout=subprocess.DEVNULL, check=True, preexec_fn=big_stack)
+        outs = sorted(p.name for p in d.iterdir() if p.name not in before)
+        arrays["deck_" + name] = np.array(text)
+        arrays["tool_" + name] = np.array(tool)
+        arrays["files_" + name] = np.array(outs)
+        for f in outs:
+            arrays["out_%s__%s" % (name, f)] = np.array((d / f).read_text())
+    path = out_dir / "obs.npz"
+    np.savez_compressed(path, **arrays)
+    return path
+
+
 def make_medium(out_path: Path, work: Path) -> None:
     """Per-cell tables of the inputm.dat medium (n_e=80, B=0.13 G, p=2.3)."""
     d = work / "medium"
@@ -213,6 +269,9 @@ def main() -> None:
             print("wrote", p, p.stat().st_size, "bytes")
         if not args.only or args.only == "census_fmt":
             p = make_census_format(out, work)
+            print("wrote", p, p.stat().st_size, "bytes")
+        if not args.only or args.only == "obs":
+            p = make_observer(out, work)
             print("wrote", p, p.stat().st_size, "bytes")
         if not args.only:
             mp = ROOT / "compton2d_amd" / "data" / "medium_inputm.npz"

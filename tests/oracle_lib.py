@@ -31,7 +31,8 @@ def load(flavor: str = "ref") -> C.CDLL:
     if flavor in _libs:
         return _libs[flavor]
     path = ORACLE_DIR / "_build" / ("liboracle_%s.so" % flavor)
-    srcs = (ORACLE_DIR / "c2d_oracle.c", ORACLE_DIR / "c2d_fp_oracle.c")
+    srcs = (ORACLE_DIR / "c2d_oracle.c", ORACLE_DIR / "c2d_fp_oracle.c",
+            ORACLE_DIR / "c2d_obs_oracle.c")
     if not path.exists() or any(path.stat().st_mtime < s.stat().st_mtime for s in srcs):
         build()
     lib = C.CDLL(str(path))
@@ -159,3 +160,21 @@ def fp_step(grid: abi.GridConfig, const: abi.FpConstants, ncycle: int, time: flo
     if rc != 0:
         raise RuntimeError("c2o_fp_step failed: %d" % rc)
     return call.result()
+
+
+def obs_bin(binning, events: np.ndarray, flavor: str = "ref"):
+    """The tools' per-event loop (oracle/c2d_obs_oracle.c) in event order:
+    (F, F2, count) each [n_t, n_mu, n_e]."""
+    lib = load(flavor)
+    lib.c2o_obs_bin.restype = C.c_int
+    lib.c2o_obs_bin.argtypes = [C.POINTER(abi.ObsBins), C.POINTER(C.c_double), C.c_int64] + \
+        [C.POINTER(C.c_double)] * 3
+    b = binning.to_ctypes()
+    ev = np.ascontiguousarray(events, np.float64).reshape(-1, abi.EVENT_WORDS)
+    shape = (binning.n_t, binning.n_mu, binning.n_e)
+    F, F2, cnt = (np.zeros(shape) for _ in range(3))
+    rc = lib.c2o_obs_bin(C.byref(b), ev.ctypes.data_as(abi.PD), len(ev), F.ctypes.data_as(abi.PD),
+                         F2.ctypes.data_as(abi.PD), cnt.ctypes.data_as(abi.PD))
+    if rc != 0:
+        raise RuntimeError("c2o_obs_bin failed: %d" % rc)
+    return F, F2, cnt
