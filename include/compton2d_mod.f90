@@ -110,6 +110,20 @@ module compton2d
      real(c_double) :: E_tot_old = 0, E_tot_new = 0, hr_total = 0, hr_st_total = 0, dT_max = 0
   end type c2d_fp_step_out
 
+  ! ---- observer-frame binning (c2d_obs_*; postprocessing/pspt.c, plcm.c) ----
+  integer, parameter :: C2D_OBS_SED = 0, C2D_OBS_LC = 1
+
+  type, bind(C) :: c2d_obs_bins
+     integer(c_int32_t) :: mode = 0
+     real(c_double) :: gam_bulk = 33.d0, rmax = 1.d16, t_offset = 0.d0
+     integer(c_int32_t) :: n_t = 0
+     type(c_ptr) :: t0 = c_null_ptr, t1 = c_null_ptr
+     integer(c_int32_t) :: n_mu = 0
+     type(c_ptr) :: mu0 = c_null_ptr, mu1 = c_null_ptr
+     integer(c_int32_t) :: n_e = 0
+     type(c_ptr) :: E0 = c_null_ptr, E1 = c_null_ptr
+  end type c2d_obs_bins
+
   type, bind(C) :: c2d_tally_layout
      integer(c_int64_t) :: edep, prdep, ecens, npcen, n_field, E_IC, nelectron, fout, &
           edout, erlki, erlko, erlku, erlkl, Ed_in, counters, total
@@ -216,5 +230,23 @@ module compton2d
        type(c2d_fp_step_in), intent(in) :: fin
        type(c2d_fp_step_out), intent(inout) :: fout
      end function c2d_fp_step
+
+     integer(c_int) function c2d_obs_begin(ctx, bins) bind(C, name='c2d_obs_begin')
+       import :: c_int, c_ptr, c2d_obs_bins
+       type(c_ptr), value :: ctx
+       type(c2d_obs_bins), intent(in) :: bins
+     end function c2d_obs_begin
+
+     integer(c_int) function c2d_obs_accumulate(ctx, events, n) bind(C, name='c2d_obs_accumulate')
+       import :: c_int, c_ptr, c_int64_t
+       type(c_ptr), value :: ctx, events           ! c_null_ptr: device events of the last step
+       integer(c_int64_t), value :: n
+     end function c2d_obs_accumulate
+
+     integer(c_int) function c2d_obs_result(ctx, F, F2, cnt, kernel_ms) bind(C, name='c2d_obs_result')
+       import :: c_int, c_ptr, c_double
+       type(c_ptr), value :: ctx, F, F2, cnt       ! [n_e, n_mu, n_t] in Fortran order
+       real(c_double), intent(out) :: kernel_ms
+     end function c2d_obs_result
   end interface
 end module compton2d

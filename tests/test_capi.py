@@ -50,6 +50,8 @@ int main(void) {
   P(c2d_config, seed) P(c2d_config, rank) P(c2d_config, queue_capacity) P(c2d_config, mu)
   P(c2d_step_in, kappa_tot) P(c2d_step_in, nsv) P(c2d_step_in, tbbl) P(c2d_step_in, spectra)
   P(c2d_step_in, n_spectra) P(c2d_step_in, dt)
+  printf("c2d_obs_bins %zu\n", sizeof(c2d_obs_bins));
+  P(c2d_obs_bins, t_offset) P(c2d_obs_bins, t1) P(c2d_obs_bins, n_mu) P(c2d_obs_bins, E1)
   return 0;
 }
 '''
@@ -68,8 +70,10 @@ int main(void) {
     assert int(got["c2d_fp_config"]) == C.sizeof(abi.FpConfig)
     assert int(got["c2d_fp_step_in"]) == C.sizeof(abi.FpStepIn)
     assert int(got["c2d_fp_step_out"]) == C.sizeof(abi.FpStepOut)
+    assert int(got["c2d_obs_bins"]) == C.sizeof(abi.ObsBins)
     classes = {"c2d_config": abi.Config, "c2d_step_in": abi.StepIn, "c2d_fp_config": abi.FpConfig,
-               "c2d_fp_step_in": abi.FpStepIn, "c2d_fp_step_out": abi.FpStepOut}
+               "c2d_fp_step_in": abi.FpStepIn, "c2d_fp_step_out": abi.FpStepOut,
+               "c2d_obs_bins": abi.ObsBins}
     for key, val in got.items():
         if "." in key:
             t, f = key.split(".")
