@@ -77,6 +77,22 @@ enum : int32_t {
   ERR_CENSUS = 1, ERR_EVENT = 2, ERR_QUEUE = 4, ERR_SPEC = 8
 };
 
+/* Explicit global-address-space access for pointers that arrive through
+ * KParams (generic pointers): global_load/store/atomic instead of flat ones,
+ * which would also count against lgkmcnt and stall LDS waits. */
+#define C2D_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ T gld(const T* p) { return *(const C2D_GLOBAL T*)p; }
+template <class T>
+__device__ __forceinline__ void gst(T* p, T v) { *(C2D_GLOBAL T*)p = v; }
+__device__ __forceinline__ void gadd(double* p, double v) {
+  __hip_atomic_fetch_add((C2D_GLOBAL double*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void gor(int32_t* p, int32_t v) {
+  __hip_atomic_fetch_or((C2D_GLOBAL int32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct KParams {
   int32_t nz, nr, ncell, nphtotal, nph_lc, nmu;
   int32_t split1, split2, split3, spl3_trg, spec_switch;

@@ -55,8 +55,11 @@ C2D_RHD uint32_t c2d_mulhi32(uint32_t a, uint32_t b) {
 /* Philox4x32-10 (Salmon et al., SC'11). */
 C2D_RHD void c2d_philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#ifndef C2D_PHILOX_ROUNDS
+#define C2D_PHILOX_ROUNDS 10
+#endif
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < C2D_PHILOX_ROUNDS; ++r) {
     uint32_t hi0 = c2d_mulhi32(M0, c[0]), lo0 = M0 * c[0];
     uint32_t hi1 = c2d_mulhi32(M1, c[2]), lo1 = M1 * c[2];
     uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;

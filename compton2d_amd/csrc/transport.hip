@@ -65,6 +65,8 @@
 #endif
 
 namespace c2d {
+/* the transport kernel's dynamic LDS: Geo image | cell tallies | escape tallies */
+extern __shared__ double c2d_tr_lds[];
 namespace {
 
 constexpr double PI_REF = 3.1415926536;        /* general.pa:24 */
@@ -114,22 +116,26 @@ struct LaneCnt {
 
 /* Tally views.  Cell tallies edep|prdep|ecens|npcen (stride ncell) and
  * escape tallies fout|edout|erlki|erlko|erlku|erlkl have the same layout in
- * LDS and in the fused global buffer, so three base pointers suffice. */
+ * LDS and in the fused global buffer.  LDS addresses are formed from the
+ * c2d_tr_lds symbol (offsets, not stored pointers) so the compiler emits ds_*
+ * instructions instead of flat ones with a run-time address-space dispatch. */
 struct Tal {
   const Geo* g;      /* LDS image of the grids */
-  double* cells;     /* LDS (privatised) or global */
-  double* esc;       /* LDS */
+  int cells_off;     /* offset of the privatised cell tallies in c2d_tr_lds (P.lds_cells) */
+  int esc_off;       /* offset of the escape tallies in c2d_tr_lds */
 };
-#define T_EDEP(P, T) ((T).cells)
-#define T_PRDEP(P, T) ((T).cells + (P).ncell)
-#define T_ECENS(P, T) ((T).cells + 2 * (P).ncell)
-#define T_NPCEN(P, T) ((T).cells + 3 * (P).ncell)
-#define T_FOUT(P, T) ((T).esc)
-#define T_EDOUT(P, T) ((T).esc + (P).nmu * C2D_NPHOMAX)
-#define T_ERLKI(P, T) ((T).esc + (P).nmu * (C2D_NPHOMAX + C2D_NPHLCMAX))
+#define T_FOUT(P, T) (c2d_tr_lds + (T).esc_off)
+#define T_EDOUT(P, T) (T_FOUT(P, T) + (P).nmu * C2D_NPHOMAX)
+#define T_ERLKI(P, T) (T_FOUT(P, T) + (P).nmu * (C2D_NPHOMAX + C2D_NPHLCMAX))
 #define T_ERLKO(P, T) (T_ERLKI(P, T) + (P).nz)
 #define T_ERLKU(P, T) (T_ERLKI(P, T) + 2 * (P).nz)
 #define T_ERLKL(P, T) (T_ERLKI(P, T) + 2 * (P).nz + (P).nr)
+enum : int { TC_EDEP = 0, TC_PRDEP = 1, TC_ECENS = 2, TC_NPCEN = 3 };
+/* cell tallies edep|prdep|ecens|npcen: LDS when privatised, else the fused buffer */
+__device__ __forceinline__ void cell_add(const KParams& P, const Tal& T, int which, int cell, double v) {
+  if (P.lds_cells) atomicAdd(&c2d_tr_lds[T.cells_off + which * P.ncell + cell], v);
+  else gadd(P.T + P.off.edep + which * P.ncell + cell, v);
+}
 
 /* Next draw of the packet's stream.  Every key change sets ctr = 0, except a
  * packet loaded from a record mid-stream, which calls rng_sync first. */
@@ -161,7 +167,10 @@ __device__ __forceinline__ unsigned long long wave_reserve(unsigned long long* c
   unsigned long long lt = (lane == 0) ? 0ull : (mask & ((~0ull) >> (64 - lane)));
   uint32_t rank = (uint32_t)__popcll(lt);
   unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(mask));
+  if (lane == leader)
+    base = __hip_atomic_fetch_add((C2D_GLOBAL unsigned long long*)counter,
+                                  (unsigned long long)__popcll(mask), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
   uint32_t lo = __builtin_amdgcn_readlane((uint32_t)base, leader);
   uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(base >> 32), leader);
   return (((unsigned long long)hi << 32) | lo) + rank;
@@ -269,12 +278,12 @@ __device__ __forceinline__ double comtot_table(const KParams& P, int cell, const
                                                const int tg, const double t) {
   if (tg == 0) return comtot_exact(P, cell, xnu);
   const double* tb = P.comtab + (int64_t)cell * C2D_COMTAB_N + (tg - 1);
-  const double y0 = tb[0], y1 = tb[1], y2 = tb[2], y3 = tb[3];
+  const double y0 = gld(tb), y1 = gld(tb + 1), y2 = gld(tb + 2), y3 = gld(tb + 3);
   const double tm1 = t - 1.0, tm2 = t - 2.0, tp1 = t + 1.0;
   const double cosig = -(t * tm1 * tm2) * (1.0 / 6.0) * y0 + (tp1 * tm1 * tm2) * 0.5 * y1 -
                        (tp1 * t * tm2) * 0.5 * y2 + (tp1 * t * tm1) * (1.0 / 6.0) * y3;
   if (cosig < 1.0e-40) return 1.0e-40;
-  return P.n_e[cell] * cosig;
+  return gld(P.n_e + cell) * cosig;
 }
 #endif
 
@@ -449,9 +458,10 @@ __device__ __forceinline__ void push_event(const KParams& P, double tb, const Pk
   unsigned long long slot = wave_reserve(P.n_ev);
   if (slot < (unsigned long long)P.cap_ev) {
     double* e = P.ev + slot * C2D_EVENT_WORDS;
-    e[0] = tb; e[1] = p.xnu; e[2] = p.ew; e[3] = p.rpre; e[4] = p.zpre; e[5] = p.wmu; e[6] = p.phi;
+    gst(e, tb); gst(e + 1, p.xnu); gst(e + 2, p.ew); gst(e + 3, p.rpre); gst(e + 4, p.zpre);
+    gst(e + 5, p.wmu); gst(e + 6, p.phi);
   } else {
-    atomicOr(P.err, ERR_EVENT);
+    gor(P.err, ERR_EVENT);
   }
   LC_ADD(lc, C2D_CNT_EVENTS);
 }
@@ -478,7 +488,7 @@ __device__ __forceinline__ int imcleak(const KParams& P, const Tal& T, Pkt& p, L
   const double tb = P.time + P.dt - RAD_CP * p.dcen;   /* H4: fresh t_bound everywhere */
   if (p.jph <= 0) {
     if (P.tbbl[p.kph - 1] > 0.0) {
-      atomicAdd(&P.T[P.off.Ed_in + p.kph - 1], p.ew);
+      gadd(&P.T[P.off.Ed_in + p.kph - 1], p.ew);
       atomicAdd(&T_ERLKL(P, T)[p.kph - 1], p.ew);
     }
     if (P.ncycle > 0) {
@@ -507,25 +517,25 @@ __device__ __forceinline__ int imcleak(const KParams& P, const Tal& T, Pkt& p, L
 __device__ __forceinline__ void census_write(const KParams& P, const Tal& T, const Pkt& p, LaneCnt& lc) {
   const Geo* g = T.g;
   int cell = (p.jph - 1) * P.nr + (p.kph - 1);
-  atomicAdd(&T_NPCEN(P, T)[cell], 1.0);
-  atomicAdd(&T_ECENS(P, T)[cell], p.ew);
+  cell_add(P, T, TC_NPCEN, cell, 1.0);
+  cell_add(P, T, TC_ECENS, cell, p.ew);
   int i = grid_index(g->E_field, C2D_NPHFIELD, p.xnu);
   double Egg_min = (g->E_field[1] * g->E_field[1]) / g->E_field[2];
   if (p.xnu > Egg_min)
-    atomicAdd(&P.T[P.off.n_field + (int64_t)cell * C2D_NPHFIELD + (i - 1)], 6.25e8 * p.ew / p.xnu);
+    gadd(&P.T[P.off.n_field + (int64_t)cell * C2D_NPHFIELD + (i - 1)], 6.25e8 * p.ew / p.xnu);
   unsigned long long slot = wave_reserve(P.n_cout);
   if (slot < (unsigned long long)P.cap_cout) {
-    P.cout.rpre[slot] = p.rpre;
-    P.cout.zpre[slot] = p.zpre;
-    P.cout.wmu[slot] = p.wmu;
-    P.cout.phi[slot] = p.phi;
-    P.cout.ew[slot] = p.ew;
-    P.cout.xnu[slot] = p.xnu;
-    P.cout.jk[slot] = ((uint32_t)p.jph << 16) | (uint32_t)p.kph;
-    P.cout.bins[slot] = (uint32_t)p.jgpsp | ((uint32_t)p.jgplc << 8) | ((uint32_t)p.jgpmu << 16);
-    P.cout.key[slot] = c2d_derive_s(p.key, C2D_TAG_CENSUS, p.ctr, 0u, p.sub);
+    gst(P.cout.rpre + slot, p.rpre);
+    gst(P.cout.zpre + slot, p.zpre);
+    gst(P.cout.wmu + slot, p.wmu);
+    gst(P.cout.phi + slot, p.phi);
+    gst(P.cout.ew + slot, p.ew);
+    gst(P.cout.xnu + slot, p.xnu);
+    gst(P.cout.jk + slot, ((uint32_t)p.jph << 16) | (uint32_t)p.kph);
+    gst(P.cout.bins + slot, (uint32_t)p.jgpsp | ((uint32_t)p.jgplc << 8) | ((uint32_t)p.jgpmu << 16));
+    gst(P.cout.key + slot, c2d_derive_s(p.key, C2D_TAG_CENSUS, p.ctr, 0u, p.sub));
   } else {
-    atomicOr(P.err, ERR_CENSUS);
+    gor(P.err, ERR_CENSUS);
   }
   LC_ADD(lc, C2D_CNT_CENSUS);
 }
@@ -535,7 +545,7 @@ __device__ __forceinline__ void push_scat(const KParams& P, ScatRec* q, unsigned
   if (slot < (unsigned long long)P.cap_q) {
     q[slot] = r;
   } else {
-    atomicOr(P.err, ERR_QUEUE);
+    gor(P.err, ERR_QUEUE);
   }
 }
 
@@ -703,7 +713,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   }
   /* absorption (imctrk2d.f:382-462); gamma-gamma opacity inert (H6) */
   const double* kap = p.kap ? P.kappa_s : P.kappa_cv;
-  double sigabs = 1.0e-40 + 1.0 * kap[(int64_t)cell * C2D_N_VOL + (p.ie - 1)];
+  double sigabs = 1.0e-40 + 1.0 * gld(kap + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
   if (sigabs < 1.0e-40) sigabs = 1.0e-40;
   const double xabs = sigabs * trld;
   const double ewnew = (xabs < 100.0) ? p.ew * c2d_exp(-xabs) : 0.0;
@@ -726,8 +736,8 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   }
   const double delpr = deleabs * wmustar * C_LIGHT;
   if (p.mode != 0) {
-    atomicAdd(&T_EDEP(P, T)[cell], deleabs);
-    atomicAdd(&T_PRDEP(P, T)[cell], delpr);
+    cell_add(P, T, TC_EDEP, cell, deleabs);
+    cell_add(P, T, TC_PRDEP, cell, delpr);
   }
   if (ewnew <= p.wtmin) {
     LC_ADD(lc, C2D_CNT_KILLED);
@@ -805,7 +815,7 @@ __device__ __forceinline__ void planck(const KParams& P, const Geo* G, Pkt& p, d
 /* file_sample (src/imcsurf2d_para.f:694-788) */
 __device__ __forceinline__ void file_sample(const KParams& P, const Geo* G, Pkt& p, int spec) {
   if (spec < 0 || spec >= P.n_spectra) {
-    atomicOr(P.err, ERR_SPEC);
+    gor(P.err, ERR_SPEC);
     p.xnu = 1.0;
     p.jgpsp = 0; p.jgplc = 0; p.jgpmu = bin_mu(G, P.nmu, p.wmu);
     return;
@@ -1019,14 +1029,14 @@ __device__ __forceinline__ void store_pk(const PktSoA& s, int64_t i, const Pkt& 
 }
 
 __device__ __forceinline__ void load_pk(Pkt& p, const PktSoA& s, int64_t i) {
-  p.rpre = s.rpre[i]; p.zpre = s.zpre[i]; p.wmu = s.wmu[i]; p.phi = s.phi[i];
-  p.ew = s.ew[i]; p.xnu = s.xnu[i]; p.dcen = s.dcen[i];
-  const uint32_t jk = s.jk[i], bn = s.bins[i];
+  p.rpre = gld(s.rpre + i); p.zpre = gld(s.zpre + i); p.wmu = gld(s.wmu + i); p.phi = gld(s.phi + i);
+  p.ew = gld(s.ew + i); p.xnu = gld(s.xnu + i); p.dcen = gld(s.dcen + i);
+  const uint32_t jk = gld(s.jk + i), bn = gld(s.bins + i);
   p.jph = (int32_t)(jk >> 16); p.kph = (int32_t)(jk & 0xffffu);
   p.jgpsp = (int32_t)(bn & 0xffu); p.jgplc = (int32_t)((bn >> 8) & 0xffu);
   p.jgpmu = (int32_t)((bn >> 16) & 0xffu); p.kap = (int32_t)(bn >> 24);
-  p.ctr = s.ctr[i];
-  p.key = s.key[i];
+  p.ctr = gld(s.ctr + i);
+  p.key = gld(s.key + i);
   p.sub = 0;
 }
 
@@ -1145,7 +1155,7 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
       if (p.phi > twopi) p.phi = p.phi - twopi;
       const unsigned long long slot = wave_reserve(A.n_pk);
       if (slot < (unsigned long long)P.cap_pk) store_pk(P.pk, (int64_t)slot, p);
-      else atomicOr(P.err, ERR_QUEUE);
+      else gor(P.err, ERR_QUEUE);
     }
   }
   __syncthreads();
@@ -1161,14 +1171,14 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
 __device__ __forceinline__ void load_source(const KParams& P, Pkt& p, long long item) {
   if (item < P.n_cens_items) {
     const int64_t i = item;
-    p.rpre = P.cin.rpre[i]; p.zpre = P.cin.zpre[i];
-    p.wmu = clampd(P.cin.wmu[i], 0.99999999);
-    p.phi = P.cin.phi[i]; p.ew = P.cin.ew[i]; p.xnu = P.cin.xnu[i];
-    const uint32_t jk = P.cin.jk[i], bn = P.cin.bins[i];
+    p.rpre = gld(P.cin.rpre + i); p.zpre = gld(P.cin.zpre + i);
+    p.wmu = clampd(gld(P.cin.wmu + i), 0.99999999);
+    p.phi = gld(P.cin.phi + i); p.ew = gld(P.cin.ew + i); p.xnu = gld(P.cin.xnu + i);
+    const uint32_t jk = gld(P.cin.jk + i), bn = gld(P.cin.bins + i);
     p.jph = (int32_t)(jk >> 16); p.kph = (int32_t)(jk & 0xffffu);
     p.jgpsp = (int32_t)(bn & 0xffu); p.jgplc = (int32_t)((bn >> 8) & 0xffu);
     p.jgpmu = (int32_t)((bn >> 16) & 0xffu);
-    p.key = P.cin.key[i];
+    p.key = gld(P.cin.key + i);
     p.sub = 0;
     p.dcen = P.cdt;                                    /* imcfield2d.f:117 */
     p.kap = 0;
@@ -1183,29 +1193,22 @@ __device__ __forceinline__ void load_source(const KParams& P, Pkt& p, long long 
 __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kernel)(const KParams* __restrict__ Pg,
                                                                       const GenArgs A) {
   const KParams& P = *Pg;
-  extern __shared__ double lds[];
+  double* const lds = c2d_tr_lds;
   const int tid = threadIdx.x;
   const uint32_t lane = lane_id();
   /* LDS carve-up: Geo image | cell tallies (optional) | escape tallies */
-  double* cur = lds + GEO_DOUBLES;
   Tal T;
   T.g = reinterpret_cast<const Geo*>(lds);
-  double* cells_lds = cur;
-  if (P.lds_cells) {
-    T.cells = cur;
-    cur += 4 * P.ncell;
-  } else {
-    T.cells = P.T + P.off.edep;
-  }
-  double* esc_lds = cur;
-  T.esc = cur;
-  cur += P.nmu * (C2D_NPHOMAX + C2D_NPHLCMAX) + 2 * P.nz + 2 * P.nr;
-  const int n_cells_lds = (int)(esc_lds - cells_lds);
-  const int n_esc = (int)(cur - esc_lds);
+  T.cells_off = GEO_DOUBLES;
+  const int n_cells_lds = P.lds_cells ? 4 * P.ncell : 0;
+  T.esc_off = GEO_DOUBLES + n_cells_lds;
+  const int n_esc = P.nmu * (C2D_NPHOMAX + C2D_NPHLCMAX) + 2 * P.nz + 2 * P.nr;
+  double* const cells_lds = lds + T.cells_off;
+  double* const esc_lds = lds + T.esc_off;
   {
     const double* gsrc = reinterpret_cast<const double*>(P.geo);
-    for (int i = tid; i < GEO_DOUBLES; i += BLOCK) lds[i] = gsrc[i];
-    for (int i = tid; i < (int)(cur - cells_lds); i += BLOCK) cells_lds[i] = 0.0;
+    for (int i = tid; i < GEO_DOUBLES; i += BLOCK) lds[i] = gld(gsrc + i);
+    for (int i = tid; i < n_cells_lds + n_esc; i += BLOCK) cells_lds[i] = 0.0;
   }
   __shared__ uint32_t cnt_lds[C2D_NCOUNTERS];
   init_counters(cnt_lds);
