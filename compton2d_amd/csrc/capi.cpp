@@ -33,7 +33,7 @@ extern "C" int c2d_transport_occupancy_exact(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t s);
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
-                                      double* tab, int ncell, hipStream_t s);
+                                      double* tab, double* coef, int ncell, hipStream_t s);
 extern "C" int c2d_launch_fp(const FpParams* P, int ncell, hipStream_t s);
 extern "C" int c2d_launch_obs(const ObsDev* O, const double* ev, int64_t n, int grid,
                               hipStream_t s);
@@ -44,8 +44,9 @@ extern "C" int c2d_launch_tridag(const double* a, const double* b, const double*
 
 namespace {
 
-enum { CTL_WORK = 0, CTL_NCOUT = 1, CTL_NEV = 2, CTL_N2 = 3, CTL_N3 = 4, CTL_NPK = 5, CTL_CNT = 8,
-       CTL_WORDS = 8 + C2D_NCOUNTERS };
+/* CTL_EVSH: the C2D_EV_SHARDS event counters, one per 128-B line */
+enum { CTL_WORK = 0, CTL_NCOUT = 1, CTL_N2 = 3, CTL_N3 = 4, CTL_NPK = 5, CTL_CNT = 8,
+       CTL_EVSH = 32, CTL_WORDS = CTL_EVSH + C2D_EV_SHARDS * C2D_EV_SHARD_STRIDE };
 
 /* the packet store (c2d_device.hpp PktSoA) */
 struct DevPk {
@@ -108,12 +109,14 @@ struct c2d_ctx {
   SpecDev* spectra = nullptr;
   std::vector<double*> spec_bufs;
   int n_spectra = 0;
-  double *comtab = nullptr, *comS = nullptr;
+  double *comtab = nullptr, *comS = nullptr, *comcoef = nullptr;
   DevCensus cens[2];
   int cur_out = 0;           /* census buffer written by the last step */
   int64_t n_census = 0;      /* packets in cens[cur_out] */
   double* ev = nullptr;
   int64_t n_ev = 0;
+  int64_t ev_cnt[C2D_EV_SHARDS] = {};   /* events in each shard of the buffer (last step) */
+  int64_t ev_cap_sh = 0;                /* per-shard capacity                             */
   ScatRec *q2[2] = {nullptr, nullptr}, *q3[2] = {nullptr, nullptr};
   DevPk pk;
   double* T = nullptr;
@@ -247,6 +250,7 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   HIPCHK(c, dalloc(&c->tbbl, (size_t)c->nr));
   if (cfg->comtot_mode == C2D_COMTOT_TABLE) {
     HIPCHK(c, dalloc(&c->comtab, nc * C2D_COMTAB_N));
+    HIPCHK(c, dalloc(&c->comcoef, nc * (size_t)(C2D_COMTAB_N - 3) * 4));
     HIPCHK(c, dalloc(&c->comS, (size_t)C2D_COMTAB_N * C2D_NUM_NT));
     int rc = c2d_launch_comtab_sigma(c->gnt, c->comS, c->stream);
     if (rc) return fail(c, C2D_E_HIP, "comtab_sigma launch: %d", rc);
@@ -293,7 +297,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->geo, c->gnt, c->kappa_cur, c->kappa_prev, c->eps_tot, c->eps_th, c->f_nt,
                   c->Pnt, c->n_e, c->vfrac, c->ewsv, c->surf_ew, c->surf_tbb, c->tbbl,
-                  c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comS,
+                  c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comcoef, c->comS,
                   c->ev, c->q2[0], c->q2[1], c->q3[0], c->q3[1], c->T_own, c->ctl, c->derr, c->dP};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -483,7 +487,7 @@ extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
   }
 
   if (c->cfg.comtot_mode == C2D_COMTOT_TABLE) {
-    int rc = c2d_launch_comtab_gemm(c->f_nt, c->gnt, c->comS, c->comtab, nc, c->stream);
+    int rc = c2d_launch_comtab_gemm(c->f_nt, c->gnt, c->comS, c->comtab, c->comcoef, nc, c->stream);
     if (rc) return fail(c, C2D_E_HIP, "comtab_gemm launch: %d", rc);
   }
   c2d_set_clock(c, in->ncycle, in->time, in->dt);
@@ -513,6 +517,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.surf_tbb = c->surf_tbb; P.surf_spec = c->surf_spec; P.tbbl = c->tbbl;
   P.spectra = c->spectra; P.n_spectra = c->n_spectra; P.nslot = c->nslot;
   P.comtab = c->comtab;
+  P.comcoef = c->comcoef;
   P.comtab_du_inv = (double)(C2D_COMTAB_N - 1) / (C2D_COMTAB_U1 - C2D_COMTAB_U0);
   const int in_buf = c->cur_out, out_buf = 1 - c->cur_out;
   P.cin = c->cens[in_buf].soa();
@@ -520,7 +525,10 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.n_cin = c->n_census;
   P.cap_cout = cfg.census_capacity;
   P.n_cout = c->ctl + CTL_NCOUT;
-  P.ev = c->ev; P.cap_ev = cfg.event_capacity; P.n_ev = c->ctl + CTL_NEV;
+  P.ev = c->ev; P.cap_ev = cfg.event_capacity;
+  P.n_ev_sh = c->ctl + CTL_EVSH;
+  c->ev_cap_sh = std::max<int64_t>(cfg.event_capacity / C2D_EV_SHARDS, 0);
+  P.cap_ev_sh = c->ev_cap_sh;
   P.cap_q = cfg.queue_capacity;
   P.T = c->T;
   P.off.edep = c->L.edep; P.off.prdep = c->L.prdep; P.off.ecens = c->L.ecens;
@@ -666,15 +674,23 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   HIPCHK(c, hipMemcpyAsync(c->T + c->L.counters, hc, sizeof hc, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const int64_t ncout = (int64_t)ctl[CTL_NCOUT];
-  c->n_ev = std::min<int64_t>((int64_t)ctl[CTL_NEV], cfg.event_capacity);
+  c->n_ev = 0;
+  unsigned long long ev_reserved = 0;
+  for (int sh = 0; sh < C2D_EV_SHARDS; sh++) {
+    const unsigned long long m = ctl[CTL_EVSH + sh * C2D_EV_SHARD_STRIDE];
+    ev_reserved += m;
+    c->ev_cnt[sh] = std::min<int64_t>((int64_t)m, c->ev_cap_sh);
+    c->n_ev += c->ev_cnt[sh];
+  }
   c->cur_out = out_buf;
   c->n_census = std::min<int64_t>(ncout, cfg.census_capacity);
   if (herr & ERR_CENSUS)
     return fail(c, C2D_E_CENSUS_OVERFLOW, "too many photons: census %lld > capacity %lld",
                 (long long)ncout, (long long)cfg.census_capacity);
   if (herr & ERR_EVENT)
-    return fail(c, C2D_E_EVENT_OVERFLOW, "event buffer overflow: %llu > %lld",
-                ctl[CTL_NEV], (long long)cfg.event_capacity);
+    return fail(c, C2D_E_EVENT_OVERFLOW,
+                "event buffer overflow: %llu events, capacity %lld (%d shards of %lld)", ev_reserved,
+                (long long)cfg.event_capacity, C2D_EV_SHARDS, (long long)c->ev_cap_sh);
   if (herr & ERR_QUEUE) return fail(c, C2D_E_QUEUE_OVERFLOW, "scatter queue overflow");
   if (herr & ERR_SPEC) return fail(c, C2D_E_ARG, "surface packet without a seed spectrum");
   return C2D_OK;
@@ -710,10 +726,16 @@ extern "C" int c2d_tally_download(c2d_ctx* c, double* host, int64_t n) {
 extern "C" int c2d_events(c2d_ctx* c, double* buf, int64_t cap, int64_t* n) {
   if (!c || !n) return C2D_E_ARG;
   *n = c->n_ev;
-  const int64_t m = std::min(cap, c->n_ev);
-  if (m > 0 && buf) {
-    HIPCHK(c, hipSetDevice(c->cfg.device));
-    HIPCHK(c, hipMemcpy(buf, c->ev, sizeof(double) * C2D_EVENT_WORDS * m, hipMemcpyDeviceToHost));
+  if (!buf) return C2D_OK;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  int64_t done = 0;   /* the shards' filled prefixes, in shard order */
+  for (int sh = 0; sh < C2D_EV_SHARDS && done < cap; sh++) {
+    const int64_t m = std::min(cap - done, c->ev_cnt[sh]);
+    if (m > 0)
+      HIPCHK(c, hipMemcpy(buf + done * C2D_EVENT_WORDS,
+                          c->ev + (size_t)sh * c->ev_cap_sh * C2D_EVENT_WORDS,
+                          sizeof(double) * C2D_EVENT_WORDS * m, hipMemcpyDeviceToHost));
+    done += m;
   }
   return C2D_OK;
 }
@@ -1086,7 +1108,13 @@ extern "C" int c2d_obs_accumulate(c2d_ctx* c, const double* events, int64_t n) {
   if (!c) return C2D_E_ARG;
   if (!c->obs_ready) return fail(c, C2D_E_STATE, "c2d_obs_begin must precede c2d_obs_accumulate");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  if (!events) return obs_launch(c, c->ev, c->n_ev);
+  if (!events) {
+    for (int sh = 0; sh < C2D_EV_SHARDS; sh++) {
+      const int rc = obs_launch(c, c->ev + (size_t)sh * c->ev_cap_sh * C2D_EVENT_WORDS, c->ev_cnt[sh]);
+      if (rc) return rc;
+    }
+    return C2D_OK;
+  }
   if (n < 0) return C2D_E_ARG;
   if (n > c->obs_ev_cap) {
     if (c->obs_ev) (void)hipFree(c->obs_ev);
