@@ -156,12 +156,17 @@ def main():
     t0 = time.perf_counter()
     steps_global = 0.0
     g0_ms, g0_steps, aborted = 0.0, 0, 0.0
+    per_step = {k: 0.0 for k in ("sources", "escapes", "census", "collisions", "events", "generations")}
+    cidx = {"sources": abi.CNT_SOURCES, "escapes": abi.CNT_ESCAPES, "census": abi.CNT_CENSUS,
+            "collisions": abi.CNT_COLLIDE, "events": abi.CNT_EVENTS, "generations": abi.CNT_GENS}
     for _ in range(args.steps):
         one_step(n)
         n += 1
         c = T[cnt0:cnt0 + abi.NCOUNTERS].cpu().numpy()
         steps_global += float(c[abi.CNT_STEPS])
         aborted += float(c[abi.CNT_ABORTED])
+        for k, i in cidx.items():
+            per_step[k] += float(c[i]) / args.steps
         ms, _, _ = eng.last_kernel_ms()
         g0_ms += ms
         g0_steps += eng.last_gen0_steps()
@@ -199,6 +204,7 @@ def main():
             "parallelism": "lineage-sharded sources, %d rank(s), RCCL all-reduce of tallies" % world,
             "packet_steps_timed": steps_global,
             "aborted_packets": aborted,
+            "per_step_counts": per_step,
         },
         "roofline": {
             "bound": "hbm",

@@ -127,7 +127,6 @@ struct KParams {
   const SpecDev* spectra;
   int32_t n_spectra, nslot;
   const double* comtab;         /* [ncell][C2D_COMTAB_N] cosig on the u grid */
-  const double* comcoef;        /* [C2D_COMTAB_N-3][ncell][4] cubic coefficients */
   double comtab_du_inv;
   /* census */
   CensusSoA cin, cout;

@@ -33,7 +33,7 @@ extern "C" int c2d_transport_occupancy_exact(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t s);
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
-                                      double* tab, double* coef, int ncell, hipStream_t s);
+                                      double* tab, int ncell, hipStream_t s);
 extern "C" int c2d_launch_fp(const FpParams* P, int ncell, hipStream_t s);
 extern "C" int c2d_launch_obs(const ObsDev* O, const double* ev, int64_t n, int grid,
                               hipStream_t s);
@@ -109,7 +109,7 @@ struct c2d_ctx {
   SpecDev* spectra = nullptr;
   std::vector<double*> spec_bufs;
   int n_spectra = 0;
-  double *comtab = nullptr, *comS = nullptr, *comcoef = nullptr;
+  double *comtab = nullptr, *comS = nullptr;
   DevCensus cens[2];
   int cur_out = 0;           /* census buffer written by the last step */
   int64_t n_census = 0;      /* packets in cens[cur_out] */
@@ -250,7 +250,6 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   HIPCHK(c, dalloc(&c->tbbl, (size_t)c->nr));
   if (cfg->comtot_mode == C2D_COMTOT_TABLE) {
     HIPCHK(c, dalloc(&c->comtab, nc * C2D_COMTAB_N));
-    HIPCHK(c, dalloc(&c->comcoef, nc * (size_t)(C2D_COMTAB_N - 3) * 4));
     HIPCHK(c, dalloc(&c->comS, (size_t)C2D_COMTAB_N * C2D_NUM_NT));
     int rc = c2d_launch_comtab_sigma(c->gnt, c->comS, c->stream);
     if (rc) return fail(c, C2D_E_HIP, "comtab_sigma launch: %d", rc);
@@ -297,7 +296,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->geo, c->gnt, c->kappa_cur, c->kappa_prev, c->eps_tot, c->eps_th, c->f_nt,
                   c->Pnt, c->n_e, c->vfrac, c->ewsv, c->surf_ew, c->surf_tbb, c->tbbl,
-                  c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comcoef, c->comS,
+                  c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comS,
                   c->ev, c->q2[0], c->q2[1], c->q3[0], c->q3[1], c->T_own, c->ctl, c->derr, c->dP};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -487,7 +486,7 @@ extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
   }
 
   if (c->cfg.comtot_mode == C2D_COMTOT_TABLE) {
-    int rc = c2d_launch_comtab_gemm(c->f_nt, c->gnt, c->comS, c->comtab, c->comcoef, nc, c->stream);
+    int rc = c2d_launch_comtab_gemm(c->f_nt, c->gnt, c->comS, c->comtab, nc, c->stream);
     if (rc) return fail(c, C2D_E_HIP, "comtab_gemm launch: %d", rc);
   }
   c2d_set_clock(c, in->ncycle, in->time, in->dt);
@@ -517,7 +516,6 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.surf_tbb = c->surf_tbb; P.surf_spec = c->surf_spec; P.tbbl = c->tbbl;
   P.spectra = c->spectra; P.n_spectra = c->n_spectra; P.nslot = c->nslot;
   P.comtab = c->comtab;
-  P.comcoef = c->comcoef;
   P.comtab_du_inv = (double)(C2D_COMTAB_N - 1) / (C2D_COMTAB_U1 - C2D_COMTAB_U0);
   const int in_buf = c->cur_out, out_buf = 1 - c->cur_out;
   P.cin = c->cens[in_buf].soa();

@@ -277,12 +277,11 @@ __device__ __noinline__ double comtot_exact(const KParams& P, int cell, double x
 __device__ __forceinline__ double comtot_table(const KParams& P, int cell, const double xnu,
                                                const int tg, const double t) {
   if (tg == 0) return comtot_exact(P, cell, xnu);
-  /* segment-major coefficients: the 4 values of a lookup share one 32-B
-   * record, and a packet stepping to a neighbouring cell at the same energy
-   * reads the neighbouring record (same or next cache line) */
-  const double* cf = P.comcoef + ((int64_t)(tg - 1) * P.ncell + cell) * 4;
-  const double c0 = gld(cf), c1 = gld(cf + 1), c2 = gld(cf + 2), c3 = gld(cf + 3);
-  const double cosig = ((c3 * t + c2) * t + c1) * t + c0;
+  const double* tb = P.comtab + (int64_t)cell * C2D_COMTAB_N + (tg - 1);
+  const double y0 = gld(tb), y1 = gld(tb + 1), y2 = gld(tb + 2), y3 = gld(tb + 3);
+  const double tm1 = t - 1.0, tm2 = t - 2.0, tp1 = t + 1.0;
+  const double cosig = -(t * tm1 * tm2) * (1.0 / 6.0) * y0 + (tp1 * tm1 * tm2) * 0.5 * y1 -
+                       (tp1 * t * tm2) * 0.5 * y2 + (tp1 * t * tm1) * (1.0 / 6.0) * y3;
   if (cosig < 1.0e-40) return 1.0e-40;
   return gld(P.n_e + cell) * cosig;
 }
@@ -1406,23 +1405,6 @@ __global__ void __launch_bounds__(256) c2d_comtab_gemm(const double* f_nt, const
       if (c < ncell && gg < C2D_COMTAB_N) tab[(int64_t)c * C2D_COMTAB_N + gg] = acc[m][n];
     }
 }
-
-/* cubic Lagrange interpolant through tab[g..g+3] at nodes -1, 0, 1, 2 as
- * polynomial coefficients in t (segment g+1 of the table), stored
- * [g][cell][4] for the transport kernel's lookups */
-__global__ void __launch_bounds__(256) c2d_comtab_coef(const double* tab, double* coef, int ncell) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t nseg = C2D_COMTAB_N - 3;
-  if (i >= nseg * ncell) return;
-  const int64_t g = i / ncell, cell = i % ncell;
-  const double* y = tab + cell * C2D_COMTAB_N + g;
-  const double y0 = y[0], y1 = y[1], y2 = y[2], y3 = y[3];
-  double* o = coef + i * 4;
-  o[0] = y1;
-  o[1] = -y0 / 3.0 - 0.5 * y1 + y2 - y3 / 6.0;
-  o[2] = 0.5 * y0 - y1 + 0.5 * y2;
-  o[3] = (y3 - y0) / 6.0 + 0.5 * (y1 - y2);
-}
 #endif
 
 }  // namespace c2d
@@ -1461,12 +1443,9 @@ extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t
   return (int)hipGetLastError();
 }
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
-                                      double* tab, double* coef, int ncell, hipStream_t stream) {
+                                      double* tab, int ncell, hipStream_t stream) {
   dim3 grid(C2D_COMTAB_N / 64, (ncell + 63) / 64);
   hipLaunchKernelGGL(c2d::c2d_comtab_gemm, grid, dim3(256), 0, stream, f_nt, gnt, S, tab, ncell);
-  const int64_t n = (int64_t)(C2D_COMTAB_N - 3) * ncell;
-  hipLaunchKernelGGL(c2d::c2d_comtab_coef, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                     tab, coef, ncell);
   return (int)hipGetLastError();
 }
 #endif
