@@ -33,7 +33,7 @@ extern "C" int c2d_transport_occupancy_exact(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t s);
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
-                                      double* tab, int ncell, hipStream_t s);
+                                      float* tab, int ncell, hipStream_t s);
 extern "C" int c2d_launch_fp(const FpParams* P, int ncell, hipStream_t s);
 extern "C" int c2d_launch_obs(const ObsDev* O, const double* ev, int64_t n, int grid,
                               hipStream_t s);
@@ -109,7 +109,8 @@ struct c2d_ctx {
   SpecDev* spectra = nullptr;
   std::vector<double*> spec_bufs;
   int n_spectra = 0;
-  double *comtab = nullptr, *comS = nullptr;
+  float* comtab = nullptr;
+  double* comS = nullptr;
   DevCensus cens[2];
   int cur_out = 0;           /* census buffer written by the last step */
   int64_t n_census = 0;      /* packets in cens[cur_out] */
