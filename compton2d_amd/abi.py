@@ -477,3 +477,53 @@ class ObsBins(C.Structure):
         ("n_mu", _i32), ("mu0", PD), ("mu1", PD),
         ("n_e", _i32), ("E0", PD), ("E1", PD),
     ]
+
+
+# ---------------------------------------------------------------------------
+# Per-step emission / absorption tables (c2d_vem_in / c2d_vem_out)
+# ---------------------------------------------------------------------------
+class VemIn(C.Structure):
+    _fields_ = [("dt", _d), ("tea", Array2), ("tna", Array2), ("n_e", Array2), ("B_field", Array2),
+                ("f_pair", Array2), ("zsurf", Array2), ("vol", Array2), ("ep_switch", IArray2),
+                ("f_nt", Array3)]
+
+
+class VemOut(C.Structure):
+    _fields_ = [("kappa_tot", MArray3), ("eps_tot", MArray3), ("eps_th", MArray3),
+                ("B_field", MArray2), ("Eloss_sy", MArray2), ("Eloss_cy", MArray2),
+                ("Eloss_th", MArray2), ("Eloss_tot", MArray2), ("E_ph", PD)]
+
+
+VEM_STATE_KEYS = ("tea", "tna", "n_e", "B_field", "f_pair", "zsurf", "vol")
+
+
+class VemCall:
+    """Builds c2d_vem_in/out over dense numpy arrays: per-cell state [nz, nr],
+    f_nt [nz, nr, NUM_NT], ep_switch [nz, nr] (int, optional); outputs
+    kappa_tot/eps_tot/eps_th [nz, nr, N_VOL] and the per-cell scalars."""
+
+    def __init__(self, dt: float, state: dict):
+        f = np.ascontiguousarray(state["f_nt"], np.float64)
+        nz, nr = f.shape[:2]
+        self.keep = []
+
+        def a2(key, dflt=0.0):
+            v = state.get(key)
+            arr = np.ascontiguousarray(np.full((nz, nr), dflt) if v is None else v, np.float64)
+            self.keep.append(arr)
+            return Array2(arr.ctypes.data_as(PD), nr, 1)
+
+        ep = state.get("ep_switch")
+        ep = np.ascontiguousarray(np.zeros((nz, nr)) if ep is None else ep, np.int32)
+        self.keep += [f, ep]
+        self.sin = VemIn(float(dt), *(a2(k) for k in VEM_STATE_KEYS),
+                         IArray2(ep.ctypes.data_as(PI32), nr, 1),
+                         Array3(f.ctypes.data_as(PD), 1, nr * NUM_NT, NUM_NT))
+        self.res = {k: np.zeros((nz, nr, N_VOL)) for k in ("kappa_tot", "eps_tot", "eps_th")}
+        for k in ("B_field", "Eloss_sy", "Eloss_cy", "Eloss_th", "Eloss_tot"):
+            self.res[k] = np.zeros((nz, nr))
+        self.res["E_ph"] = np.zeros(N_VOL)
+        r = self.res
+        m3 = [MArray3(r[k].ctypes.data_as(PD), 1, nr * N_VOL, N_VOL) for k in ("kappa_tot", "eps_tot", "eps_th")]
+        m2 = [MArray2(r[k].ctypes.data_as(PD), nr, 1) for k in ("B_field", "Eloss_sy", "Eloss_cy", "Eloss_th", "Eloss_tot")]
+        self.sout = VemOut(*m3, *m2, r["E_ph"].ctypes.data_as(PD))

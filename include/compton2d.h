@@ -268,6 +268,26 @@ typedef struct c2d_fp_step_out {
 } c2d_fp_step_out;
 
 /* ------------------------------------------------------------------------
+ * Per-step emission / absorption tables (replaces the per-cell loop of
+ * imcgen2d, src/imcgen2d.f:209-333, with volume_em, src/volume2d.f:10-394):
+ * B from ep_switch, l_min, volume_em (kappa_tot = kappa_sy, eps_tot, eps_th,
+ * Eloss_cy, Eloss_th), Eloss_sy from f_nt, and the dt*vol / dt*zsurf scaling.
+ * Pair annihilation is inert (pair_switch = 0 path, hazard H6).
+ * ---------------------------------------------------------------------- */
+typedef struct c2d_vem_in {
+  double dt;                                         /* dt(1)                     */
+  c2d_array2 tea, tna, n_e, B_field, f_pair, zsurf, vol;
+  c2d_iarray2 ep_switch;                             /* null data: all 0          */
+  c2d_array3 f_nt;                                   /* (e-bin, j, k) like Pnt    */
+} c2d_vem_in;
+
+typedef struct c2d_vem_out {                         /* any data may be NULL      */
+  c2d_marray3 kappa_tot, eps_tot, eps_th;            /* (energy, j, k)            */
+  c2d_marray2 B_field, Eloss_sy, Eloss_cy, Eloss_th, Eloss_tot;
+  double* E_ph;                                      /* [C2D_N_VOL] photon grid   */
+} c2d_vem_out;
+
+/* ------------------------------------------------------------------------
  * Observer-frame binning of escape events on the device (replaces running
  * postprocessing/pspt.c:245-322 and plcm.c:382-456 over p###_evb.dat).
  * Bin edges are explicit arrays so each tool's own edge arithmetic is kept
@@ -362,6 +382,14 @@ int  c2d_obs_result(c2d_ctx* ctx, double* F, double* F2, double* count, double* 
 
 /* Device time of the last c2d_fp_step's FP kernel (HIP events, ms). */
 int  c2d_last_fp_ms(c2d_ctx* ctx, double* ms);
+
+/* imcgen2d's per-cell emission/absorption loop (volume_em for every cell)
+ * on the GPU, one workgroup per cell; results written to the host arrays of
+ * `out` and kept on the device (the next c2d_set_step may still pass them).
+ * Synchronous. */
+int  c2d_volume_em(c2d_ctx* ctx, const c2d_vem_in* in, c2d_vem_out* out);
+/* Device time of the last c2d_volume_em kernel (HIP events, ms). */
+int  c2d_last_vem_ms(c2d_ctx* ctx, double* ms);
 /* Packet-steps executed by that generation-0 launch (roofline numerator). */
 int  c2d_last_gen0_steps(c2d_ctx* ctx, int64_t* steps);
 

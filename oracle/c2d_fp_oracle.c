@@ -111,6 +111,11 @@ static double gamma_bar_g(double Theta, int64_t* guard) {
   return g;
 }
 
+double c2o_mcdonald(double nu, double z) {
+  int64_t guard = 0;
+  return mcdonald(nu, z, &guard);
+}
+
 double c2o_gamma_bar(double Theta) {
   int64_t guard = 0;
   return gamma_bar_g(Theta, &guard);

@@ -52,7 +52,11 @@ for f in $OBJS; do objs="$objs $OUT/obj/$f.o"; done
   "$HERE/c2d_censdrv.f" -o "$OUT/obj/c2d_censdrv.o"
 "$FC" -o "$OUT/c2d_censdrv" "$OUT/obj/c2d_censdrv.o" "$OUT/obj/census2d.o" \
   -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
-echo "build_ref: $OUT/c2d_refdrv $OUT/c2d_censdrv"
+"$FC" -c $FFLAGS -I"$MPI_INC" -I"$SRC" -module-dir "$OUT/mod" \
+  "$HERE/c2d_vemdrv.f" -o "$OUT/obj/c2d_vemdrv.o"
+"$FC" -o "$OUT/c2d_vemdrv" "$OUT/obj/c2d_vemdrv.o" "$OUT/obj/volume2d.o" \
+  -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
+echo "build_ref: $OUT/c2d_refdrv $OUT/c2d_censdrv $OUT/c2d_vemdrv"
 
 # The post-processing tools (postprocessing/pspt.c, plcm.c: K&R C reading an
 # input deck on stdin) for the observer-frame binning fixtures.

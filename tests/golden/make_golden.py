@@ -230,6 +230,67 @@ def make_observer(out_dir: Path, work: Path) -> Path:
     return path
 
 
+def vem_cells():
+    """Cell states for the volume_em fixture: the inputm.dat medium, the
+    reference's own f_nt of the FP fixtures (after FP steps), and draws that
+    reach every branch (Theta < / > 0.2, the absorbed branch, nu <= nu_p)."""
+    rng = np.random.default_rng(11)
+    fnts = []
+    for case in ("ssc_tau", "grid3x4"):
+        g = np.load(HERE / ("%s.npz" % case))
+        fnts += list(g["in0_f_nt"].reshape(-1, 200)[:2])
+    for case in ("fp_pick", "fp_inj"):
+        g = np.load(HERE / ("%s.npz" % case))
+        for n in (1, 2):
+            if "fpout%d_f_nt" % n in g.files:
+                fnts += list(g["fpout%d_f_nt" % n].reshape(-1, 200)[:2])
+    gnt = np.load(HERE / "ssc_tau.npz")["cfg_gnt"]
+    cells = [  # T_keV, n_e, B, l_min
+        (100.0, 80.0, 0.13, 3.75e15), (500.0, 4.0e6, 1.0, 1.0e15), (5.0, 1.0e3, 0.01, 5.0e15),
+        (50.0, 1.0e10, 100.0, 1.0e13), (1000.0, 1.0e8, 10.0, 1.0e12), (102.0, 2.0e6, 0.13, 3.0e15),
+        (300.0, 1.0e12, 1.0, 1.0e16),
+    ]
+    for _ in range(17):
+        cells.append((10 ** rng.uniform(0.5, 3.0), 10 ** rng.uniform(0.0, 11.0),
+                      10 ** rng.uniform(-2.0, 2.5), 10 ** rng.uniform(12.0, 16.0)))
+    out = []
+    for i, (T, ne, B, lm) in enumerate(cells):
+        out.append(dict(T=T, ne=ne, B=B, l_min=lm, amxwl=0.0, gmin=1e2, gmax=1e5, p_nth=2.3,
+                        f_pair=0.0, f_nt=np.asarray(fnts[i % len(fnts)], np.float64)))
+    return gnt, out
+
+
+def make_vem(out_dir: Path, work: Path) -> Path:
+    """The reference's own volume_em (src/volume2d.f) on vem_cells(), through
+    oracle/ref/c2d_vemdrv.f; pins oracle/c2d_vem_oracle.c."""
+    import subprocess
+    gnt, cells = vem_cells()
+    w = work / "vem"
+    w.mkdir(parents=True, exist_ok=True)
+    with open(w / "in.bin", "wb") as f:
+        f.write(np.array([len(cells)], "<i4").tobytes())
+        f.write(np.asarray(gnt, "<f8").tobytes())
+        for c in cells:
+            f.write(np.array([c["T"], c["ne"], c["B"], c["l_min"], c["amxwl"], c["gmin"], c["gmax"],
+                              c["p_nth"], c["f_pair"]], "<f8").tobytes())
+            f.write(c["f_nt"].astype("<f8").tobytes())
+    subprocess.run([str(ROOT / "oracle" / "_ref" / "c2d_vemdrv"), str(w / "in.bin"), str(w / "out.bin")],
+                   check=True, stdout=subprocess.DEVNULL)
+    raw = np.fromfile(w / "out.bin", "<f8")
+    n = len(cells)
+    E_ph = raw[:400]
+    rec = raw[400:].reshape(n, 3 * 400 + 2)
+    path = out_dir / "vem.npz"
+    np.savez_compressed(
+        path, gnt=gnt, E_ph=E_ph,
+        state=np.array([[c["T"], c["ne"], c["B"], c["l_min"]] for c in cells]),
+        f_nt=np.array([c["f_nt"] for c in cells]),
+        kappa_tot=rec[:, :400], eps_tot=rec[:, 400:800], eps_th=rec[:, 800:1200],
+        Eloss_cy=rec[:, 1200], Eloss_th=rec[:, 1201],
+        source="reference volume_em (src/volume2d.f:10-394) via oracle/ref/c2d_vemdrv.f")
+    return path
+
+
 def make_medium(out_path: Path, work: Path) -> None:
     """Per-cell tables of the inputm.dat medium (n_e=80, B=0.13 G, p=2.3)."""
     d = work / "medium"
@@ -269,6 +330,9 @@ def main() -> None:
             print("wrote", p, p.stat().st_size, "bytes")
         if not args.only or args.only == "census_fmt":
             p = make_census_format(out, work)
+            print("wrote", p, p.stat().st_size, "bytes")
+        if not args.only or args.only == "vem":
+            p = make_vem(out, work)
             print("wrote", p, p.stat().st_size, "bytes")
         if not args.only or args.only == "obs":
             p = make_observer(out, work)

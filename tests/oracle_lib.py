@@ -178,3 +178,41 @@ def obs_bin(binning, events: np.ndarray, flavor: str = "ref"):
     if rc != 0:
         raise RuntimeError("c2o_obs_bin failed: %d" % rc)
     return F, F2, cnt
+
+
+def volume_em(gnt, f_nt, T_keV, ne, B, l_min, flavor: str = "ref"):
+    """One cell of volume_em (oracle/c2d_vem_oracle.c): kappa, eps_tot,
+    eps_th [400], Eloss_cy, Eloss_th (raw sums)."""
+    lib = load(flavor)
+    P = C.POINTER(C.c_double)
+    lib.c2o_volume_em.restype = None
+    lib.c2o_volume_em.argtypes = [P, P] + [C.c_double] * 4 + [P] * 5
+    g = np.ascontiguousarray(gnt, np.float64)
+    f = np.ascontiguousarray(f_nt, np.float64)
+    kap, et, eh = (np.zeros(abi.N_VOL) for _ in range(3))
+    ecy, eth = C.c_double(), C.c_double()
+    lib.c2o_volume_em(g.ctypes.data_as(P), f.ctypes.data_as(P), T_keV, ne, B, l_min,
+                      kap.ctypes.data_as(P), et.ctypes.data_as(P), eh.ctypes.data_as(P),
+                      C.byref(ecy), C.byref(eth))
+    return kap, et, eh, ecy.value, eth.value
+
+
+def vem_grid(flavor: str = "ref") -> np.ndarray:
+    lib = load(flavor)
+    e = np.zeros(abi.N_VOL)
+    lib.c2o_vem_grid.argtypes = [C.POINTER(C.c_double)]
+    lib.c2o_vem_grid(e.ctypes.data_as(C.POINTER(C.c_double)))
+    return e
+
+
+def vem_step(grid: abi.GridConfig, dt: float, state: dict, flavor: str = "det") -> dict:
+    """imcgen2d's per-cell loop (oracle c2o_vem_step) over dense state arrays."""
+    lib = load(flavor)
+    lib.c2o_vem_step.restype = C.c_int
+    lib.c2o_vem_step.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VemIn), C.POINTER(abi.VemOut)]
+    g = grid.to_ctypes()
+    call = abi.VemCall(dt, state)
+    rc = lib.c2o_vem_step(C.byref(g), C.byref(call.sin), C.byref(call.sout))
+    if rc != 0:
+        raise RuntimeError("c2o_vem_step failed: %d" % rc)
+    return call.res
