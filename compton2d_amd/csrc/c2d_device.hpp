@@ -170,6 +170,26 @@ struct GenArgs {
   int32_t gen;
 };
 
+/* ---- emission / absorption tables (vem.hip) ---- */
+/* per-cell input record [ncell][VZ_N], packed by the host */
+enum : int32_t {
+  VZ_TEA = 0, VZ_TNA, VZ_NE, VZ_B, VZ_FPAIR, VZ_ZSURF, VZ_VOL, VZ_EP, VZ_LMIN, VZ_N = 12
+};
+/* per-cell output record [ncell][VO_N] */
+enum : int32_t { VO_B = 0, VO_ESY, VO_ECY, VO_ETH, VO_ETOT, VO_N = 8 };
+struct VemParams {
+  const double* zin;      /* [ncell][VZ_N]          */
+  const double* f_nt;     /* [ncell][NUM_NT]        */
+  const double* gnt;      /* [NUM_NT]               */
+  const double* E_ph;     /* [N_VOL] photon grid    */
+  const double* mcd;      /* McDonald abscissae (C2D_FP_MCD_N x 4) */
+  double dE, pow3_15, dt; /* grid ratio, 3**1.5, dt(1) */
+  double* kappa;          /* [ncell][N_VOL] outputs */
+  double* eps_tot;
+  double* eps_th;
+  double* zout;           /* [ncell][VO_N]          */
+};
+
 /* ---- Fokker-Planck solve (fp.hip) ---- */
 /* per-zone input record [ncell][FZ_N], packed by the host */
 enum : int32_t {

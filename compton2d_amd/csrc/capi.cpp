@@ -35,6 +35,7 @@ extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
                                       float* tab, int ncell, hipStream_t s);
 extern "C" int c2d_launch_fp(const FpParams* P, int ncell, hipStream_t s);
+extern "C" int c2d_launch_vem(const VemParams* P, int ncell, hipStream_t s);
 extern "C" int c2d_launch_obs(const ObsDev* O, const double* ev, int64_t n, int grid,
                               hipStream_t s);
 extern "C" size_t c2d_obs_lds_bytes(int n_t, int n_mu, int n_e, int lds_rows);
@@ -142,6 +143,10 @@ struct c2d_ctx {
          *fp_nf = nullptr, *fp_fout = nullptr, *fp_Pout = nullptr, *fp_zout = nullptr;
   int32_t* fp_err = nullptr;
   float last_fp_ms = 0.f;
+  /* emission / absorption tables (c2d_volume_em) */
+  double *vem_zin = nullptr, *vem_fnt = nullptr, *vem_eph = nullptr, *vem_kap = nullptr,
+         *vem_et = nullptr, *vem_eh = nullptr, *vem_zout = nullptr;
+  float last_vem_ms = 0.f;
   /* observer-frame binning */
   bool obs_ready = false;
   ObsDev obs;
@@ -312,6 +317,9 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
   void* optrs[] = {c->obs_edges, c->obs_hist, c->obs_ev};
   for (void* p : optrs)
     if (p) (void)hipFree(p);
+  void* vptrs[] = {c->vem_zin, c->vem_fnt, c->vem_eph, c->vem_kap, c->vem_et, c->vem_eh, c->vem_zout};
+  for (void* q : vptrs)
+    if (q) (void)hipFree(q);
   void* fptrs[] = {c->fp_FT, c->fp_mcd, c->fp_zin, c->fp_fin, c->fp_Pin, c->fp_nf, c->fp_fout, c->fp_Pout,
                    c->fp_zout, c->fp_err};
   for (void* p : fptrs)
@@ -846,6 +854,28 @@ extern "C" int c2d_last_kernel_ms(c2d_ctx* c, double* gen0_ms, double* all_ms, i
 /* ------------------------------------------------------------------ */
 /* Fokker-Planck (src/update2d.f:7-327, FP_calc :337-1739)             */
 /* ------------------------------------------------------------------ */
+/* McDonald series abscissae (volume2d.f:604-620) for the wave-level K2/K3
+ * (c2d_wave.hpp): t_n by repeated multiplication exactly as the reference
+ * loop forms it, with the argument-independent factors of each term (same
+ * c2d_math code and rounding as the kernels).  Built once per context. */
+static int ensure_mcd(c2d_ctx* c) {
+  if (c->fp_mcd) return C2D_OK;
+  std::vector<double> mt((size_t)C2D_FP_MCD_N * 4);
+  const double dtm = 1.001, sm = 5.0e-1 * (1.0 + dtm);
+  double t = 1.0;
+  for (int n = 0; n < C2D_FP_MCD_N; n++) {
+    const double ts = t * sm;
+    mt[(size_t)n * 4 + 0] = t;
+    mt[(size_t)n * 4 + 1] = ts;
+    mt[(size_t)n * 4 + 2] = c2d_pow(ts * ts - 1.0, 1.5);
+    mt[(size_t)n * 4 + 3] = c2d_pow(ts * ts - 1.0, 2.5);
+    t = t * dtm;
+  }
+  HIPCHK(c, dalloc(&c->fp_mcd, mt.size()));
+  HIPCHK(c, hipMemcpy(c->fp_mcd, mt.data(), mt.size() * sizeof(double), hipMemcpyHostToDevice));
+  return C2D_OK;
+}
+
 extern "C" int c2d_fp_set_config(c2d_ctx* c, const c2d_fp_config* fc) {
   if (!c || !fc || !fc->F_IC) return C2D_E_ARG;
   if (fc->pair_switch != 0)
@@ -864,24 +894,8 @@ extern "C" int c2d_fp_set_config(c2d_ctx* c, const c2d_fp_config* fc) {
     HIPCHK(c, dalloc(&c->fp_Pout, nc * C2D_NUM_NT));
     HIPCHK(c, dalloc(&c->fp_zout, nc * FO_N));
     HIPCHK(c, dalloc(&c->fp_err, 1));
-    /* McDonald series abscissae (volume2d.f:604-620): t_n by repeated
-     * multiplication exactly as the reference loop forms it, with the
-     * argument-independent factors of each term (same c2d_math code and
-     * rounding as the kernel) */
-    std::vector<double> mt((size_t)C2D_FP_MCD_N * 4);
-    const double dtm = 1.001, sm = 5.0e-1 * (1.0 + dtm);
-    double t = 1.0;
-    for (int n = 0; n < C2D_FP_MCD_N; n++) {
-      const double ts = t * sm;
-      mt[(size_t)n * 4 + 0] = t;
-      mt[(size_t)n * 4 + 1] = ts;
-      mt[(size_t)n * 4 + 2] = c2d_pow(ts * ts - 1.0, 1.5);
-      mt[(size_t)n * 4 + 3] = c2d_pow(ts * ts - 1.0, 2.5);
-      t = t * dtm;
-    }
-    HIPCHK(c, dalloc(&c->fp_mcd, mt.size()));
-    HIPCHK(c, hipMemcpy(c->fp_mcd, mt.data(), mt.size() * sizeof(double), hipMemcpyHostToDevice));
   }
+  if (int rc = ensure_mcd(c)) return rc;
   /* F_IC(i, ph) -> FT[ph][i]: lanes (bins i) read consecutive addresses */
   std::vector<double> ft((size_t)C2D_NPHFIELD * C2D_NUM_NT);
   for (int ph = 0; ph < C2D_NPHFIELD; ph++)
@@ -1024,6 +1038,105 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
 extern "C" int c2d_last_fp_ms(c2d_ctx* c, double* ms) {
   if (!c || !ms) return C2D_E_ARG;
   *ms = c->last_fp_ms;
+  return C2D_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* emission / absorption tables (imcgen2d.f:209-333, volume_em)         */
+/* ------------------------------------------------------------------ */
+extern "C" int c2d_volume_em(c2d_ctx* c, const c2d_vem_in* in, c2d_vem_out* out) {
+  if (!c || !in || !out) return C2D_E_ARG;
+  if (!in->tea.data || !in->tna.data || !in->n_e.data || !in->B_field.data || !in->f_pair.data ||
+      !in->zsurf.data || !in->vol.data || !in->f_nt.data)
+    return fail(c, C2D_E_ARG, "c2d_volume_em: missing input array");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const int nz = c->nz, nr = c->nr;
+  const size_t nc = (size_t)c->ncell;
+  if (!c->vem_zin) {
+    HIPCHK(c, dalloc(&c->vem_zin, nc * VZ_N));
+    HIPCHK(c, dalloc(&c->vem_fnt, nc * C2D_NUM_NT));
+    HIPCHK(c, dalloc(&c->vem_eph, (size_t)C2D_N_VOL));
+    HIPCHK(c, dalloc(&c->vem_kap, nc * C2D_N_VOL));
+    HIPCHK(c, dalloc(&c->vem_et, nc * C2D_N_VOL));
+    HIPCHK(c, dalloc(&c->vem_eh, nc * C2D_N_VOL));
+    HIPCHK(c, dalloc(&c->vem_zout, nc * VO_N));
+  }
+  if (int rc = ensure_mcd(c)) return rc;
+  /* the photon grid volume_em writes into E_ph (volume2d.f:98,106-107) */
+  const double dE = c2d_exp(c2d_log(1.0e20) / (double)C2D_N_VOL);
+  std::vector<double> eph(C2D_N_VOL);
+  double E = 1.0e-10 / dE;
+  for (int i = 0; i < C2D_N_VOL; i++) {
+    E = E * dE;
+    eph[i] = E;
+  }
+  std::vector<double> zin(nc * VZ_N, 0.0), fnt(nc * C2D_NUM_NT);
+  for (int j = 0; j < nz; j++)
+    for (int k = 0; k < nr; k++) {
+      const size_t cell = (size_t)j * nr + k;
+      double* z = &zin[cell * VZ_N];
+      z[VZ_TEA] = at2(in->tea, j, k);
+      z[VZ_TNA] = at2(in->tna, j, k);
+      z[VZ_NE] = at2(in->n_e, j, k);
+      z[VZ_B] = at2(in->B_field, j, k);
+      z[VZ_FPAIR] = at2(in->f_pair, j, k);
+      z[VZ_ZSURF] = at2(in->zsurf, j, k);
+      z[VZ_VOL] = at2(in->vol, j, k);
+      z[VZ_EP] = in->ep_switch.data ? (double)in->ep_switch.data[j * in->ep_switch.s_j + k * in->ep_switch.s_k] : 0.0;
+      /* l_min (imcgen2d.f:238-246) */
+      const double dz = (j == 0) ? c->cfg.z[0] : c->cfg.z[j] - c->cfg.z[j - 1];
+      const double drr = (k == 0) ? c->cfg.r[0] - c->cfg.rmin : c->cfg.r[k] - c->cfg.r[k - 1];
+      z[VZ_LMIN] = (dz < drr) ? dz : drr;
+      for (int i = 0; i < C2D_NUM_NT; i++)
+        fnt[cell * C2D_NUM_NT + i] = in->f_nt.data[i * in->f_nt.s_i + j * in->f_nt.s_j + k * in->f_nt.s_k];
+    }
+  const hipStream_t st = c->stream;
+  HIPCHK(c, hipMemcpyAsync(c->vem_zin, zin.data(), zin.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->vem_fnt, fnt.data(), fnt.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->vem_eph, eph.data(), eph.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  VemParams P;
+  P.zin = c->vem_zin; P.f_nt = c->vem_fnt; P.gnt = c->gnt; P.E_ph = c->vem_eph; P.mcd = c->fp_mcd;
+  P.dE = dE; P.pow3_15 = c2d_pow(3.0, 1.5); P.dt = in->dt;
+  P.kappa = c->vem_kap; P.eps_tot = c->vem_et; P.eps_th = c->vem_eh; P.zout = c->vem_zout;
+  HIPCHK(c, hipEventRecord(c->ev_g0a, st));
+  int rc = c2d_launch_vem(&P, (int)nc, st);
+  if (rc) return fail(c, C2D_E_HIP, "vem launch: %s", hipGetErrorString((hipError_t)rc));
+  HIPCHK(c, hipEventRecord(c->ev_g0b, st));
+  std::vector<double> kap(nc * C2D_N_VOL), et(nc * C2D_N_VOL), eh(nc * C2D_N_VOL), zo(nc * VO_N);
+  HIPCHK(c, hipMemcpyAsync(kap.data(), c->vem_kap, kap.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(et.data(), c->vem_et, et.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(eh.data(), c->vem_eh, eh.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(zo.data(), c->vem_zout, zo.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  (void)hipEventElapsedTime(&c->last_vem_ms, c->ev_g0a, c->ev_g0b);
+  if (out->E_ph) std::copy(eph.begin(), eph.end(), out->E_ph);
+  auto put3 = [&](c2d_marray3& m, const std::vector<double>& v, size_t cell, int j, int k) {
+    if (!m.data) return;
+    for (int i = 0; i < C2D_N_VOL; i++)
+      m.data[i * m.s_i + j * m.s_j + k * m.s_k] = v[cell * C2D_N_VOL + i];
+  };
+  auto put2 = [&](c2d_marray2& m, int j, int k, double v) {
+    if (m.data) m.data[j * m.s_j + k * m.s_k] = v;
+  };
+  for (int j = 0; j < nz; j++)
+    for (int k = 0; k < nr; k++) {
+      const size_t cell = (size_t)j * nr + k;
+      put3(out->kappa_tot, kap, cell, j, k);
+      put3(out->eps_tot, et, cell, j, k);
+      put3(out->eps_th, eh, cell, j, k);
+      const double* o = &zo[cell * VO_N];
+      put2(out->B_field, j, k, o[VO_B]);
+      put2(out->Eloss_sy, j, k, o[VO_ESY]);
+      put2(out->Eloss_cy, j, k, o[VO_ECY]);
+      put2(out->Eloss_th, j, k, o[VO_ETH]);
+      put2(out->Eloss_tot, j, k, o[VO_ETOT]);
+    }
+  return C2D_OK;
+}
+
+extern "C" int c2d_last_vem_ms(c2d_ctx* c, double* ms) {
+  if (!c || !ms) return C2D_E_ARG;
+  *ms = c->last_vem_ms;
   return C2D_OK;
 }
 

@@ -96,6 +96,10 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_fp_step.argtypes = [vp, C.POINTER(abi.FpStepIn), C.POINTER(abi.FpStepOut)]
     lib.c2d_last_fp_ms.restype = C.c_int
     lib.c2d_last_fp_ms.argtypes = [vp, C.POINTER(C.c_double)]
+    lib.c2d_volume_em.restype = C.c_int
+    lib.c2d_volume_em.argtypes = [vp, C.POINTER(abi.VemIn), C.POINTER(abi.VemOut)]
+    lib.c2d_last_vem_ms.restype = C.c_int
+    lib.c2d_last_vem_ms.argtypes = [vp, C.POINTER(C.c_double)]
     lib.c2d_obs_begin.restype = C.c_int
     lib.c2d_obs_begin.argtypes = [vp, C.POINTER(abi.ObsBins)]
     lib.c2d_obs_accumulate.restype = C.c_int
@@ -263,6 +267,20 @@ class Engine:
     def last_fp_ms(self) -> float:
         ms = C.c_double()
         self._check(self.lib.c2d_last_fp_ms(self.ctx, C.byref(ms)))
+        return ms.value
+
+    # -- emission / absorption tables (imcgen2d.f:209-333, volume_em) ---------
+    def volume_em(self, dt: float, state: dict) -> dict:
+        """kappa_tot, eps_tot, eps_th [nz, nr, 400], B_field, Eloss_sy/cy/th/tot
+        [nz, nr] and E_ph [400] for the cell state (tea, tna, n_e, B_field,
+        f_pair, zsurf, vol [nz, nr], f_nt [nz, nr, 200], ep_switch)."""
+        call = abi.VemCall(dt, state)
+        self._check(self.lib.c2d_volume_em(self.ctx, C.byref(call.sin), C.byref(call.sout)))
+        return call.res
+
+    def last_vem_ms(self) -> float:
+        ms = C.c_double()
+        self._check(self.lib.c2d_last_vem_ms(self.ctx, C.byref(ms)))
         return ms.value
 
     # -- observer-frame binning (postprocessing/pspt.c, plcm.c) ---------------

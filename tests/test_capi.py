@@ -50,7 +50,9 @@ int main(void) {
   P(c2d_config, seed) P(c2d_config, rank) P(c2d_config, queue_capacity) P(c2d_config, mu)
   P(c2d_step_in, kappa_tot) P(c2d_step_in, nsv) P(c2d_step_in, tbbl) P(c2d_step_in, spectra)
   P(c2d_step_in, n_spectra) P(c2d_step_in, dt)
-  printf("c2d_obs_bins %zu\n", sizeof(c2d_obs_bins));
+  printf("c2d_obs_bins %zu\nc2d_vem_in %zu\nc2d_vem_out %zu\n", sizeof(c2d_obs_bins),
+         sizeof(c2d_vem_in), sizeof(c2d_vem_out));
+  P(c2d_vem_in, ep_switch) P(c2d_vem_in, f_nt) P(c2d_vem_out, E_ph) P(c2d_vem_out, Eloss_tot)
   P(c2d_obs_bins, t_offset) P(c2d_obs_bins, t1) P(c2d_obs_bins, n_mu) P(c2d_obs_bins, E1)
   return 0;
 }
@@ -71,9 +73,11 @@ int main(void) {
     assert int(got["c2d_fp_step_in"]) == C.sizeof(abi.FpStepIn)
     assert int(got["c2d_fp_step_out"]) == C.sizeof(abi.FpStepOut)
     assert int(got["c2d_obs_bins"]) == C.sizeof(abi.ObsBins)
+    assert int(got["c2d_vem_in"]) == C.sizeof(abi.VemIn)
+    assert int(got["c2d_vem_out"]) == C.sizeof(abi.VemOut)
     classes = {"c2d_config": abi.Config, "c2d_step_in": abi.StepIn, "c2d_fp_config": abi.FpConfig,
                "c2d_fp_step_in": abi.FpStepIn, "c2d_fp_step_out": abi.FpStepOut,
-               "c2d_obs_bins": abi.ObsBins}
+               "c2d_obs_bins": abi.ObsBins, "c2d_vem_in": abi.VemIn, "c2d_vem_out": abi.VemOut}
     for key, val in got.items():
         if "." in key:
             t, f = key.split(".")
