@@ -110,6 +110,25 @@ module compton2d
      real(c_double) :: E_tot_old = 0, E_tot_new = 0, hr_total = 0, hr_st_total = 0, dT_max = 0
   end type c2d_fp_step_out
 
+  ! ---- emission / absorption tables (c2d_volume_em; imcgen2d.f:209-333) ----
+  type, bind(C) :: c2d_iarray2
+     type(c_ptr) :: data = c_null_ptr
+     integer(c_int64_t) :: s_j = 0, s_k = 0
+  end type c2d_iarray2
+
+  type, bind(C) :: c2d_vem_in
+     real(c_double) :: dt = 0
+     type(c2d_array2) :: tea, tna, n_e, B_field, f_pair, zsurf, vol
+     type(c2d_iarray2) :: ep_switch              ! null data: all 0
+     type(c2d_array3) :: f_nt
+  end type c2d_vem_in
+
+  type, bind(C) :: c2d_vem_out
+     type(c2d_marray3) :: kappa_tot, eps_tot, eps_th
+     type(c2d_marray2) :: B_field, Eloss_sy, Eloss_cy, Eloss_th, Eloss_tot
+     type(c_ptr) :: E_ph = c_null_ptr
+  end type c2d_vem_out
+
   ! ---- observer-frame binning (c2d_obs_*; postprocessing/pspt.c, plcm.c) ----
   integer, parameter :: C2D_OBS_SED = 0, C2D_OBS_LC = 1
 
@@ -230,6 +249,13 @@ module compton2d
        type(c2d_fp_step_in), intent(in) :: fin
        type(c2d_fp_step_out), intent(inout) :: fout
      end function c2d_fp_step
+
+     integer(c_int) function c2d_volume_em(ctx, vin, vout) bind(C, name='c2d_volume_em')
+       import :: c_int, c_ptr, c2d_vem_in, c2d_vem_out
+       type(c_ptr), value :: ctx
+       type(c2d_vem_in), intent(in) :: vin
+       type(c2d_vem_out), intent(inout) :: vout
+     end function c2d_volume_em
 
      integer(c_int) function c2d_obs_begin(ctx, bins) bind(C, name='c2d_obs_begin')
        import :: c_int, c_ptr, c2d_obs_bins
