@@ -176,9 +176,13 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
 
   double hr = 0.0, hr_st = 0.0, sum_E = 0.0, t_fp = 0.0;
   int fp_steps = 0;
+  /* gamma_bar is a pure function and label 200 evaluates it at the Th_e the
+   * previous sub-step's temperature search ended on, whose value that search
+   * computed last: reuse it (one McDonald pair per sub-step saved, exact) */
+  double g_av_next = 0.0;
   for (;;) {
     /* label 200 (:577) */
-    double g_av = gamma_bar_w(Th_e, lane, P.mcd, guard);
+    double g_av = (fp_steps == 0) ? gamma_bar_w(Th_e, lane, P.mcd, guard) : g_av_next;
     /* hr_th_c = hr_th_c - x_i, i.e. + (-x_i) bit for bit */
     const double hr_th_c = seq_sum(0.0, 1, NT - 1, lane, [&](int i) {
       return -(8.176e-7 * s_dgic[i] * s_fold[i] * (s_gnt[i + 1] - s_gnt[i]) * volume * n_lept);
@@ -468,6 +472,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
     }
     Te_new = 5.11e2 * The_new;
     Th_e = The_new;
+    g_av_next = g_av;                                  /* = gamma_bar(Th_e) */
     if (!(t_fp < P.dt)) break;                         /* :1473 */
   }
 
