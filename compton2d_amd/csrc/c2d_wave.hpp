@@ -83,9 +83,19 @@ __device__ inline double gammln(double xx) {
  * (c2d_fp_set_config); only exp(z*ts) depends on the argument.  Beyond the
  * table the abscissa chain is replayed per lane from the last value.  Terms
  * are added in the reference's order up to each series' own stopping term,
- * so K2 and K3 equal two sequential McDonald calls bit for bit. */
+ * so K2 and K3 equal two sequential McDonald calls bit for bit.  The terms of
+ * a pass go through `scr` (LDS, 2*FPB doubles owned by this wave): every lane
+ * reads them back with broadcast loads that issue ahead of the add chain, so
+ * the chain runs at the adds' latency (a readlane chain serialises on its
+ * SGPR hazards: ~108 cycles per term against ~15). */
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ inline void mcdonald23_w(double z, int lane, const double* __restrict__ tab, double& K2,
-                             double& K3, long long& guard) {
+                             double& K3, long long& guard, double* scr) {
   const double dt = 1.001, d = dt - 1.0, s = 5.0e-1 * (1.0 + dt);
   double sum2 = 0.0, sum3 = 0.0, t0 = 1.0;
   bool run2 = true, run3 = true;
@@ -116,15 +126,20 @@ __device__ inline void mcdonald23_w(double z, int lane, const double* __restrict
     const int n2 = run2 ? (st2 ? __ffsll((long long)st2) : FPB) : 0;
     const int n3 = run3 ? (st3 ? __ffsll((long long)st3) : FPB) : 0;
     const int nm = n2 > n3 ? n2 : n3;
+    scr[lane] = term2;
+    scr[FPB + lane] = term3;
+    wave_sync();
     if (n2 == FPB && n3 == FPB) {
+#pragma unroll 16
       for (int m = 0; m < FPB; m++) {
-        sum2 = sum2 + rl(term2, m);
-        sum3 = sum3 + rl(term3, m);
+        sum2 = sum2 + scr[m];
+        sum3 = sum3 + scr[FPB + m];
       }
     } else {
-      for (int m = 0; m < n2; m++) sum2 = sum2 + rl(term2, m);
-      for (int m = 0; m < n3; m++) sum3 = sum3 + rl(term3, m);
+      for (int m = 0; m < n2; m++) sum2 = sum2 + scr[m];
+      for (int m = 0; m < n3; m++) sum3 = sum3 + scr[FPB + m];
     }
+    wave_sync();
     if (st2) run2 = false;
     if (st3) run3 = false;
     guard += nm;
@@ -136,7 +151,8 @@ __device__ inline void mcdonald23_w(double z, int lane, const double* __restrict
 }
 
 /* gamma_bar (volume2d.f:572-594) */
-__device__ inline double gamma_bar_w(double Theta, int lane, const double* tab, long long& guard) {
+__device__ inline double gamma_bar_w(double Theta, int lane, const double* tab, long long& guard,
+                                     double* scr) {
   double g;
   if (Theta < F32(0.2)) {
     g = (1. + F32(4.375) * Theta + F32(7.383) * (Theta * Theta) +
@@ -145,7 +161,7 @@ __device__ inline double gamma_bar_w(double Theta, int lane, const double* tab, 
         Theta;
   } else {
     double K2, K3;
-    mcdonald23_w(1.0 / Theta, lane, tab, K2, K3, guard);
+    mcdonald23_w(1.0 / Theta, lane, tab, K2, K3, guard, scr);
     g = K3 / K2 - Theta;
   }
   if (g < 1.0) g = 1.0;

@@ -93,6 +93,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
   __shared__ double s_gnt[NT + 2], s_gam[NT + 2], s_fold[NT + 2], s_fnew[NT + 2];
   __shared__ double s_dgic[NT + 2], s_dgdt[NT + 2], s_disp[NT + 2];
   __shared__ double s_a[NT + 2], s_b[NT + 2], s_c[NT + 2];
+  __shared__ double s_mcd[2 * FPB];   /* McDonald term exchange (c2d_wave.hpp) */
   __shared__ double s_smw[NT + 2], s_bigW[NT + 2], s_bigC[NT + 2], s_em[NT + 2], s_inj[NT + 2];
   __shared__ double s_Pnt[NT + 2], s_nf[NPH];
 
@@ -180,9 +181,17 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
    * previous sub-step's temperature search ended on, whose value that search
    * computed last: reuse it (one McDonald pair per sub-step saved, exact) */
   double g_av_next = 0.0;
+#ifdef C2D_FP_PROF
+  long long pf_gb = 0, pf_tri = 0, pf_loop0 = clock64(), pf_t0, pf_calls = 0;
+#define PF_BEGIN() pf_t0 = clock64()
+#define PF_END(acc) acc += clock64() - pf_t0
+#else
+#define PF_BEGIN()
+#define PF_END(acc)
+#endif
   for (;;) {
     /* label 200 (:577) */
-    double g_av = (fp_steps == 0) ? gamma_bar_w(Th_e, lane, P.mcd, guard) : g_av_next;
+    double g_av = (fp_steps == 0) ? gamma_bar_w(Th_e, lane, P.mcd, guard, s_mcd) : g_av_next;
     /* hr_th_c = hr_th_c - x_i, i.e. + (-x_i) bit for bit */
     const double hr_th_c = seq_sum(0.0, 1, NT - 1, lane, [&](int i) {
       return -(8.176e-7 * s_dgic[i] * s_fold[i] * (s_gnt[i + 1] - s_gnt[i]) * volume * n_lept);
@@ -354,6 +363,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
       s_a[NT] = 0.0; s_b[NT] = 1.0; s_c[NT] = 0.0;
     }
     __syncthreads();
+    PF_BEGIN();
     /* tridag (:2476-2518): the recurrences run in the reference order on
      * wave-uniform values (readlane) with each 64-bin chunk's operands staged
      * in registers; gam is kept in s_smw */
@@ -413,6 +423,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
       }
       __syncthreads();
     }
+    PF_END(pf_tri);
     if (lane == 0) {
       s_fnew[NT] = 0.0;
       s_fnew[1] = 0.0;
@@ -452,20 +463,28 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
       return s_gam[i] * s_fnew[i] * (s_gnt[i + 1] - s_gnt[i]);
     });
     double The_new = Th_e;
+    PF_BEGIN();
     if (gbar > g_av) {
       while (gbar > g_av) {
         The_new = The_new * F32(1.005);
-        g_av = gamma_bar_w(The_new, lane, P.mcd, guard);
+#ifdef C2D_FP_PROF
+        pf_calls++;
+#endif
+        g_av = gamma_bar_w(The_new, lane, P.mcd, guard, s_mcd);
         if (guard > GUARD_MAX) break;
       }
     } else {
       while (gbar < g_av) {
         The_new = The_new / F32(1.005);
-        g_av = gamma_bar_w(The_new, lane, P.mcd, guard);
+#ifdef C2D_FP_PROF
+        pf_calls++;
+#endif
+        g_av = gamma_bar_w(The_new, lane, P.mcd, guard, s_mcd);
         if (The_new < 1.0e-2) break;
         if (guard > GUARD_MAX) break;
       }
     }
+    PF_END(pf_gb);
     if (guard > GUARD_MAX) {
       if (lane == 0) atomicOr(P.err, FPERR_GUARD);
       return;
@@ -561,6 +580,12 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
     zo[FO_DIAG + C2D_FP_STEPS] = (double)fp_steps;
     zo[FO_DIAG + C2D_FP_SKIPPED] = 0.0;
     zo[FO_DIAG + 7] = 0.0;
+#ifdef C2D_FP_PROF
+    zo[FO_DIAG + 0] = (double)pf_gb;
+    zo[FO_DIAG + 1] = (double)pf_tri;
+    zo[FO_DIAG + 2] = (double)(clock64() - pf_loop0);
+    zo[FO_DIAG + 3] = (double)pf_calls;
+#endif
   }
 }
 

@@ -1,13 +1,16 @@
 /*
  * selftest.hip — device-side diagnostics exported through the C-ABI:
- * evaluates the deterministic elementary functions (c2d_math.h) and the
- * lineage RNG (c2d_rng.h) on the GPU so tests can check them bit for bit
- * against the host build of the same code.
+ * evaluates the deterministic elementary functions (c2d_math.h), the
+ * lineage RNG (c2d_rng.h) and McDonald's series (c2d_wave.hpp) on the GPU so
+ * tests can check them bit for bit against the host build of the same code.
  */
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "c2d_math.h"
 #include "c2d_rng.h"
+#include "c2d_wave.hpp"
 
 namespace c2d {
 __global__ void c2d_selftest_math_kernel(int fn, const double* x, double* y, int64_t n) {
@@ -46,5 +49,64 @@ extern "C" int c2d_selftest_math(int device, int fn, const double* x_host, doubl
   if (!rc && hipMemcpy(y_host, y, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) rc = -2;
   (void)hipFree(x);
   (void)hipFree(y);
+  return rc;
+}
+
+/* McDonald K2, K3 at n arguments z (one wavefront each, c2d_wave.hpp's
+ * mcdonald23_w) and the shader cycles each evaluation took: parity with the
+ * oracle's sequential McDonald (src/volume2d.f:598-626) and a latency probe. */
+
+namespace c2d {
+__global__ void __launch_bounds__(64) c2d_selftest_mcd_kernel(const double* z, const double* tab,
+                                                             double* out, int n) {
+  const int i = blockIdx.x;
+  if (i >= n) return;
+  const int lane = threadIdx.x;
+  __shared__ double scr[2 * wave::FPB];
+  long long guard = 0;
+  double K2, K3;
+  const long long t0 = clock64();
+  wave::mcdonald23_w(z[i], lane, tab, K2, K3, guard, scr);
+  const long long t1 = clock64();
+  if (lane == 0) {
+    out[3 * i] = K2;
+    out[3 * i + 1] = K3;
+    out[3 * i + 2] = (double)(t1 - t0);
+  }
+}
+}  // namespace c2d
+
+extern "C" int c2d_selftest_mcdonald(int device, const double* z_host, int n, double* out_host) {
+  if (n <= 0) return 0;
+  if (hipSetDevice(device) != hipSuccess) return -2;
+  std::vector<double> mt((size_t)C2D_FP_MCD_N * 4);
+  const double dtm = 1.001, sm = 5.0e-1 * (1.0 + dtm);
+  double t = 1.0;
+  for (int k = 0; k < C2D_FP_MCD_N; k++) {
+    const double ts = t * sm;
+    mt[(size_t)k * 4 + 0] = t;
+    mt[(size_t)k * 4 + 1] = ts;
+    mt[(size_t)k * 4 + 2] = c2d_pow(ts * ts - 1.0, 1.5);
+    mt[(size_t)k * 4 + 3] = c2d_pow(ts * ts - 1.0, 2.5);
+    t = t * dtm;
+  }
+  double *z = nullptr, *tab = nullptr, *out = nullptr;
+  int rc = 0;
+  if (hipMalloc((void**)&z, n * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&tab, mt.size() * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&out, 3 * (size_t)n * sizeof(double)) != hipSuccess)
+    rc = -2;
+  if (!rc && (hipMemcpy(z, z_host, n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemcpy(tab, mt.data(), mt.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess))
+    rc = -2;
+  if (!rc) {
+    hipLaunchKernelGGL(c2d::c2d_selftest_mcd_kernel, dim3((unsigned)n), dim3(64), 0, 0, z, tab, out, n);
+    if (hipDeviceSynchronize() != hipSuccess) rc = -2;
+  }
+  if (!rc && hipMemcpy(out_host, out, 3 * (size_t)n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+    rc = -2;
+  if (z) (void)hipFree(z);
+  if (tab) (void)hipFree(tab);
+  if (out) (void)hipFree(out);
   return rc;
 }

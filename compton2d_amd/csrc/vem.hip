@@ -70,6 +70,7 @@ __global__ void __launch_bounds__(VEM_BLOCK) c2d_vem_kernel(const VemParams P) {
   __shared__ double s_gnt[NT], s_f[NT], s_q[NT], s_gamp[NT], s_facg[NT], s_dg[NT];
   __shared__ double s_cP[NV], s_cC[NV], s_cT[NV], s_P[NV], s_Pth[NV];
   __shared__ double s_sc[8];   /* B, K2, f_rz, P_sum, sum_th, Eloss_cy, Eloss_th, Eloss_sy */
+  __shared__ double s_mcd[2 * FPB];   /* McDonald term exchange (wave 0) */
   const int cell = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const double* zin = P.zin + (int64_t)cell * VZ_N;
@@ -91,7 +92,7 @@ __global__ void __launch_bounds__(VEM_BLOCK) c2d_vem_kernel(const VemParams P) {
         uB = 1.5 * Th + 7.5 * (Th * Th);
       } else {
         double K2b, K3b;
-        mcdonald23_w(1.0 / Th, lane, P.mcd, K2b, K3b, guard);
+        mcdonald23_w(1.0 / Th, lane, P.mcd, K2b, K3b, guard, s_mcd);
         uB = K3b / K2b - Th - 1.0;
       }
       if (ep == 1)
@@ -103,7 +104,7 @@ __global__ void __launch_bounds__(VEM_BLOCK) c2d_vem_kernel(const VemParams P) {
     const double Theta = tea / 5.11e2;
     double K2 = 0.0, K2m = 0.0, K3m = 0.0;
     const bool big = !(Theta < F32(0.2)) || !(Theta < 2.0e-1);
-    if (big) mcdonald23_w(1. / Theta, lane, P.mcd, K2m, K3m, guard);
+    if (big) mcdonald23_w(1. / Theta, lane, P.mcd, K2m, K3m, guard, s_mcd);
     if (Theta < 2.0e-1)                                 /* volume2d.f:56-65 */
       K2 = 1.2533 * __builtin_sqrt(Theta) *
            (1. + 1.875 * Theta + 8.2031e-1 * (Theta * Theta) - 2.03e-1 * (Theta * Theta * Theta)) /

@@ -336,6 +336,20 @@ def obs_engine(device: int = 0) -> Engine:
     return Engine(g)
 
 
+def device_mcdonald(z: np.ndarray, device: int = 0):
+    """K2(z), K3(z) by the GPU's wave-level McDonald series and the shader
+    cycles of each evaluation (c2d_selftest_mcdonald)."""
+    lib = load_library()
+    lib.c2d_selftest_mcdonald.restype = C.c_int
+    lib.c2d_selftest_mcdonald.argtypes = [C.c_int, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double)]
+    z = np.ascontiguousarray(z, np.float64)
+    out = np.zeros((len(z), 3))
+    rc = lib.c2d_selftest_mcdonald(device, z.ctypes.data_as(abi.PD), len(z), out.ctypes.data_as(abi.PD))
+    if rc != 0:
+        raise C2DError(rc, "c2d_selftest_mcdonald failed")
+    return out[:, 0], out[:, 1], out[:, 2]
+
+
 def device_math(fn: int, x: np.ndarray, device: int = 0) -> np.ndarray:
     """Evaluate c2d_math function `fn` on the GPU (c2d_selftest_math)."""
     lib = load_library()

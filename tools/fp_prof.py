@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""FP kernel section timers (build with FP_FLAGS=-DC2D_FP_PROF; select it with
+C2D_LIBRARY): shader cycles per zone in the temperature search (gamma_bar),
+the tridiagonal solve and the whole sub-step loop, from zone_diag slots 0-2."""
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
+
+
+def main():
+    from compton2d_amd.engine import Engine
+    from fp_bench import tiled_case
+    c, g, tile = tiled_case(8, 8)
+    g.device = 0
+    eng = Engine(g)
+    eng.fp_set_config(c.constants())
+    r = eng.fp_step(tile["ncycle"], tile["time"], tile["dt"], tile, tile)
+    d = np.asarray(r["zone_diag"]).reshape(-1, 8)
+    steps = d[:, 5]
+    out = {"zones": len(d), "substeps_mean": float(steps.mean()), "kernel_ms": eng.last_fp_ms()}
+    for i, k in enumerate(("search_cycles", "tridag_cycles", "loop_cycles", "search_calls")):
+        out[k + "_per_substep"] = float((d[:, i] / steps).mean())
+    print(json.dumps(out))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
