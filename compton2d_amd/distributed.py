@@ -69,3 +69,105 @@ def barrier(device=None) -> None:
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
+
+
+# ---------------------------------------------------------------------------
+# census load balance (replaces imcredist, src/imcredist.f:5-133)
+# ---------------------------------------------------------------------------
+REC_WORDS = 13   # 6 f64 + 5 i32 + lineage key as two 32-bit halves, all exact in f64
+
+
+def rebalance_plan(counts):
+    """Deterministic moves (src, dst, n) that level `counts` to
+    total//W (+1 on the lowest ranks): surplus ranks, in rank order, fill
+    deficit ranks in rank order (every rank computes the same plan)."""
+    W = len(counts)
+    total = int(sum(counts))
+    target = [total // W + (1 if r < total % W else 0) for r in range(W)]
+    sur = [[r, int(counts[r]) - target[r]] for r in range(W) if counts[r] > target[r]]
+    dfc = [[r, target[r] - int(counts[r])] for r in range(W) if counts[r] < target[r]]
+    plan, i, j = [], 0, 0
+    while i < len(sur) and j < len(dfc):
+        n = min(sur[i][1], dfc[j][1])
+        plan.append((sur[i][0], dfc[j][0], n))
+        sur[i][1] -= n
+        dfc[j][1] -= n
+        if sur[i][1] == 0:
+            i += 1
+        if dfc[j][1] == 0:
+            j += 1
+    return plan
+
+
+def _pack(d6, i5, keys):
+    import numpy as np
+    k = np.asarray(keys, np.uint64)
+    return np.column_stack([np.asarray(d6, np.float64), np.asarray(i5, np.float64),
+                            (k & np.uint64(0xFFFFFFFF)).astype(np.float64),
+                            (k >> np.uint64(32)).astype(np.float64)])
+
+
+def _unpack(rec):
+    import numpy as np
+    rec = np.asarray(rec, np.float64).reshape(-1, REC_WORDS)
+    keys = rec[:, 11].astype(np.uint64) | (rec[:, 12].astype(np.uint64) << np.uint64(32))
+    return rec[:, :6].copy(), rec[:, 6:11].astype(np.int32), keys
+
+
+def rebalance_census(d6, i5, keys, device=None):
+    """Level the census record counts over the ranks (records as exported by
+    Engine.census(): d6 [n,6], i5 [n,5], keys [n]).  Records move whole, so
+    with lineage keys the histories, and every tally, do not depend on which
+    rank tracks them.  Collectives: one all_gather of the counts, then
+    point-to-point transfers of the surplus records."""
+    import numpy as np
+    if not is_dist():
+        return d6, i5, keys
+    import torch
+    import torch.distributed as dist
+    rank, W = dist.get_rank(), dist.get_world_size()
+    n = len(keys)
+    cnt = torch.tensor([n], dtype=torch.int64, device=device)
+    allc = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(W)]
+    dist.all_gather(allc, cnt)
+    counts = [int(c.item()) for c in allc]
+    plan = rebalance_plan(counts)
+    rec = _pack(d6, i5, keys)
+    keep = n - sum(m for s, _, m in plan if s == rank)
+    ops, sends, recvs = [], [], []
+    off = keep
+    for s, d, m in plan:
+        if s == rank:
+            t = torch.from_numpy(np.ascontiguousarray(rec[off:off + m])).to(device)
+            off += m
+            sends.append(t)
+            ops.append(dist.P2POp(dist.isend, t, d))
+        elif d == rank:
+            t = torch.empty((m, REC_WORDS), dtype=torch.float64, device=device)
+            recvs.append(t)
+            ops.append(dist.P2POp(dist.irecv, t, s))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    parts = [rec[:keep]] + [t.cpu().numpy() for t in recvs]
+    return _unpack(np.concatenate(parts) if parts else rec[:0])
+
+
+def rebalance_engine_census(engine, threshold: float = 0.1, device=None) -> bool:
+    """imcredist for an Engine: when the largest census exceeds the mean by
+    more than `threshold`, export, level and re-import (all ranks call it)."""
+    if not is_dist():
+        return False
+    import torch
+    import torch.distributed as dist
+    n = engine.census_count()
+    t = torch.tensor([float(n)], dtype=torch.float64, device=device)
+    mx = t.clone()
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    mean = float(t.item()) / dist.get_world_size()
+    if mean <= 0 or float(mx.item()) <= (1.0 + threshold) * mean:
+        return False
+    d6, i5, keys = engine.census()
+    engine.import_census(*rebalance_census(d6, i5, keys, device=device))
+    return True
