@@ -204,7 +204,7 @@ enum : int32_t { FPERR_STEPS = 1, FPERR_GUARD = 2 };
 #define C2D_FP_MCD_N 16384
 
 struct FpParams {
-  int32_t nz, nr, pick_sw, inj_switch, inj_dis, g2var_switch, cf_sentinel, pad0;
+  int32_t nz, nr, pick_sw, inj_switch, inj_dis, g2var_switch, cf_sentinel, pair_sw;
   double time, dt, df_implicit, df_T, r_esc, r_acc;
   double r_flare, z_flare, t_flare, sigma_r, sigma_z, sigma_t, flare_amp;
   double inj_g1, inj_g2, inj_p, inj_t, inj_L, pick_rate, inj_gg, inj_sigma, inj_v;

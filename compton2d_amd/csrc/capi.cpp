@@ -878,8 +878,8 @@ static int ensure_mcd(c2d_ctx* c) {
 
 extern "C" int c2d_fp_set_config(c2d_ctx* c, const c2d_fp_config* fc) {
   if (!c || !fc || !fc->F_IC) return C2D_E_ARG;
-  if (fc->pair_switch != 0)
-    return fail(c, C2D_E_ARG, "pair_switch=1 in the FP solve (pa_calc/trid_p) is not supported");
+  if (fc->pair_switch != 0 && fc->pair_switch != 1)
+    return fail(c, C2D_E_ARG, "pair_switch must be 0 or 1 (got %d)", fc->pair_switch);
   if (fc->inj_switch != 0 && fc->inj_dis != 1 && fc->inj_dis != 2)
     return fail(c, C2D_E_ARG, "inj_dis must be 1 or 2 when inj_switch is on (got %d)", fc->inj_dis);
   HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -938,6 +938,10 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
       z[FZ_ECOLD] = a2(in->ec_old, j, k, 0.0);
       z[FZ_TURB] = a2(in->turb_lev, j, k, 0.0);
       z[FZ_FPAIR] = a2(in->f_pair, j, k, 0.0);
+      if (c->fpc.pair_switch == 1 && z[FZ_FPAIR] != 0.0)
+        return fail(c, C2D_E_ARG,
+                    "pair_switch=1 needs f_pair = 0 (positrons are inert, H6); zone (%d,%d) has %g",
+                    j + 1, k + 1, z[FZ_FPAIR]);
       const double* pp = m2(out->p_nth, j, k);
       z[FZ_PNTH] = pp ? *pp : 0.0;
       for (int i = 0; i < C2D_NUM_NT; i++) {
@@ -962,7 +966,7 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   memset(&P, 0, sizeof P);
   const c2d_fp_config& f = c->fpc;
   P.nz = nz; P.nr = nr; P.pick_sw = f.pick_sw; P.inj_switch = f.inj_switch; P.inj_dis = f.inj_dis;
-  P.g2var_switch = f.g2var_switch; P.cf_sentinel = f.cf_sentinel;
+  P.g2var_switch = f.g2var_switch; P.cf_sentinel = f.cf_sentinel; P.pair_sw = f.pair_switch;
   P.time = in->time; P.dt = in->dt; P.df_implicit = f.df_implicit; P.df_T = f.df_T;
   P.r_esc = f.r_esc; P.r_acc = f.r_acc; P.r_flare = f.r_flare; P.z_flare = f.z_flare;
   P.t_flare = f.t_flare; P.sigma_r = f.sigma_r; P.sigma_z = f.sigma_z; P.sigma_t = f.sigma_t;
@@ -1080,6 +1084,10 @@ extern "C" int c2d_volume_em(c2d_ctx* c, const c2d_vem_in* in, c2d_vem_out* out)
       z[VZ_NE] = at2(in->n_e, j, k);
       z[VZ_B] = at2(in->B_field, j, k);
       z[VZ_FPAIR] = at2(in->f_pair, j, k);
+      if (c->cfg.pair_switch == 1 && !(z[VZ_FPAIR] < 1.0e-10))  /* volume2d.f:322 */
+        return fail(c, C2D_E_ARG,
+                    "volume_em: pair annihilation (pair_switch=1, f_pair=%g in zone (%d,%d)) needs "
+                    "a positron population; positrons are inert here (H6)", z[VZ_FPAIR], j + 1, k + 1);
       z[VZ_ZSURF] = at2(in->zsurf, j, k);
       z[VZ_VOL] = at2(in->vol, j, k);
       z[VZ_EP] = in->ep_switch.data ? (double)in->ep_switch.data[j * in->ep_switch.s_j + k * in->ep_switch.s_k] : 0.0;

@@ -252,7 +252,19 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
     }
     double d_t = f_t_implicit * P.dt;                  /* :1142-1146 */
     if (d_t > (P.dt - t_fp)) d_t = 1.00001 * (P.dt - t_fp);
-    n_positron = 0.0;                                  /* pairs off (:1164-1167) */
+    if (P.pair_sw == 1) {
+      /* pairs on with no positrons (H6: n_pos = dn_pp = 0, f_pair = 0): the
+       * pa_calc rates vanish, so loop 460 (:1187-1217) adds 0/ne and clips
+       * f_old below 1e-50; trid_p solves for npos = 0 (:1400), unused here */
+      __syncthreads();
+      for (int i = lane + 1; i <= NT - 1; i += FPB) {
+        double v = s_fold[i] + 0.0 / ne;
+        if (v < 1.0e-50) v = 0.0;
+        s_fold[i] = v;
+      }
+      __syncthreads();
+    }
+    n_positron = 0.0;                                  /* :1164-1167 / :1218 */
     ne = n_p + n_positron;
     /* injection (:1226-1306) */
     double n_inject = 0.0;

@@ -225,7 +225,7 @@ typedef struct c2d_marray2 { double* data; int64_t s_j, s_k; } c2d_marray2;
  * F_IC from IC_loss src/icloss2d.f:1-64, broadcast by FP_bcast
  * src/fp_mpi.f:596). */
 typedef struct c2d_fp_config {
-  int32_t pair_switch;            /* pairs in the FP solve: only 0 supported    */
+  int32_t pair_switch;            /* 0/1; 1 = inert positrons (H6), f_pair = 0  */
   double  df_implicit, df_T;      /* 1e-2, 0.25 in the reference               */
   double  r_esc, r_acc;           /* escape / acceleration time [z(nz)/c]      */
   int32_t cf_sentinel;            /* coronal flare on/off                      */
@@ -272,7 +272,8 @@ typedef struct c2d_fp_step_out {
  * imcgen2d, src/imcgen2d.f:209-333, with volume_em, src/volume2d.f:10-394):
  * B from ep_switch, l_min, volume_em (kappa_tot = kappa_sy, eps_tot, eps_th,
  * Eloss_cy, Eloss_th), Eloss_sy from f_nt, and the dt*vol / dt*zsurf scaling.
- * Pair annihilation is inert (pair_switch = 0 path, hazard H6).
+ * Pair annihilation is inert (volume2d.f:322 skips it for f_pair < 1e-10; with
+ * pair_switch = 1 a larger f_pair is C2D_E_ARG, hazard H6).
  * ---------------------------------------------------------------------- */
 typedef struct c2d_vem_in {
   double dt;                                         /* dt(1)                     */

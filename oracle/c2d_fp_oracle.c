@@ -25,8 +25,10 @@
  * Hazard H10: dg_ic(num_nt) is never assigned (loop :568-574 stops at
  * num_nt-1) yet dgdt(num_nt) enters b_i(num_nt-1) through smw(num_nt-1)
  * (:1375-1386).  It is taken as 0, here and on the GPU.
- * pair_switch = 1 (pa_calc, trid_p, positron bookkeeping :1164-1221) is
- * not restated; c2o_fp_step rejects it, like the GPU path.
+ * pair_switch = 1 is restated for the MPI reference's inert pairs (H6:
+ * n_pos, dn_pp and f_pair stay 0): pa_calc's rates are then -0/0, trid_p
+ * solves for npos = 0, and the only trace on the electrons is loop 460's
+ * f_old clip below 1e-50 (:1187-1217).  f_pair != 0 is rejected.
  *
  * Built twice with c2d_oracle.c: glibc libm (liboracle_ref: parity with the
  * Fortran FP_calc) and c2d_math.h (liboracle_det: parity with the GPU).
@@ -280,7 +282,15 @@ static int fp_calc(const c2d_config* g, const c2d_fp_config* fc, double time, do
     }
     double d_t = f_t_implicit * dt;                     /* :1142-1146 */
     if (d_t > (dt - t_fp)) d_t = 1.00001 * (dt - t_fp);
-    /* pairs off (:1164-1167, :1219-1221) */
+    if (fc->pair_switch == 1) {
+      /* pairs on, no positrons (H6): loop 460 (:1187-1217) with dn_pp = 0 and
+       * pa_calc's dne_pa = -ne*f*pa_el = -0 adds 0/ne and clips f_old */
+      for (int i = 1; i <= NT - 1; i++) {
+        f_old[i] = f_old[i] + 0.0 / ne;
+        if (f_old[i] < 1.0e-50) f_old[i] = 0.0;
+      }
+    }
+    /* no positrons either way (:1164-1167, :1218-1221) */
     n_positron = 0.0;
     ne = n_p + n_positron;
     /* injection (:1226-1306) */
@@ -484,11 +494,15 @@ static double* M2(const c2d_marray2* a, int j, int k) {
 int c2o_fp_step(const c2d_config* g, const c2d_fp_config* fc, const c2d_fp_step_in* in,
                 c2d_fp_step_out* out) {
   if (!g || !fc || !in || !out) return C2D_E_ARG;
-  if (fc->pair_switch != 0) return C2D_E_ARG;
+  if (fc->pair_switch != 0 && fc->pair_switch != 1) return C2D_E_ARG;
   if (fc->inj_switch != 0 && fc->inj_dis != 1 && fc->inj_dis != 2) return C2D_E_ARG;
   if (!fc->F_IC || !in->n_field.data || !in->ecens.data || !out->f_nt.data || !out->Pnt.data)
     return C2D_E_ARG;
   const int nz = g->nz, nr = g->nr;
+  if (fc->pair_switch == 1)
+    for (int j = 0; j < nz; j++)
+      for (int k = 0; k < nr; k++)
+        if (A2(&in->f_pair, j, k, 0.0) != 0.0) return C2D_E_ARG;
   double* FIC = (double*)malloc(sizeof(double) * NT * NPH);
   if (!FIC) return C2D_E_NOMEM;
   for (int i = 0; i < NT; i++)

@@ -78,6 +78,10 @@ c     IC loss kernel of setup (icloss2d.f:1-64), input of FP_calc
       close(u)
 c
       do 500 n = 0, nsteps-1
+c        H6: the master's n_ph never receives the workers' tallies (no
+c        reduce of it, src/update2d.f:1958-1973) and stays 0, so pairprod
+c        (dn_pp) and kgg_calc (k_gg) see no photons under MPI
+         if (pair_switch.eq.1) n_ph = 0.d0
 c        master part of the step
          call imcgen2d
 c        worker-side resets (src/imcgen2d.f:559-601)

@@ -54,6 +54,10 @@ FP_CASES = {
                              g2var_switch=1, inj_t=0.0, inj_L=5e40, cf_sentinel=1,
                              flare_amp=10.0, t_flare=1.0e5, sigma_t=1.0e6, sigma_r=1.0e16,
                              sigma_z=1.0e16), nsteps=3),
+    # C3's pair_switch = 1 (src_20121026/input.dat): pa_calc / trid_p / loop
+    # 460 run with the MPI build's inert positrons (hazard H6)
+    "fp_pair": dict(case=dict(nz=2, nr=2, n_e=4.0e6, nst=400, T_const=0, pick_sw=1,
+                              turb_lev=1.0e-2, pair_switch=1), nsteps=3),
 }
 FP_CONST_KEYS = ("cf_sentinel", "r_flare", "z_flare", "t_flare", "sigma_r", "sigma_z", "sigma_t",
                  "flare_amp", "r_esc", "r_acc", "inj_switch", "inj_dis", "g2var_switch", "pick_sw",

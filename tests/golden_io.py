@@ -50,7 +50,7 @@ class GoldenCase:
         return self.a["out%d_%s" % (n, key)]
 
 
-FP_CASES = ("fp_pick", "fp_inj")
+FP_CASES = ("fp_pick", "fp_inj", "fp_pair")
 
 
 def fp_fic() -> np.ndarray:
@@ -81,7 +81,8 @@ class FpGoldenCase:
         return g
 
     def constants(self) -> abi.FpConstants:
-        return abi.FpConstants(F_IC=fp_fic(), **self.meta["fp_const"])
+        return abi.FpConstants(F_IC=fp_fic(), pair_switch=int(self.meta.get("pair_switch", 0)),
+                               **self.meta["fp_const"])
 
     def fp_in(self, n: int) -> dict:
         d = {k[len("fpin%d_" % n):]: v for k, v in self.a.items() if k.startswith("fpin%d_" % n)}

@@ -82,3 +82,32 @@ def test_gamma_bar_limits():
     for th in (0.5, 2.0, 10.0):                  # relativistic limit <gamma> ~ 3 Theta
         g = lib.c2o_gamma_bar(th)
         assert 1.0 < g and abs(g / (3 * th) - 1) < 0.6
+
+
+def test_fp_pair_switch_branch_is_exercised():
+    """fp_pair runs the reference with pair_switch = 1 (C3's setting) and the
+    MPI build's inert positrons (H6, emulated in oracle/ref/c2d_refdrv.f by
+    the master's n_ph staying 0): loop 460 (update2d.f:1187-1217) clips
+    f_old below 1e-50 every sub-step, so the pair_switch = 0 solve differs
+    from the reference on this fixture while pair_switch = 1 is bit-exact
+    (test above)."""
+    case = FpGoldenCase("fp_pair")
+    c0 = case.constants()
+    c0.pair_switch = 0
+    differs = False
+    for n in case.steps:
+        fi = case.fp_in(n)
+        assert np.all(fi["f_pair"] == 0.0)
+        r = OL.fp_step(case.grid(), c0, fi["ncycle"], fi["time"], fi["dt"], fi, fi, flavor="ref")
+        differs |= not np.array_equal(r["f_nt"], case.fp_out(n)["f_nt"])
+    assert differs
+
+
+def test_fp_pair_switch_rejects_positron_population():
+    case = FpGoldenCase("fp_pair")
+    fi = case.fp_in(case.steps[0])
+    fi["f_pair"] = fi["f_pair"].copy()
+    fi["f_pair"][0, 0] = 0.2
+    with pytest.raises(RuntimeError):
+        OL.fp_step(case.grid(), case.constants(), fi["ncycle"], fi["time"], fi["dt"], fi, fi,
+                   flavor="ref")

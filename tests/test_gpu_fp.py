@@ -58,14 +58,22 @@ def test_gpu_fp_reads_photon_field_from_device_tallies():
     eng.close()
 
 
-def test_gpu_fp_rejects_pairs_and_requires_config():
-    case = FpGoldenCase("fp_pick")
+def test_gpu_fp_rejects_positrons_and_requires_config():
+    """pair_switch = 1 runs with the MPI build's inert positrons (H6); a zone
+    with f_pair != 0 (a positron population) and pair_switch = 2 are errors."""
+    case = FpGoldenCase("fp_pair")
     eng = Engine(case.grid(device=0))
     fi = case.fp_in(case.steps[0])
     with pytest.raises(Exception, match="C2D_E_STATE"):
         eng.fp_step(fi["ncycle"], fi["time"], fi["dt"], fi, fi)
     c = case.constants()
-    c.pair_switch = 1
+    assert c.pair_switch == 1
+    eng.fp_set_config(c)
+    bad = dict(fi, f_pair=fi["f_pair"].copy())
+    bad["f_pair"][1, 0] = 0.1
+    with pytest.raises(Exception, match="C2D_E_ARG"):
+        eng.fp_step(fi["ncycle"], fi["time"], fi["dt"], bad, fi)
+    c.pair_switch = 2
     with pytest.raises(Exception, match="C2D_E_ARG"):
         eng.fp_set_config(c)
     eng.close()

@@ -11,8 +11,8 @@ on the GPU through the C-ABI
 
 on a 30x9 grid (C3's zone count, Mrk 421 set-up src_20121026/input.dat) of the
 inputm.dat medium with FP on (pick-up switch of the FP fixture's constants,
-tests/golden/fp_pick.npz; pair_switch = 0, pairs being inert in the MPI
-reference, hazard H6).  Reports per-phase times per step and packet-steps/s.
+tests/golden/fp_pair.npz, with C3's pair_switch = 1: positrons inert as in the
+MPI reference, hazard H6).  Reports per-phase times per step and packet-steps/s.
 Synthetic: the medium's tables and electron spectrum are the reference's
 (compton2d_amd/data/medium_inputm.npz); no network, no checkpoints.
 
@@ -59,7 +59,7 @@ def main():
     fixed = dict(tna=full(100.0), B_field=full(0.13), f_pair=full(0.0), turb_lev=full(1e-20), vol=vol,
                  zsurf=zs)
     eng = Engine(wl.grid)
-    eng.fp_set_config(FpGoldenCase("fp_pick").constants())
+    eng.fp_set_config(FpGoldenCase("fp_pair").constants())
     dt = wl.dt
     ec_old = np.zeros(cells)
     rows = []
