@@ -101,6 +101,13 @@ __device__ __forceinline__ void gor(int32_t* p, int32_t v) {
   __hip_atomic_fetch_or((C2D_GLOBAL int32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+/* n_field census tallies go to C2D_NF_REPL replicas (workgroup b adds to
+ * replica b mod C2D_NF_REPL), summed into the tally buffer after the last
+ * generation.  f64 atomics execute at the memory side and serialise per
+ * address; packets that census together share (cell, energy bin), so a single
+ * copy is a hot spot (2.5x on the EC light-curve workload). */
+#define C2D_NF_REPL 32
+
 struct KParams {
   int32_t nz, nr, ncell, nphtotal, nph_lc, nmu;
   int32_t split1, split2, split3, spl3_trg, spec_switch;
@@ -148,6 +155,7 @@ struct KParams {
   int64_t n_vol_global, n_surf_global;
   /* tallies */
   double* T;
+  double* nf_rep;           /* C2D_NF_REPL replicas of n_field, [r][cell][nphfield] */
   TallyOff off;
   unsigned long long* cnt;  /* [C2D_NCOUNTERS] */
   int32_t* err;

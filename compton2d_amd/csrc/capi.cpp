@@ -123,6 +123,7 @@ struct c2d_ctx {
   DevPk pk;
   double* T = nullptr;
   double* T_own = nullptr;
+  double* nf_rep = nullptr;     /* C2D_NF_REPL x ncell x nphfield */
   unsigned long long* ctl = nullptr;
   int32_t* derr = nullptr;
   KParams* dP = nullptr;
@@ -275,6 +276,7 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   }
   HIPCHK(c, dalloc(&c->T_own, (size_t)c->L.total));
   HIPCHK(c, hipMemset(c->T_own, 0, sizeof(double) * c->L.total));
+  HIPCHK(c, dalloc(&c->nf_rep, (size_t)C2D_NF_REPL * c->ncell * C2D_NPHFIELD));
   c->T = c->T_own;
   HIPCHK(c, dalloc(&c->ctl, CTL_WORDS));
   HIPCHK(c, dalloc(&c->derr, 1));
@@ -303,7 +305,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
   void* ptrs[] = {c->geo, c->gnt, c->kappa_cur, c->kappa_prev, c->eps_tot, c->eps_th, c->f_nt,
                   c->Pnt, c->n_e, c->vfrac, c->ewsv, c->surf_ew, c->surf_tbb, c->tbbl,
                   c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comS,
-                  c->ev, c->q2[0], c->q2[1], c->q3[0], c->q3[1], c->T_own, c->ctl, c->derr, c->dP};
+                  c->ev, c->q2[0], c->q2[1], c->q3[0], c->q3[1], c->T_own, c->nf_rep, c->ctl, c->derr, c->dP};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int b = 0; b < 2; b++) {
@@ -504,6 +506,17 @@ extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
   return C2D_OK;
 }
 
+/* n_field[i] += sum of the C2D_NF_REPL census replicas (replica order: fixed) */
+__global__ void __launch_bounds__(256) c2d_nf_reduce(const double* __restrict__ rep, int64_t n,
+                                                     double* __restrict__ nf) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int r = 0; r < C2D_NF_REPL; r++) s += rep[r * n + i];
+    if (s != 0.0) nf[i] += s;
+  }
+}
+
 extern "C" int c2d_run_step(c2d_ctx* c) {
   if (!c) return C2D_E_ARG;
   if (!c->have_step) return fail(c, C2D_E_STATE, "c2d_set_step must precede c2d_run_step");
@@ -538,6 +551,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.cap_ev_sh = c->ev_cap_sh;
   P.cap_q = cfg.queue_capacity;
   P.T = c->T;
+  P.nf_rep = c->nf_rep;
   P.off.edep = c->L.edep; P.off.prdep = c->L.prdep; P.off.ecens = c->L.ecens;
   P.off.npcen = c->L.npcen; P.off.n_field = c->L.n_field; P.off.E_IC = c->L.E_IC;
   P.off.nelectron = c->L.nelectron; P.off.fout = c->L.fout; P.off.edout = c->L.edout;
@@ -577,6 +591,8 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.cap_pk = c->pk.cap;
 
   HIPCHK(c, hipMemsetAsync(c->T, 0, sizeof(double) * c->L.total, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->nf_rep, 0, sizeof(double) * C2D_NF_REPL * c->ncell * C2D_NPHFIELD,
+                           c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl, 0, sizeof(unsigned long long) * CTL_WORDS, c->stream));
   HIPCHK(c, hipMemsetAsync(c->derr, 0, sizeof(int32_t), c->stream));
 
@@ -655,6 +671,14 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     HIPCHK(c, hipMemcpyAsync(nq, c->ctl + CTL_N2, sizeof nq, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     gen++;
+  }
+  {
+    const int64_t n = (int64_t)c->ncell * C2D_NPHFIELD;
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 16);
+    hipLaunchKernelGGL(c2d_nf_reduce, dim3(grid), dim3(256), 0, c->stream, c->nf_rep, n,
+                       c->T + c->L.n_field);
+    HIPCHK(c, hipGetLastError());
+    launches++;
   }
   HIPCHK(c, hipEventRecord(c->ev_end, c->stream));
   unsigned long long ctl[CTL_WORDS];

@@ -133,6 +133,9 @@ struct Tal {
 enum : int { TC_EDEP = 0, TC_PRDEP = 1, TC_ECENS = 2, TC_NPCEN = 3 };
 /* cell tallies edep|prdep|ecens|npcen: LDS when privatised, else the fused buffer */
 __device__ __forceinline__ void cell_add(const KParams& P, const Tal& T, int which, int cell, double v) {
+#ifdef C2D_ABLATE_CELL_TALLY            /* profiling ablation only (tools/build_sweep.sh) */
+  if (v != 12345.0) return;
+#endif
   if (P.lds_cells) atomicAdd(&c2d_tr_lds[T.cells_off + which * P.ncell + cell], v);
   else gadd(P.T + P.off.edep + which * P.ncell + cell, v);
 }
@@ -522,8 +525,13 @@ __device__ __forceinline__ void census_write(const KParams& P, const Tal& T, con
   cell_add(P, T, TC_ECENS, cell, p.ew);
   int i = grid_index(g->E_field, C2D_NPHFIELD, p.xnu);
   double Egg_min = (g->E_field[1] * g->E_field[1]) / g->E_field[2];
+#ifdef C2D_ABLATE_NFIELD                /* profiling ablation only (tools/build_sweep.sh) */
+  if (p.xnu < 0.0)
+#else
   if (p.xnu > Egg_min)
-    gadd(&P.T[P.off.n_field + (int64_t)cell * C2D_NPHFIELD + (i - 1)], 6.25e8 * p.ew / p.xnu);
+#endif
+    gadd(&P.nf_rep[(int64_t)(blockIdx.x % C2D_NF_REPL) * P.ncell * C2D_NPHFIELD +
+                   (int64_t)cell * C2D_NPHFIELD + (i - 1)], 6.25e8 * p.ew / p.xnu);
   unsigned long long slot = wave_reserve(P.n_cout);
   if (slot < (unsigned long long)P.cap_cout) {
     gst(P.cout.rpre + slot, p.rpre);

@@ -86,3 +86,19 @@ def test_g25_spectrum_is_usable():
     tab, int_file = S.file_sp(S.seed_spectrum("blackbody_G25_4spectra"), S.EcConstants(g_bulk=25.0))
     assert len(tab.E_file) == abi.NFMAX - 1
     assert np.isfinite(tab.P_file).all() and tab.P_file[-1] == 1.0 and int_file > 0
+
+
+@pytest.mark.skipif(not (REF_DISK.parent / "postprocessing").is_dir(),
+                    reason="reference sources not present (GPU box)")
+def test_c5_binning_equals_ext25_deck():
+    import importlib.util
+    from compton2d_amd import observer as O
+    root = Path(__file__).resolve().parents[1]
+    spec = importlib.util.spec_from_file_location("c5_bench", root / "tools" / "c5_bench.py")
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    a = m.ext25_binning()
+    b = O.parse_plcm_deck((REF_DISK.parent / "postprocessing" / "ext25_lc.input").read_text())
+    for k in ("mode", "gam_bulk", "rmax", "t0", "t1", "mu0", "mu1", "E0", "E1", "dt",
+              "t_offset", "t_stop"):
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k))
