@@ -76,7 +76,9 @@ struct TallyOff {
 #define C2D_EV_SHARDS 32
 #define C2D_EV_SHARD_STRIDE 16
 
+#ifndef C2D_COMTAB_N
 #define C2D_COMTAB_N 2048
+#endif
 /* comtot table: x grid in u = ln(xnu/keV) */
 #define C2D_COMTAB_U0 (-27.631021115928547)   /* ln(1e-12) */
 #define C2D_COMTAB_U1 (29.933606208922594)    /* ln(1e13)  */
