@@ -181,6 +181,24 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
    * previous sub-step's temperature search ended on, whose value that search
    * computed last: reuse it (one McDonald pair per sub-step saved, exact) */
   double g_av_next = 0.0;
+  /* The temperature search steps Theta by x1.005 or /1.005 from the last
+   * sub-step's value, so successive sub-steps keep re-evaluating the same few
+   * arguments (T oscillating across the crossing). gamma_bar is a pure
+   * function of Theta: a 4-entry memo keyed on the exact bits returns the
+   * value it would recompute (bit-identical), skipping its McDonald pair. */
+  double memo_th[4] = {-1.0, -1.0, -1.0, -1.0}, memo_g[4] = {0.0, 0.0, 0.0, 0.0};
+  int memo_next = 0;
+  auto gamma_bar_m = [&](double th) -> double {
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (memo_th[q] == th) return memo_g[q];
+    const double g = gamma_bar_w(th, lane, P.mcd, guard, s_mcd);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (q == memo_next) { memo_th[q] = th; memo_g[q] = g; }
+    memo_next = (memo_next + 1) & 3;
+    return g;
+  };
 #ifdef C2D_FP_PROF
   long long pf_gb = 0, pf_tri = 0, pf_loop0 = clock64(), pf_t0, pf_calls = 0;
 #define PF_BEGIN() pf_t0 = clock64()
@@ -191,7 +209,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
 #endif
   for (;;) {
     /* label 200 (:577) */
-    double g_av = (fp_steps == 0) ? gamma_bar_w(Th_e, lane, P.mcd, guard, s_mcd) : g_av_next;
+    double g_av = (fp_steps == 0) ? gamma_bar_m(Th_e) : g_av_next;
     /* hr_th_c = hr_th_c - x_i, i.e. + (-x_i) bit for bit */
     const double hr_th_c = seq_sum(0.0, 1, NT - 1, lane, [&](int i) {
       return -(8.176e-7 * s_dgic[i] * s_fold[i] * (s_gnt[i + 1] - s_gnt[i]) * volume * n_lept);
@@ -482,7 +500,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
 #ifdef C2D_FP_PROF
         pf_calls++;
 #endif
-        g_av = gamma_bar_w(The_new, lane, P.mcd, guard, s_mcd);
+        g_av = gamma_bar_m(The_new);
         if (guard > GUARD_MAX) break;
       }
     } else {
@@ -491,7 +509,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
 #ifdef C2D_FP_PROF
         pf_calls++;
 #endif
-        g_av = gamma_bar_w(The_new, lane, P.mcd, guard, s_mcd);
+        g_av = gamma_bar_m(The_new);
         if (The_new < 1.0e-2) break;
         if (guard > GUARD_MAX) break;
       }
