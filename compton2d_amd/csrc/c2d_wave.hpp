@@ -84,7 +84,7 @@ __device__ inline double gammln(double xx) {
  * table the abscissa chain is replayed per lane from the last value.  Terms
  * are added in the reference's order up to each series' own stopping term,
  * so K2 and K3 equal two sequential McDonald calls bit for bit.  The terms of
- * a pass go through `scr` (LDS, 2*FPB doubles owned by this wave): every lane
+ * a pass go through `scr` (LDS, 4*FPB doubles owned by this wave): every lane
  * reads them back with broadcast loads that issue ahead of the add chain, so
  * the chain runs at the adds' latency (a readlane chain serialises on its
  * SGPR hazards: ~108 cycles per term against ~15). */
@@ -94,12 +94,84 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+/* One term of each series at n = n0 + lane from the abscissa table. */
+struct McdTerm {
+  double term2, term3, tn;
+  bool stop2, stop3;
+};
+__device__ __forceinline__ McdTerm mcd_term_tab(double z, int n, const double* __restrict__ tab) {
+  const double dt = 1.001, d = dt - 1.0;
+  const double* e = tab + (size_t)n * 4;
+  const double t = e[0], ts = e[1], p2 = e[2], p3 = e[3];
+  const double y = z * ts;
+  double sd2 = 0.0, sd3 = 0.0;
+  if (y < 2.25e2) {
+    const double ey = c2d_exp(y);
+    sd2 = p2 / ey;
+    sd3 = p3 / ey;
+  }
+  McdTerm r;
+  r.term2 = d * t * sd2;
+  r.term3 = d * t * sd3;
+  r.tn = t * dt;
+  r.stop2 = !(r.tn < 2.0 || sd2 > 1.0e-8);
+  r.stop3 = !(r.tn < 2.0 || sd3 > 1.0e-8);
+  return r;
+}
+
+/* Number of terms of a 64-term block that enter a running series: up to and
+ * including its first stopping term (0 once the series has stopped). */
+__device__ __forceinline__ int mcd_take(bool run, unsigned long long st) {
+  return run ? (st ? __ffsll((long long)st) : FPB) : 0;
+}
+
+/* `scr` holds 4*FPB doubles (LDS, owned by this wave).  While both 64-term
+ * blocks of a pass lie inside the abscissa table, each lane evaluates two
+ * terms (n and n+64): their exp/divide chains are independent, so one
+ * exposes its latency while the other issues (one wave per SIMD hides
+ * nothing else).  The sums still run in n order over exactly the terms the
+ * reference adds, so the result is unchanged bit for bit. */
 __device__ inline void mcdonald23_w(double z, int lane, const double* __restrict__ tab, double& K2,
                              double& K3, long long& guard, double* scr) {
-  const double dt = 1.001, d = dt - 1.0, s = 5.0e-1 * (1.0 + dt);
+  const double dt = 1.001, s = 5.0e-1 * (1.0 + dt);
   double sum2 = 0.0, sum3 = 0.0, t0 = 1.0;
   bool run2 = true, run3 = true;
-  for (int n0 = 0; run2 || run3; n0 += FPB) {
+  int n0 = 0;
+  while (run2 || run3) {
+    if (n0 + 2 * FPB <= C2D_FP_MCD_N) {
+      const McdTerm a = mcd_term_tab(z, n0 + lane, tab);
+      const McdTerm b = mcd_term_tab(z, n0 + FPB + lane, tab);
+      const unsigned long long sa2 = __ballot(a.stop2), sa3 = __ballot(a.stop3);
+      const unsigned long long sb2 = __ballot(b.stop2), sb3 = __ballot(b.stop3);
+      const int na2 = mcd_take(run2, sa2), na3 = mcd_take(run3, sa3);
+      const int nb2 = mcd_take(run2 && !sa2, sb2), nb3 = mcd_take(run3 && !sa3, sb3);
+      scr[lane] = a.term2;
+      scr[FPB + lane] = b.term2;
+      scr[2 * FPB + lane] = a.term3;
+      scr[3 * FPB + lane] = b.term3;
+      wave_sync();
+      const int n2 = na2 + nb2, n3 = na3 + nb3;
+      if (n2 == 2 * FPB && n3 == 2 * FPB) {
+#pragma unroll 16
+        for (int m = 0; m < 2 * FPB; m++) {
+          sum2 = sum2 + scr[m];
+          sum3 = sum3 + scr[2 * FPB + m];
+        }
+      } else {
+        for (int m = 0; m < n2; m++) sum2 = sum2 + scr[m];
+        for (int m = 0; m < n3; m++) sum3 = sum3 + scr[2 * FPB + m];
+      }
+      wave_sync();
+      if (sa2 || sb2) run2 = false;
+      if (sa3 || sb3) run3 = false;
+      guard += n2 > n3 ? n2 : n3;
+      if (guard > GUARD_MAX) break;
+      t0 = rl(b.tn, FPB - 1);
+      n0 += 2 * FPB;
+      continue;
+    }
+    /* single 64-term pass (tail of the table, then abscissae replayed per lane) */
+    const double d = dt - 1.0;
     const int n = n0 + lane;
     double t, ts, p2, p3;
     if (n0 + FPB <= C2D_FP_MCD_N) {
@@ -123,8 +195,8 @@ __device__ inline void mcdonald23_w(double z, int lane, const double* __restrict
     const double tn = t * dt;
     const unsigned long long st2 = __ballot(!(tn < 2.0 || sd2 > 1.0e-8));
     const unsigned long long st3 = __ballot(!(tn < 2.0 || sd3 > 1.0e-8));
-    const int n2 = run2 ? (st2 ? __ffsll((long long)st2) : FPB) : 0;
-    const int n3 = run3 ? (st3 ? __ffsll((long long)st3) : FPB) : 0;
+    const int n2 = mcd_take(run2, st2);
+    const int n3 = mcd_take(run3, st3);
     const int nm = n2 > n3 ? n2 : n3;
     scr[lane] = term2;
     scr[FPB + lane] = term3;
@@ -145,6 +217,7 @@ __device__ inline void mcdonald23_w(double z, int lane, const double* __restrict
     guard += nm;
     if (guard > GUARD_MAX) break;
     t0 = rl(tn, FPB - 1);
+    n0 += FPB;
   }
   K2 = __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, 2.0) * sum2 / c2d_exp(gammln(5.0e-1 + 2.0));
   K3 = __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, 3.0) * sum3 / c2d_exp(gammln(5.0e-1 + 3.0));

@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
   __shared__ double s_gnt[NT + 2], s_gam[NT + 2], s_fold[NT + 2], s_fnew[NT + 2];
   __shared__ double s_dgic[NT + 2], s_dgdt[NT + 2], s_disp[NT + 2];
   __shared__ double s_a[NT + 2], s_b[NT + 2], s_c[NT + 2];
-  __shared__ double s_mcd[2 * FPB];   /* McDonald term exchange (c2d_wave.hpp) */
+  __shared__ double s_mcd[4 * FPB];   /* McDonald term exchange (c2d_wave.hpp) */
   __shared__ double s_smw[NT + 2], s_bigW[NT + 2], s_bigC[NT + 2], s_em[NT + 2], s_inj[NT + 2];
   __shared__ double s_Pnt[NT + 2], s_nf[NPH];
 

@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(64) c2d_selftest_mcd_kernel(const double* z, c
   const int i = blockIdx.x;
   if (i >= n) return;
   const int lane = threadIdx.x;
-  __shared__ double scr[2 * wave::FPB];
+  __shared__ double scr[4 * wave::FPB];
   long long guard = 0;
   double K2, K3;
   const long long t0 = clock64();

@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(VEM_BLOCK) c2d_vem_kernel(const VemParams P) {
   __shared__ double s_gnt[NT], s_f[NT], s_q[NT], s_gamp[NT], s_facg[NT], s_dg[NT];
   __shared__ double s_cP[NV], s_cC[NV], s_cT[NV], s_P[NV], s_Pth[NV];
   __shared__ double s_sc[8];   /* B, K2, f_rz, P_sum, sum_th, Eloss_cy, Eloss_th, Eloss_sy */
-  __shared__ double s_mcd[2 * FPB];   /* McDonald term exchange (wave 0) */
+  __shared__ double s_mcd[4 * FPB];   /* McDonald term exchange (wave 0) */
   const int cell = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const double* zin = P.zin + (int64_t)cell * VZ_N;
