@@ -1,4 +1,7 @@
-import sys; sys.path[:0]=['.','tests']
+import sys
+from pathlib import Path
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / 'tests')]
 import numpy as np
 from compton2d_amd.engine import device_mcdonald
 z = np.array([0.5, 1.0, 2.0, 5.0, 10.0, 20.0, 50.0])
