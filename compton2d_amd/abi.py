@@ -33,7 +33,7 @@ CNT_STEPS, CNT_ESCAPES, CNT_CENSUS, CNT_COLLIDE, CNT_KILLED, CNT_SOURCES, \
 ERRORS = {
     0: "C2D_OK", -1: "C2D_E_ARG", -2: "C2D_E_HIP", -3: "C2D_E_CENSUS_OVERFLOW",
     -4: "C2D_E_EVENT_OVERFLOW", -5: "C2D_E_QUEUE_OVERFLOW", -6: "C2D_E_NOMEM",
-    -7: "C2D_E_STATE",
+    -7: "C2D_E_STATE", -9: "C2D_E_RCCL",
 }
 
 PD = C.POINTER(C.c_double)
@@ -84,7 +84,12 @@ class StepIn(C.Structure):
         ("tbbi", PD), ("tbbo", PD), ("tbbu", PD), ("tbbl", PD),
         ("spec_i", PI32), ("spec_o", PI32), ("spec_u", PI32), ("spec_l", PI32),
         ("n_spectra", C.c_int32), ("spectra", C.POINTER(Spectrum)),
+        ("device_tables", C.c_int32),
     ]
+
+COMM_ID_BYTES = 128          # C2D_COMM_ID_BYTES
+# c2d_step_in.device_tables (include/compton2d.h)
+DEV_EMISSION, DEV_ELECTRONS = 1, 2
 
 
 class TallyLayout(C.Structure):
@@ -206,16 +211,18 @@ class StepInputs:
 
     Dense C-order layouts: kappa_tot/eps_tot/eps_th [nz,nr,N_VOL],
     f_nt/Pnt [nz,nr,NUM_NT], zone scalars [nz,nr], z-surface arrays [nz],
-    r-surface arrays [nr].
+    r-surface arrays [nr].  kappa_tot/eps_tot/eps_th = None: the tables of
+    the context's last volume_em (C2D_DEV_EMISSION); f_nt/Pnt = None: the
+    context's device electron state (C2D_DEV_ELECTRONS).
     """
     ncycle: int
     time: float
     dt: float
-    kappa_tot: np.ndarray
-    eps_tot: np.ndarray
-    eps_th: np.ndarray
-    f_nt: np.ndarray
-    Pnt: np.ndarray
+    kappa_tot: Optional[np.ndarray]
+    eps_tot: Optional[np.ndarray]
+    eps_th: Optional[np.ndarray]
+    f_nt: Optional[np.ndarray]
+    Pnt: Optional[np.ndarray]
     n_e: np.ndarray
     Eloss_th: np.ndarray
     Eloss_tot: np.ndarray
@@ -269,11 +276,22 @@ class StepInputs:
         s.ncycle = int(self.ncycle)
         s.time = float(self.time)
         s.dt = float(self.dt)
-        s.kappa_tot = a3(self.kappa_tot, N_VOL)
-        s.eps_tot = a3(self.eps_tot, N_VOL)
-        s.eps_th = a3(self.eps_th, N_VOL)
-        s.f_nt = a3(self.f_nt, NUM_NT)
-        s.Pnt = a3(self.Pnt, NUM_NT)
+        dev = 0
+        em = (self.kappa_tot, self.eps_tot, self.eps_th)
+        if all(x is None for x in em):
+            dev |= DEV_EMISSION
+            s.kappa_tot = s.eps_tot = s.eps_th = Array3(None, 0, 0, 0)
+        else:
+            s.kappa_tot = a3(self.kappa_tot, N_VOL)
+            s.eps_tot = a3(self.eps_tot, N_VOL)
+            s.eps_th = a3(self.eps_th, N_VOL)
+        if self.f_nt is None and self.Pnt is None:
+            dev |= DEV_ELECTRONS
+            s.f_nt = s.Pnt = Array3(None, 0, 0, 0)
+        else:
+            s.f_nt = a3(self.f_nt, NUM_NT)
+            s.Pnt = a3(self.Pnt, NUM_NT)
+        s.device_tables = dev
         s.n_e = a2(self.n_e)
         s.Eloss_th = a2(self.Eloss_th)
         s.Eloss_tot = a2(self.Eloss_tot)
@@ -443,13 +461,16 @@ class FpCall:
             assert nf.shape == (nz, nr, NPHFIELD)
             keep.append(nf)
             s.n_field = Array3(_pd(nf), 1, nr * NPHFIELD, NPHFIELD)
-        self.st = {k: np.array(state[k], dtype=np.float64, copy=True) for k in
-                   ("f_nt", "Pnt") + FP_STATE_KEYS}
+        # f_nt/Pnt absent or None: the context's device electron state (C2D_DEV_ELECTRONS)
+        self.device_electrons = state.get("f_nt") is None and state.get("Pnt") is None
+        el = () if self.device_electrons else ("f_nt", "Pnt")
+        self.st = {k: np.array(state[k], dtype=np.float64, copy=True) for k in el + FP_STATE_KEYS}
         self.st["Te_new"] = np.zeros((nz, nr))
         self.diag = np.zeros((nz, nr, FP_NDIAG))
         o = FpStepOut()
         for k in ("f_nt", "Pnt"):
-            setattr(o, k, MArray3(_pd(self.st[k]), 1, nr * NUM_NT, NUM_NT))
+            setattr(o, k, MArray3(_pd(self.st[k]), 1, nr * NUM_NT, NUM_NT) if k in self.st
+                    else MArray3(None, 0, 0, 0))
         for k in FP_STATE_KEYS + ("Te_new",):
             setattr(o, k, MArray2(_pd(self.st[k]), nr, 1))
         o.zone_diag = _pd(self.diag)
@@ -502,9 +523,13 @@ class VemCall:
     f_nt [nz, nr, NUM_NT], ep_switch [nz, nr] (int, optional); outputs
     kappa_tot/eps_tot/eps_th [nz, nr, N_VOL] and the per-cell scalars."""
 
-    def __init__(self, dt: float, state: dict):
-        f = np.ascontiguousarray(state["f_nt"], np.float64)
-        nz, nr = f.shape[:2]
+    def __init__(self, dt: float, state: dict, tables_to_host: bool = True):
+        """state['f_nt'] = None reads the context's device electron state;
+        tables_to_host = False leaves kappa_tot/eps_tot/eps_th on the device
+        only (for a following set_step with C2D_DEV_EMISSION)."""
+        f = state.get("f_nt")
+        f = None if f is None else np.ascontiguousarray(f, np.float64)
+        nz, nr = np.asarray(state["tea"]).shape
         self.keep = []
 
         def a2(key, dflt=0.0):
@@ -516,14 +541,17 @@ class VemCall:
         ep = state.get("ep_switch")
         ep = np.ascontiguousarray(np.zeros((nz, nr)) if ep is None else ep, np.int32)
         self.keep += [f, ep]
+        fv = (Array3(None, 0, 0, 0) if f is None else
+              Array3(f.ctypes.data_as(PD), 1, nr * NUM_NT, NUM_NT))
         self.sin = VemIn(float(dt), *(a2(k) for k in VEM_STATE_KEYS),
-                         IArray2(ep.ctypes.data_as(PI32), nr, 1),
-                         Array3(f.ctypes.data_as(PD), 1, nr * NUM_NT, NUM_NT))
-        self.res = {k: np.zeros((nz, nr, N_VOL)) for k in ("kappa_tot", "eps_tot", "eps_th")}
+                         IArray2(ep.ctypes.data_as(PI32), nr, 1), fv)
+        tabs = ("kappa_tot", "eps_tot", "eps_th")
+        self.res = {k: np.zeros((nz, nr, N_VOL)) for k in tabs} if tables_to_host else {}
         for k in ("B_field", "Eloss_sy", "Eloss_cy", "Eloss_th", "Eloss_tot"):
             self.res[k] = np.zeros((nz, nr))
         self.res["E_ph"] = np.zeros(N_VOL)
         r = self.res
-        m3 = [MArray3(r[k].ctypes.data_as(PD), 1, nr * N_VOL, N_VOL) for k in ("kappa_tot", "eps_tot", "eps_th")]
+        m3 = [MArray3(r[k].ctypes.data_as(PD), 1, nr * N_VOL, N_VOL) if k in r else MArray3(None, 0, 0, 0)
+              for k in tabs]
         m2 = [MArray2(r[k].ctypes.data_as(PD), nr, 1) for k in ("B_field", "Eloss_sy", "Eloss_cy", "Eloss_th", "Eloss_tot")]
         self.sout = VemOut(*m3, *m2, r["E_ph"].ctypes.data_as(PD))

@@ -5,6 +5,7 @@
  * tiny per-step prefix sums, and the generation loop.
  */
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -130,6 +131,12 @@ struct c2d_ctx {
   /* host state of the current step */
   KParams P;
   bool have_step = false;
+  bool have_electrons = false;  /* f_nt/Pnt hold an electron state (C2D_DEV_ELECTRONS) */
+  bool have_vem = false;        /* vem_* hold the last c2d_volume_em tables (C2D_DEV_EMISSION) */
+  int32_t* mono_flag = nullptr;
+  /* RCCL communicator of the tally all-reduce (c2d_comm_init) */
+  ncclComm_t comm = nullptr;
+  int comm_rank = 0, comm_world = 1;
   int64_t n_vol_global = 0, n_surf_global = 0;
   int eps_linear = 0;
   std::vector<double> h_stage;
@@ -302,6 +309,8 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->mono_flag) (void)hipFree(c->mono_flag);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
   void* ptrs[] = {c->geo, c->gnt, c->kappa_cur, c->kappa_prev, c->eps_tot, c->eps_th, c->f_nt,
                   c->Pnt, c->n_e, c->vfrac, c->ewsv, c->surf_ew, c->surf_tbb, c->tbbl,
                   c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comS,
@@ -365,32 +374,72 @@ extern "C" int c2d_set_clock(c2d_ctx* c, int32_t ncycle, double time, double dt)
   return C2D_OK;
 }
 
+/* flag = 1 if some row of a [rows][n] table is not non-decreasing (or NaN):
+ * the emission CDFs are then searched linearly, as the reference does */
+__global__ void __launch_bounds__(256) c2d_check_monotone(const double* __restrict__ a, int rows, int n,
+                                                          int32_t* __restrict__ flag) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < (int64_t)rows * n;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % n);
+    if (i > 0 && !(a[t] >= a[t - 1])) atomicOr(flag, 1);
+  }
+}
+
 extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
   if (!c || !in) return C2D_E_ARG;
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const int nz = c->nz, nr = c->nr, nc = c->ncell;
   const size_t nvol = (size_t)nc * C2D_N_VOL, nnt = (size_t)nc * C2D_NUM_NT;
-  std::vector<double>& h = c->h_stage;
-  h.resize(nvol);
-  gather3(c, in->kappa_tot, C2D_N_VOL, h.data());
-  HIPCHK(c, hipMemcpy(c->kappa_cur, h.data(), nvol * sizeof(double), hipMemcpyHostToDevice));
-  gather3(c, in->eps_tot, C2D_N_VOL, h.data());
-  int nonmono = 0;
-  for (int cc = 0; cc < nc && !nonmono; cc++)
-    for (int i = 1; i < C2D_N_VOL; i++)
-      if (!(h[(size_t)cc * C2D_N_VOL + i] >= h[(size_t)cc * C2D_N_VOL + i - 1])) { nonmono = 1; break; }
-  HIPCHK(c, hipMemcpy(c->eps_tot, h.data(), nvol * sizeof(double), hipMemcpyHostToDevice));
-  gather3(c, in->eps_th, C2D_N_VOL, h.data());
-  for (int cc = 0; cc < nc && !nonmono; cc++)
-    for (int i = 1; i < C2D_N_VOL; i++)
-      if (!(h[(size_t)cc * C2D_N_VOL + i] >= h[(size_t)cc * C2D_N_VOL + i - 1])) { nonmono = 1; break; }
-  HIPCHK(c, hipMemcpy(c->eps_th, h.data(), nvol * sizeof(double), hipMemcpyHostToDevice));
-  c->eps_linear = nonmono;
-  std::vector<double> hn(nnt);
-  gather3(c, in->f_nt, C2D_NUM_NT, hn.data());
-  HIPCHK(c, hipMemcpy(c->f_nt, hn.data(), nnt * sizeof(double), hipMemcpyHostToDevice));
-  gather3(c, in->Pnt, C2D_NUM_NT, hn.data());
-  HIPCHK(c, hipMemcpy(c->Pnt, hn.data(), nnt * sizeof(double), hipMemcpyHostToDevice));
+  const int dev = in->device_tables;
+  if (dev & ~(C2D_DEV_EMISSION | C2D_DEV_ELECTRONS))
+    return fail(c, C2D_E_ARG, "c2d_set_step: unknown device_tables flags 0x%x", dev);
+  if ((dev & C2D_DEV_EMISSION) && !c->have_vem)
+    return fail(c, C2D_E_STATE, "C2D_DEV_EMISSION needs a preceding c2d_volume_em");
+  if ((dev & C2D_DEV_ELECTRONS) && !c->have_electrons)
+    return fail(c, C2D_E_STATE, "C2D_DEV_ELECTRONS needs an electron state on the device");
+  if (dev & C2D_DEV_EMISSION) {
+    const hipStream_t st = c->stream;
+    HIPCHK(c, hipMemcpyAsync(c->kappa_cur, c->vem_kap, nvol * sizeof(double), hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->eps_tot, c->vem_et, nvol * sizeof(double), hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->eps_th, c->vem_eh, nvol * sizeof(double), hipMemcpyDeviceToDevice, st));
+    if (!c->mono_flag) HIPCHK(c, dalloc(&c->mono_flag, 1));
+    HIPCHK(c, hipMemsetAsync(c->mono_flag, 0, sizeof(int32_t), st));
+    const int grid = (int)std::min<int64_t>(((int64_t)nvol + 255) / 256, (int64_t)c->n_cu * 4);
+    hipLaunchKernelGGL(c2d_check_monotone, dim3(grid), dim3(256), 0, st, c->eps_tot, nc, C2D_N_VOL,
+                       c->mono_flag);
+    hipLaunchKernelGGL(c2d_check_monotone, dim3(grid), dim3(256), 0, st, c->eps_th, nc, C2D_N_VOL,
+                       c->mono_flag);
+    HIPCHK(c, hipGetLastError());
+    int32_t nonmono = 0;
+    HIPCHK(c, hipMemcpyAsync(&nonmono, c->mono_flag, sizeof nonmono, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    c->eps_linear = nonmono;
+  } else {
+    std::vector<double>& h = c->h_stage;
+    h.resize(nvol);
+    gather3(c, in->kappa_tot, C2D_N_VOL, h.data());
+    HIPCHK(c, hipMemcpy(c->kappa_cur, h.data(), nvol * sizeof(double), hipMemcpyHostToDevice));
+    gather3(c, in->eps_tot, C2D_N_VOL, h.data());
+    int nonmono = 0;
+    for (int cc = 0; cc < nc && !nonmono; cc++)
+      for (int i = 1; i < C2D_N_VOL; i++)
+        if (!(h[(size_t)cc * C2D_N_VOL + i] >= h[(size_t)cc * C2D_N_VOL + i - 1])) { nonmono = 1; break; }
+    HIPCHK(c, hipMemcpy(c->eps_tot, h.data(), nvol * sizeof(double), hipMemcpyHostToDevice));
+    gather3(c, in->eps_th, C2D_N_VOL, h.data());
+    for (int cc = 0; cc < nc && !nonmono; cc++)
+      for (int i = 1; i < C2D_N_VOL; i++)
+        if (!(h[(size_t)cc * C2D_N_VOL + i] >= h[(size_t)cc * C2D_N_VOL + i - 1])) { nonmono = 1; break; }
+    HIPCHK(c, hipMemcpy(c->eps_th, h.data(), nvol * sizeof(double), hipMemcpyHostToDevice));
+    c->eps_linear = nonmono;
+  }
+  if (!(dev & C2D_DEV_ELECTRONS)) {
+    std::vector<double> hn(nnt);
+    gather3(c, in->f_nt, C2D_NUM_NT, hn.data());
+    HIPCHK(c, hipMemcpy(c->f_nt, hn.data(), nnt * sizeof(double), hipMemcpyHostToDevice));
+    gather3(c, in->Pnt, C2D_NUM_NT, hn.data());
+    HIPCHK(c, hipMemcpy(c->Pnt, hn.data(), nnt * sizeof(double), hipMemcpyHostToDevice));
+    c->have_electrons = true;
+  }
 
   /* zone scalars, volume fractions (imcvol2d_para.f:119-149), volume prefix */
   std::vector<double> ne(nc), ew(nc), vf(4 * (size_t)nc);
@@ -777,6 +826,44 @@ extern "C" int c2d_census_count(c2d_ctx* c, int64_t* n) {
   return C2D_OK;
 }
 
+/* strided column copy device -> host (stride 1: one contiguous copy) */
+template <class T>
+static hipError_t col_down(T* dst, const T* src, int64_t first, int64_t stride, int64_t m) {
+  if (stride == 1) return hipMemcpy(dst, src + first, m * sizeof(T), hipMemcpyDeviceToHost);
+  return hipMemcpy2D(dst, sizeof(T), src + first, stride * sizeof(T), sizeof(T), m,
+                     hipMemcpyDeviceToHost);
+}
+
+extern "C" int c2d_census_export_range(c2d_ctx* c, int64_t first, int64_t stride, double* d6,
+                                       int32_t* i5, uint64_t* keys, int64_t cap, int64_t* n) {
+  if (!c || !n || first < 0 || stride < 1) return C2D_E_ARG;
+  const int64_t avail = first < c->n_census ? (c->n_census - first + stride - 1) / stride : 0;
+  *n = avail;
+  const int64_t m = std::min(cap, avail);
+  if (m <= 0) return C2D_OK;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const DevCensus& d = c->cens[c->cur_out];
+  std::vector<double> col(m);
+  for (int f = 0; f < 6; f++) {
+    HIPCHK(c, col_down(col.data(), d.d[f], first, stride, m));
+    if (d6)
+      for (int64_t i = 0; i < m; i++) d6[6 * i + f] = col[i];
+  }
+  std::vector<uint32_t> jk(m), bins(m);
+  HIPCHK(c, col_down(jk.data(), d.jk, first, stride, m));
+  HIPCHK(c, col_down(bins.data(), d.bins, first, stride, m));
+  if (i5)
+    for (int64_t i = 0; i < m; i++) {
+      i5[5 * i + 0] = (int32_t)(bins[i] & 0xff);
+      i5[5 * i + 1] = (int32_t)((bins[i] >> 8) & 0xff);
+      i5[5 * i + 2] = (int32_t)((bins[i] >> 16) & 0xff);
+      i5[5 * i + 3] = (int32_t)(jk[i] >> 16);
+      i5[5 * i + 4] = (int32_t)(jk[i] & 0xffff);
+    }
+  if (keys) HIPCHK(c, col_down(keys, d.key, first, stride, m));
+  return C2D_OK;
+}
+
 extern "C" int c2d_census_export(c2d_ctx* c, double* d6, int32_t* i5, uint64_t* keys, int64_t cap,
                                  int64_t* n) {
   if (!c || !n) return C2D_E_ARG;
@@ -935,8 +1022,11 @@ extern "C" int c2d_fp_set_config(c2d_ctx* c, const c2d_fp_config* fc) {
 extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out* out) {
   if (!c || !in || !out) return C2D_E_ARG;
   if (!c->fp_ready) return fail(c, C2D_E_STATE, "c2d_fp_set_config must precede c2d_fp_step");
-  if (!out->f_nt.data || !out->Pnt.data)
-    return fail(c, C2D_E_ARG, "c2d_fp_step: f_nt and Pnt (in/out) are required");
+  const bool el_dev = !out->f_nt.data && !out->Pnt.data;   /* C2D_DEV_ELECTRONS */
+  if (!el_dev && (!out->f_nt.data || !out->Pnt.data))
+    return fail(c, C2D_E_ARG, "c2d_fp_step: pass both f_nt and Pnt views, or neither (device state)");
+  if (el_dev && !c->have_electrons)
+    return fail(c, C2D_E_STATE, "c2d_fp_step: no electron state on the device (c2d_set_step first)");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const int nz = c->nz, nr = c->nr, nc = c->ncell;
   const bool nf_dev = in->n_field.data == nullptr, ecens_dev = in->ecens.data == nullptr;
@@ -946,8 +1036,9 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   auto m2 = [](const c2d_marray2& a, int j, int k) -> double* {
     return a.data ? &a.data[j * a.s_j + k * a.s_k] : nullptr;
   };
-  std::vector<double> zin((size_t)nc * FZ_N, 0.0), fin((size_t)nc * C2D_NUM_NT),
-      pin((size_t)nc * C2D_NUM_NT), nf(nf_dev ? 0 : (size_t)nc * C2D_NPHFIELD);
+  const size_t nnt = el_dev ? 0 : (size_t)nc * C2D_NUM_NT;
+  std::vector<double> zin((size_t)nc * FZ_N, 0.0), fin(nnt), pin(nnt),
+      nf(nf_dev ? 0 : (size_t)nc * C2D_NPHFIELD);
   for (int j = 0; j < nz; j++)
     for (int k = 0; k < nr; k++) {
       const int cell = j * nr + k;
@@ -968,7 +1059,7 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
                     j + 1, k + 1, z[FZ_FPAIR]);
       const double* pp = m2(out->p_nth, j, k);
       z[FZ_PNTH] = pp ? *pp : 0.0;
-      for (int i = 0; i < C2D_NUM_NT; i++) {
+      for (int i = 0; i < C2D_NUM_NT && !el_dev; i++) {
         fin[(size_t)cell * C2D_NUM_NT + i] =
             out->f_nt.data[i * out->f_nt.s_i + j * out->f_nt.s_j + k * out->f_nt.s_k];
         pin[(size_t)cell * C2D_NUM_NT + i] =
@@ -981,8 +1072,10 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
     }
   const hipStream_t st = c->stream;
   HIPCHK(c, hipMemcpyAsync(c->fp_zin, zin.data(), zin.size() * sizeof(double), hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(c->fp_fin, fin.data(), fin.size() * sizeof(double), hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(c->fp_Pin, pin.data(), pin.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  if (!el_dev) {
+    HIPCHK(c, hipMemcpyAsync(c->fp_fin, fin.data(), fin.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->fp_Pin, pin.data(), pin.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  }
   if (!nf_dev)
     HIPCHK(c, hipMemcpyAsync(c->fp_nf, nf.data(), nf.size() * sizeof(double), hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemsetAsync(c->fp_err, 0, sizeof(int32_t), st));
@@ -997,21 +1090,28 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   P.flare_amp = f.flare_amp; P.inj_g1 = f.inj_g1; P.inj_g2 = f.inj_g2; P.inj_p = f.inj_p;
   P.inj_t = f.inj_t; P.inj_L = f.inj_L; P.pick_rate = f.pick_rate; P.inj_gg = f.inj_gg;
   P.inj_sigma = f.inj_sigma; P.inj_v = f.inj_v;
-  P.geo = c->geo; P.gnt = c->gnt; P.FT = c->fp_FT; P.mcd = c->fp_mcd; P.zin = c->fp_zin; P.f_in = c->fp_fin;
-  P.P_in = c->fp_Pin;
+  P.geo = c->geo; P.gnt = c->gnt; P.FT = c->fp_FT; P.mcd = c->fp_mcd; P.zin = c->fp_zin;
+  /* device electron state: updated in place (each zone's workgroup reads its
+   * row into LDS before it writes the row back) */
+  P.f_in = el_dev ? c->f_nt : c->fp_fin;
+  P.P_in = el_dev ? c->Pnt : c->fp_Pin;
   P.nf = nf_dev ? c->T + c->L.n_field : c->fp_nf;    /* tally layout: [cell][nphfield] */
   P.ecens = ecens_dev ? c->T + c->L.ecens : nullptr;
-  P.f_out = c->fp_fout; P.P_out = c->fp_Pout; P.zout = c->fp_zout; P.err = c->fp_err;
+  P.f_out = el_dev ? c->f_nt : c->fp_fout;
+  P.P_out = el_dev ? c->Pnt : c->fp_Pout;
+  P.zout = c->fp_zout; P.err = c->fp_err;
   HIPCHK(c, hipEventRecord(c->ev_g0a, st));
   int rc = c2d_launch_fp(&P, nc, st);
   if (rc) return fail(c, C2D_E_HIP, "fp launch: %s", hipGetErrorString((hipError_t)rc));
   HIPCHK(c, hipEventRecord(c->ev_g0b, st));
-  std::vector<double> zout((size_t)nc * FO_N), fout((size_t)nc * C2D_NUM_NT), pout((size_t)nc * C2D_NUM_NT);
+  std::vector<double> zout((size_t)nc * FO_N), fout(nnt), pout(nnt);
   std::vector<double> ecd(ecens_dev ? nc : 0);
   int32_t herr = 0;
   HIPCHK(c, hipMemcpyAsync(zout.data(), c->fp_zout, zout.size() * sizeof(double), hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(fout.data(), c->fp_fout, fout.size() * sizeof(double), hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(pout.data(), c->fp_Pout, pout.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  if (!el_dev) {
+    HIPCHK(c, hipMemcpyAsync(fout.data(), c->fp_fout, fout.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(pout.data(), c->fp_Pout, pout.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  }
   HIPCHK(c, hipMemcpyAsync(&herr, c->fp_err, sizeof herr, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   (void)hipEventElapsedTime(&c->last_fp_ms, c->ev_g0a, c->ev_g0b);
@@ -1029,7 +1129,7 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
       double* p;
       if ((p = m2(out->Te_new, j, k))) *p = zo[FO_TE];
       if (dg[C2D_FP_SKIPPED] == 0.0) {
-        for (int i = 0; i < C2D_NUM_NT; i++) {
+        for (int i = 0; i < C2D_NUM_NT && !el_dev; i++) {
           out->f_nt.data[i * out->f_nt.s_i + j * out->f_nt.s_j + k * out->f_nt.s_k] =
               fout[(size_t)cell * C2D_NUM_NT + i];
           out->Pnt.data[i * out->Pnt.s_i + j * out->Pnt.s_j + k * out->Pnt.s_k] =
@@ -1063,6 +1163,26 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   return C2D_OK;
 }
 
+extern "C" int c2d_electron_state(c2d_ctx* c, c2d_marray3 f_nt, c2d_marray3 Pnt) {
+  if (!c) return C2D_E_ARG;
+  if (!c->have_electrons) return fail(c, C2D_E_STATE, "c2d_electron_state: no electron state yet");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const size_t nnt = (size_t)c->ncell * C2D_NUM_NT;
+  std::vector<double> h(nnt);
+  const c2d_marray3* views[2] = {&f_nt, &Pnt};
+  const double* src[2] = {c->f_nt, c->Pnt};
+  for (int v = 0; v < 2; v++) {
+    const c2d_marray3& m = *views[v];
+    if (!m.data) continue;
+    HIPCHK(c, hipMemcpy(h.data(), src[v], nnt * sizeof(double), hipMemcpyDeviceToHost));
+    for (int j = 0; j < c->nz; j++)
+      for (int k = 0; k < c->nr; k++)
+        for (int i = 0; i < C2D_NUM_NT; i++)
+          m.data[i * m.s_i + j * m.s_j + k * m.s_k] = h[((size_t)j * c->nr + k) * C2D_NUM_NT + i];
+  }
+  return C2D_OK;
+}
+
 extern "C" int c2d_last_fp_ms(c2d_ctx* c, double* ms) {
   if (!c || !ms) return C2D_E_ARG;
   *ms = c->last_fp_ms;
@@ -1075,8 +1195,11 @@ extern "C" int c2d_last_fp_ms(c2d_ctx* c, double* ms) {
 extern "C" int c2d_volume_em(c2d_ctx* c, const c2d_vem_in* in, c2d_vem_out* out) {
   if (!c || !in || !out) return C2D_E_ARG;
   if (!in->tea.data || !in->tna.data || !in->n_e.data || !in->B_field.data || !in->f_pair.data ||
-      !in->zsurf.data || !in->vol.data || !in->f_nt.data)
+      !in->zsurf.data || !in->vol.data)
     return fail(c, C2D_E_ARG, "c2d_volume_em: missing input array");
+  const bool el_dev = !in->f_nt.data;
+  if (el_dev && !c->have_electrons)
+    return fail(c, C2D_E_STATE, "c2d_volume_em: f_nt NULL but no electron state on the device");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const int nz = c->nz, nr = c->nr;
   const size_t nc = (size_t)c->ncell;
@@ -1119,28 +1242,35 @@ extern "C" int c2d_volume_em(c2d_ctx* c, const c2d_vem_in* in, c2d_vem_out* out)
       const double dz = (j == 0) ? c->cfg.z[0] : c->cfg.z[j] - c->cfg.z[j - 1];
       const double drr = (k == 0) ? c->cfg.r[0] - c->cfg.rmin : c->cfg.r[k] - c->cfg.r[k - 1];
       z[VZ_LMIN] = (dz < drr) ? dz : drr;
-      for (int i = 0; i < C2D_NUM_NT; i++)
+      for (int i = 0; i < C2D_NUM_NT && !el_dev; i++)
         fnt[cell * C2D_NUM_NT + i] = in->f_nt.data[i * in->f_nt.s_i + j * in->f_nt.s_j + k * in->f_nt.s_k];
     }
   const hipStream_t st = c->stream;
   HIPCHK(c, hipMemcpyAsync(c->vem_zin, zin.data(), zin.size() * sizeof(double), hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(c->vem_fnt, fnt.data(), fnt.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  if (!el_dev)
+    HIPCHK(c, hipMemcpyAsync(c->vem_fnt, fnt.data(), fnt.size() * sizeof(double), hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemcpyAsync(c->vem_eph, eph.data(), eph.size() * sizeof(double), hipMemcpyHostToDevice, st));
   VemParams P;
-  P.zin = c->vem_zin; P.f_nt = c->vem_fnt; P.gnt = c->gnt; P.E_ph = c->vem_eph; P.mcd = c->fp_mcd;
+  P.zin = c->vem_zin; P.f_nt = el_dev ? c->f_nt : c->vem_fnt; P.gnt = c->gnt; P.E_ph = c->vem_eph; P.mcd = c->fp_mcd;
   P.dE = dE; P.pow3_15 = c2d_pow(3.0, 1.5); P.dt = in->dt;
   P.kappa = c->vem_kap; P.eps_tot = c->vem_et; P.eps_th = c->vem_eh; P.zout = c->vem_zout;
   HIPCHK(c, hipEventRecord(c->ev_g0a, st));
   int rc = c2d_launch_vem(&P, (int)nc, st);
   if (rc) return fail(c, C2D_E_HIP, "vem launch: %s", hipGetErrorString((hipError_t)rc));
   HIPCHK(c, hipEventRecord(c->ev_g0b, st));
-  std::vector<double> kap(nc * C2D_N_VOL), et(nc * C2D_N_VOL), eh(nc * C2D_N_VOL), zo(nc * VO_N);
-  HIPCHK(c, hipMemcpyAsync(kap.data(), c->vem_kap, kap.size() * sizeof(double), hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(et.data(), c->vem_et, et.size() * sizeof(double), hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(eh.data(), c->vem_eh, eh.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  /* tables cross to the host only for the output views that are present */
+  std::vector<double> kap(out->kappa_tot.data ? nc * C2D_N_VOL : 0),
+      et(out->eps_tot.data ? nc * C2D_N_VOL : 0), eh(out->eps_th.data ? nc * C2D_N_VOL : 0), zo(nc * VO_N);
+  if (!kap.empty())
+    HIPCHK(c, hipMemcpyAsync(kap.data(), c->vem_kap, kap.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  if (!et.empty())
+    HIPCHK(c, hipMemcpyAsync(et.data(), c->vem_et, et.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  if (!eh.empty())
+    HIPCHK(c, hipMemcpyAsync(eh.data(), c->vem_eh, eh.size() * sizeof(double), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipMemcpyAsync(zo.data(), c->vem_zout, zo.size() * sizeof(double), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   (void)hipEventElapsedTime(&c->last_vem_ms, c->ev_g0a, c->ev_g0b);
+  c->have_vem = true;
   if (out->E_ph) std::copy(eph.begin(), eph.end(), out->E_ph);
   auto put3 = [&](c2d_marray3& m, const std::vector<double>& v, size_t cell, int j, int k) {
     if (!m.data) return;
@@ -1287,5 +1417,46 @@ extern "C" int c2d_obs_result(c2d_ctx* c, double* F, double* F2, double* count, 
   if (F2) HIPCHK(c, hipMemcpy(F2, c->obs.F2, nh * sizeof(double), hipMemcpyDeviceToHost));
   if (count) HIPCHK(c, hipMemcpy(count, c->obs.cnt, nh * sizeof(double), hipMemcpyDeviceToHost));
   if (kernel_ms) *kernel_ms = c->obs_ms;
+  return C2D_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* RCCL tally all-reduce (xec_add/graphics_collect, src/xec2d.f:325-399; */
+/* cens_add_up/E_add_up, src/update2d.f:1929-2078)                      */
+/* ------------------------------------------------------------------ */
+static_assert(sizeof(ncclUniqueId) == C2D_COMM_ID_BYTES, "RCCL unique id size");
+
+extern "C" int c2d_comm_unique_id(void* id, int64_t cap) {
+  if (!id || cap < C2D_COMM_ID_BYTES) return C2D_E_ARG;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return C2D_E_RCCL;
+  memcpy(id, &u, sizeof u);
+  return C2D_OK;
+}
+
+extern "C" int c2d_comm_init(c2d_ctx* c, const void* id, int32_t rank, int32_t world) {
+  if (!c || !id || world < 1 || rank < 0 || rank >= world) return C2D_E_ARG;
+  if (c->comm) return fail(c, C2D_E_STATE, "c2d_comm_init: the context already has a communicator");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  ncclComm_t comm = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&comm, world, u, rank);
+  if (r != ncclSuccess)
+    return fail(c, C2D_E_RCCL, "ncclCommInitRank(rank %d of %d): %s", rank, world, ncclGetErrorString(r));
+  c->comm = comm;
+  c->comm_rank = rank;
+  c->comm_world = world;
+  return C2D_OK;
+}
+
+extern "C" int c2d_allreduce_tallies(c2d_ctx* c) {
+  if (!c) return C2D_E_ARG;
+  if (!c->comm) return fail(c, C2D_E_STATE, "c2d_allreduce_tallies: c2d_comm_init first");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const ncclResult_t r = ncclAllReduce(c->T, c->T, (size_t)c->L.total, ncclDouble, ncclSum, c->comm,
+                                       c->stream);
+  if (r != ncclSuccess) return fail(c, C2D_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return C2D_OK;
 }

@@ -77,6 +77,10 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_census_export.restype = C.c_int
     lib.c2d_census_export.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32),
                                       C.POINTER(C.c_uint64), C.c_int64, C.POINTER(C.c_int64)]
+    lib.c2d_census_export_range.restype = C.c_int
+    lib.c2d_census_export_range.argtypes = [vp, C.c_int64, C.c_int64, C.POINTER(C.c_double),
+                                            C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.c_int64,
+                                            C.POINTER(C.c_int64)]
     lib.c2d_census_import.restype = C.c_int
     lib.c2d_census_import.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32),
                                       C.POINTER(C.c_uint64), C.c_int64]
@@ -108,6 +112,14 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_obs_accumulate_device.argtypes = [vp, C.c_void_p, C.c_int64]
     lib.c2d_obs_result.restype = C.c_int
     lib.c2d_obs_result.argtypes = [vp] + [C.POINTER(C.c_double)] * 4
+    lib.c2d_electron_state.restype = C.c_int
+    lib.c2d_electron_state.argtypes = [vp, abi.MArray3, abi.MArray3]
+    lib.c2d_comm_unique_id.restype = C.c_int
+    lib.c2d_comm_unique_id.argtypes = [C.c_void_p, C.c_int64]
+    lib.c2d_comm_init.restype = C.c_int
+    lib.c2d_comm_init.argtypes = [vp, C.c_void_p, C.c_int32, C.c_int32]
+    lib.c2d_allreduce_tallies.restype = C.c_int
+    lib.c2d_allreduce_tallies.argtypes = [vp]
     if path is None:
         _lib = lib
     return lib
@@ -214,6 +226,21 @@ class Engine:
             n, C.byref(m)))
         return d6[:n], i5[:n], keys[:n]
 
+    def census_sample(self, first: int, stride: int, cap: int):
+        """Census records first, first+stride, ... (at most cap)."""
+        n = C.c_int64()
+        self._check(self.lib.c2d_census_export_range(self.ctx, first, stride, None, None, None, 0,
+                                                     C.byref(n)))
+        m = min(cap, n.value)
+        d6 = np.zeros((max(m, 1), 6))
+        i5 = np.zeros((max(m, 1), 5), np.int32)
+        keys = np.zeros(max(m, 1), np.uint64)
+        self._check(self.lib.c2d_census_export_range(
+            self.ctx, first, stride, d6.ctypes.data_as(C.POINTER(C.c_double)),
+            i5.ctypes.data_as(C.POINTER(C.c_int32)), keys.ctypes.data_as(C.POINTER(C.c_uint64)),
+            m, C.byref(n)))
+        return d6[:m], i5[:m], keys[:m]
+
     def import_census(self, d6, i5, keys) -> None:
         d6 = np.ascontiguousarray(d6, np.float64)
         i5 = np.ascontiguousarray(i5, np.int32)
@@ -269,12 +296,40 @@ class Engine:
         self._check(self.lib.c2d_last_fp_ms(self.ctx, C.byref(ms)))
         return ms.value
 
+    def electron_state(self):
+        """The context's device electron state (f_nt, Pnt), each [nz, nr, NUM_NT]."""
+        f = np.zeros((self.nz, self.nr, abi.NUM_NT))
+        p = np.zeros_like(f)
+        mv = lambda a: abi.MArray3(a.ctypes.data_as(abi.PD), 1, self.nr * abi.NUM_NT, abi.NUM_NT)
+        self._check(self.lib.c2d_electron_state(self.ctx, mv(f), mv(p)))
+        return f, p
+
+    # -- RCCL tally all-reduce (xec_add / cens_add_up over xGMI) --------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        lib = load_library()
+        buf = C.create_string_buffer(abi.COMM_ID_BYTES)
+        rc = lib.c2d_comm_unique_id(buf, abi.COMM_ID_BYTES)
+        if rc != 0:
+            raise C2DError(rc, "c2d_comm_unique_id failed")
+        return buf.raw
+
+    def comm_init(self, uid: bytes, rank: int, world: int) -> None:
+        buf = C.create_string_buffer(bytes(uid), abi.COMM_ID_BYTES)
+        self._check(self.lib.c2d_comm_init(self.ctx, buf, int(rank), int(world)))
+
+    def allreduce_tallies(self) -> None:
+        """One in-place RCCL all-reduce of the fused tally buffer."""
+        self._check(self.lib.c2d_allreduce_tallies(self.ctx))
+
     # -- emission / absorption tables (imcgen2d.f:209-333, volume_em) ---------
-    def volume_em(self, dt: float, state: dict) -> dict:
+    def volume_em(self, dt: float, state: dict, tables_to_host: bool = True) -> dict:
         """kappa_tot, eps_tot, eps_th [nz, nr, 400], B_field, Eloss_sy/cy/th/tot
         [nz, nr] and E_ph [400] for the cell state (tea, tna, n_e, B_field,
-        f_pair, zsurf, vol [nz, nr], f_nt [nz, nr, 200], ep_switch)."""
-        call = abi.VemCall(dt, state)
+        f_pair, zsurf, vol [nz, nr], f_nt [nz, nr, 200], ep_switch).
+        f_nt None: the device electron state; tables_to_host False: the three
+        tables stay on the device for set_step(kappa_tot=None, ...)."""
+        call = abi.VemCall(dt, state, tables_to_host)
         self._check(self.lib.c2d_volume_em(self.ctx, C.byref(call.sin), C.byref(call.sout)))
         return call.res
 

@@ -1,5 +1,5 @@
-"""Host side of the boundary sources: the EC seed spectrum (`file_sp`) and the
-per-step surface budgets `imcgen2d` hands to the transport.
+"""Host side of imcgen2d's per-step budgets: the EC seed spectrum (`file_sp`),
+the surface ring budgets and the volume packet budget handed to the transport.
 
 These produce the `StepInputs` surface fields (`nsurf*`, `ewsurf*`, `tbb*`) and
 the `SpectrumTable` that `c2d_set_step` uploads; the sampling itself
@@ -12,8 +12,10 @@ the `SpectrumTable` that `c2d_set_step` uploads; the sampling itself
   disk luminosity, and builds the power-law segment CDF `P_file`.
 * time windows  src/imcgen2d.f:111-120 (window t = first with t1(t) > time+dt/2;
   window 1 on ncycle 0) and the EC gate `time + dt/2 >= t0(t)` (`:174`).
-* lower-ring budgets  src/imcgen2d.f:174-183 (`erinl`), :442 (`nsurfl`),
-  :481-485 (`ewsurfl`), :499-506 (bias cap); ring areas src/setup2d.f:102-113.
+* ring budgets  src/imcgen2d.f:155-183 (`erinu`, `erinl`), :436-437 (`nsurfu`,
+  `nsurfl`), :476-485 (`ewsurfu`, `ewsurfl`), :499-528 (bias cap); ring areas
+  src/setup2d.f:102-113.
+* volume budget  src/imcgen2d.f:406-413 (`Emiss_tot`), :446-456 (`nsv`, `ewsv`).
 
 Arithmetic follows the reference's expression order with `math` (glibc) so the
 tables equal the reference's bit for bit (tests/test_surface.py pins them
@@ -31,7 +33,7 @@ import numpy as np
 from . import abi
 
 PI_REF = 3.1415926536                      # general.pa:25
-SIGMA_SB = 5.6704e-5                       # erg cm^-2 s^-1 K^-4 (only for tbb > 0 rings)
+SIGMA_SB = 1.0267e24                       # imcgen2d.f:13-14: sigma*T^4 with T in keV
 NFMAX = abi.NFMAX                          # general.pa:17 (500)
 DATA = Path(__file__).resolve().parent / "data" / "ec_seed_spectra.npz"
 
@@ -145,26 +147,65 @@ def time_window(ncycle: int, time: float, dt: float, t1: Sequence[float]) -> int
     return len(t1)                       # loop ran out: t = ntime+1 (no window)
 
 
-def lower_surface_budget(r: np.ndarray, rmin: float, nst: int, dt: float, tbbl: np.ndarray,
-                         ec_on: bool, int_file: float):
-    """nsurfl, ewsurfl of every lower ring for one window (src/imcgen2d.f:174-183, :442,
-    :481-485).  `tbbl[k] < 0` marks an EC file ring; `ec_on` is the `time+dt/2 >= t0`
-    gate.  r(0) is taken as rmin (hazard H9: the reference reads z(99) there, which is 0
-    for every grid below 99 zones)."""
+def ring_budget(r: np.ndarray, rmin: float, nst: int, dt: float, tbb: np.ndarray,
+                ec_on: bool, int_file: float):
+    """(nsurf, ewsurf, erin) of every upper or lower ring for one window
+    (src/imcgen2d.f:155-183 erinu/erinl, :436-437 nsurfu/nsurfl, :476-485
+    ewsurfu/ewsurfl; the two sides share the formulas).  `tbb[k] < 0` marks an
+    EC file ring; `ec_on` is the `time+dt/2 >= t0` gate.  A ring with tbb > 0
+    gets its blackbody energy erin = dt*A*sigma*tbb^4 but no packets: the
+    reference sets nsurf only for tbb < 0.  r(0) is taken as rmin (hazard H9:
+    the reference reads z(99) there, which is 0 for every grid below 99 zones)."""
     nr = len(r)
     A = ring_areas(r, rmin)
-    nsurfl = np.zeros(nr, np.int32)
-    ewsurfl = np.zeros(nr)
+    nsurf = np.zeros(nr, np.int32)
+    ewsurf = np.zeros(nr)
+    erin = np.zeros(nr)
     for k in range(nr):
         rk0 = rmin if k == 0 else r[k - 1]
-        if tbbl[k] < 0.0 and ec_on:
-            erinl = dt * A[k] * int_file
+        if tbb[k] < 0.0 and ec_on:
+            erin[k] = dt * A[k] * int_file
         else:
-            erinl = dt * A[k] * SIGMA_SB * (tbbl[k] ** 4.0)
-        if tbbl[k] < 0.0:
-            nsurfl[k] = int(nst * (r[k] ** 2 - rk0 ** 2) / r[-1] ** 2)
-        ewsurfl[k] = erinl / float(nsurfl[k]) if nsurfl[k] > 0 else 0.0
-    return nsurfl, ewsurfl
+            erin[k] = dt * A[k] * SIGMA_SB * (tbb[k] ** 4.0)
+        if tbb[k] < 0.0:
+            nsurf[k] = int(nst * (r[k] ** 2 - rk0 ** 2) / r[-1] ** 2)
+        ewsurf[k] = erin[k] / float(nsurf[k]) if nsurf[k] > 0 else 0.0
+    return nsurf, ewsurf, erin
+
+
+def lower_surface_budget(r: np.ndarray, rmin: float, nst: int, dt: float, tbbl: np.ndarray,
+                         ec_on: bool, int_file: float):
+    """nsurfl, ewsurfl of every lower ring (ring_budget)."""
+    n, ew, _ = ring_budget(r, rmin, nst, dt, tbbl, ec_on, int_file)
+    return n, ew
+
+
+def upper_surface_budget(r: np.ndarray, rmin: float, nst: int, dt: float, tbbu: np.ndarray,
+                         ec_on: bool, int_file: float):
+    """nsurfu, ewsurfu of every upper ring (ring_budget; star_switch = 0)."""
+    n, ew, _ = ring_budget(r, rmin, nst, dt, tbbu, ec_on, int_file)
+    return n, ew
+
+
+def volume_budget(nst: int, fas: np.ndarray):
+    """nsv, ewsv of every zone (src/imcgen2d.f:406-413, :446-456):
+    Emiss_tot sums fas in (j, k) order; nsv = int(0.5*nst*fas/Emiss_tot)
+    (Fortran truncation), ewsv = fas/nsv (0 for an empty zone)."""
+    fas = np.asarray(fas, np.float64)
+    nz, nr = fas.shape
+    emiss_tot = 0.0
+    for j in range(nz):
+        for k in range(nr):
+            emiss_tot = emiss_tot + float(fas[j, k])
+    nsv = np.zeros((nz, nr), np.int32)
+    ewsv = np.zeros((nz, nr))
+    half = 0.5 * float(nst)
+    for j in range(nz):
+        for k in range(nr):
+            n = int(half * float(fas[j, k]) / emiss_tot) if emiss_tot != 0.0 else 0
+            nsv[j, k] = n
+            ewsv[j, k] = float(fas[j, k]) / float(n) if n > 0 else 0.0
+    return nsv, ewsv
 
 
 def apply_bias(nst: int, step: abi.StepInputs) -> float:

@@ -5,7 +5,9 @@
 ! src/commonblock.f:53-70), passes them to c2d_transport_step in place via
 ! (c_loc, strides), and runs NSTEPS steps.  Inputs: a stream file written by
 ! tests/test_fortran_binding.py (the golden case's step tables, only the
-! [1:nz,1:nr] block); output: the fused tally buffer of every step.
+! [1:nz,1:nr] block); output: the fused tally buffer of every step after
+! the RCCL all-reduce that replaces xec_add / cens_add_up (one rank here: an
+! MPI host broadcasts the id from rank 0 and passes its own rank / size).
 !
 ! usage: fortran_driver CASE.bin OUT.bin
 program fortran_driver
@@ -22,7 +24,8 @@ program fortran_driver
   integer(c_int32_t), target :: nsurfi(jmax), nsurfo(jmax), nsurfu(kmax), nsurfl(kmax)
   real(c_double), target :: ewsurfi(jmax), ewsurfo(jmax), ewsurfu(kmax), ewsurfl(kmax)
   real(c_double), target :: tbbi(jmax), tbbo(jmax), tbbu(kmax), tbbl(kmax)
-  real(c_double), allocatable :: tal(:)
+  real(c_double), allocatable :: tal(:), tal_raw(:)
+  integer(c_int8_t) :: comm_id(C2D_COMM_ID_BYTES)
   type(c2d_config) :: cfg
   type(c2d_step_in) :: sin
   type(c2d_tally_layout) :: lay
@@ -58,7 +61,17 @@ program fortran_driver
      stop 3
   end if
   rc = c2d_tally_layout_get(ctx, lay)
-  allocate(tal(lay%total))
+  allocate(tal(lay%total), tal_raw(lay%total))
+  ! RCCL communicator for the per-step tally all-reduce: rank 0 of 1 here;
+  ! under MPI: if (myid == 0) c2d_comm_unique_id, MPI_Bcast(comm_id), then
+  ! c2d_comm_init(ctx, comm_id, myid, numprocs)
+  rc = c2d_comm_unique_id(comm_id, int(C2D_COMM_ID_BYTES, c_int64_t))
+  if (rc == C2D_OK) rc = c2d_comm_init(ctx, comm_id, 0_c_int32_t, 1_c_int32_t)
+  if (rc /= C2D_OK) then
+     write(*, '(a,i0)') 'c2d_comm_init failed: ', rc
+     call print_error(ctx)
+     stop 5
+  end if
   open(newunit=v, file=trim(fout), access='stream', form='unformatted', status='replace')
 
   ! the COMMON arrays, described in place: element (i,j,k) 0-based at
@@ -109,7 +122,20 @@ program fortran_driver
         call print_error(ctx)
         stop 4
      end if
+     rc = c2d_tally_download(ctx, tal_raw, lay%total)
+     ! xec_add + graphics_collect + cens_add_up: one all-reduce of the fused buffer
+     rc = c2d_allreduce_tallies(ctx)
+     if (rc /= C2D_OK) then
+        write(*, '(a,i0)') 'c2d_allreduce_tallies failed: ', rc
+        call print_error(ctx)
+        stop 6
+     end if
      rc = c2d_tally_download(ctx, tal, lay%total)
+     if (all(transfer(tal, 0_c_int64_t, size(tal)) == transfer(tal_raw, 0_c_int64_t, size(tal_raw)))) then
+        write(*, '(a)') 'allreduce: bitwise identical (1 rank)'
+     else
+        write(*, '(a)') 'allreduce: MISMATCH'
+     end if
      write(v) tal
      write(*, '(a,i0,a,f0.0,a,f0.0)') 'step ', ncycle, ': packet-steps ', &
           tal(lay%counters + C2D_CNT_STEPS + 1), ' census ', tal(lay%counters + C2D_CNT_CENSUS + 1)

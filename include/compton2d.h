@@ -62,6 +62,7 @@ extern "C" {
 #define C2D_E_STATE            -7   /* call order violated                        */
 #define C2D_E_FP               -8   /* FP sub-step limit (reference `stop`,
                                        src/update2d.f:585-599) or a solver guard  */
+#define C2D_E_RCCL             -9   /* RCCL (communicator / all-reduce) error     */
 
 /* comtot (src/comtot2d.f:1-334, icoms=6) evaluation mode. */
 #define C2D_COMTOT_EXACT  0   /* 199-term electron-spectrum sum per call (reference)   */
@@ -138,7 +139,18 @@ typedef struct c2d_step_in {
   const int32_t* spec_u; const int32_t* spec_l;   /* [nr]                                  */
   int32_t n_spectra;
   const c2d_spectrum* spectra;
+  int32_t device_tables;          /* C2D_DEV_* flags: tables already on the device  */
 } c2d_step_in;
+
+/* c2d_step_in.device_tables: take tables from the device instead of the
+ * host views (which may then be NULL), so a coupled MC step
+ *   c2d_volume_em -> c2d_set_step -> c2d_run_step -> c2d_fp_step
+ * moves only zone scalars through the host (imcgen2d -> transport -> update,
+ * src/xec2d.f:67-87, with no table re-gathering per step). */
+#define C2D_DEV_EMISSION   1   /* kappa_tot, eps_tot, eps_th = last c2d_volume_em  */
+#define C2D_DEV_ELECTRONS  2   /* f_nt, Pnt = the context's electron state (last
+                                  c2d_set_step upload, updated in place by a
+                                  c2d_fp_step called with NULL f_nt/Pnt views)    */
 
 /* Fused per-step tally buffer (f64).  One all-reduce over this buffer
  * replaces xec_add, graphics_collect, cens_add_up and E_add_up's scalar
@@ -259,7 +271,9 @@ typedef struct c2d_fp_step_in {
 
 /* In/out state.  f_nt, Pnt, n_e, gmin, gmax, amxwl, p_nth and tea are read
  * and updated in place; Te_new is written.  Views with NULL data are
- * skipped (tea: the update2d.f:266-276 clamp is then left to the caller). */
+ * skipped (tea: the update2d.f:266-276 clamp is then left to the caller).
+ * f_nt and Pnt both NULL: the context's device electron state is read and
+ * updated in place (C2D_DEV_ELECTRONS) and nothing 200-bin crosses the host. */
 typedef struct c2d_fp_step_out {
   c2d_marray3 f_nt, Pnt;          /* (i<num_nt, j, k)                          */
   c2d_marray2 Te_new, tea, n_e, gmin, gmax, amxwl, p_nth;
@@ -279,7 +293,9 @@ typedef struct c2d_vem_in {
   double dt;                                         /* dt(1)                     */
   c2d_array2 tea, tna, n_e, B_field, f_pair, zsurf, vol;
   c2d_iarray2 ep_switch;                             /* null data: all 0          */
-  c2d_array3 f_nt;                                   /* (e-bin, j, k) like Pnt    */
+  c2d_array3 f_nt;                                   /* (e-bin, j, k) like Pnt;
+                                                        null data: the context's
+                                                        device electron state   */
 } c2d_vem_in;
 
 typedef struct c2d_vem_out {                         /* any data may be NULL      */
@@ -348,6 +364,10 @@ int  c2d_census_export(c2d_ctx* ctx, double* d6, int32_t* i5, uint64_t* keys,
                        int64_t cap, int64_t* n);
 int  c2d_census_import(c2d_ctx* ctx, const double* d6, const int32_t* i5,
                        const uint64_t* keys, int64_t n);
+/* Records first, first+stride, ... (at most cap of them) of the census:
+ * checkpoints in chunks, or a strided sample of a large census. */
+int  c2d_census_export_range(c2d_ctx* ctx, int64_t first, int64_t stride, double* d6,
+                             int32_t* i5, uint64_t* keys, int64_t cap, int64_t* n);
 
 /* Batched tridiagonal (Thomas with the reference's clipping) solve: one
  * zone per wavefront.  x is [ncell][nt] on the host. */
@@ -381,18 +401,41 @@ int  c2d_obs_accumulate_device(c2d_ctx* ctx, const double* d_events, int64_t n);
  * and the device time of the binning launches so far (ms). */
 int  c2d_obs_result(c2d_ctx* ctx, double* F, double* F2, double* count, double* kernel_ms);
 
+/* Copy the context's device electron state (C2D_DEV_ELECTRONS) into the
+ * caller's f_nt / Pnt views (either may have NULL data), e.g. before
+ * write_record (src/write_record.f) in a device-resident run. */
+int  c2d_electron_state(c2d_ctx* ctx, c2d_marray3 f_nt, c2d_marray3 Pnt);
+
 /* Device time of the last c2d_fp_step's FP kernel (HIP events, ms). */
 int  c2d_last_fp_ms(c2d_ctx* ctx, double* ms);
 
 /* imcgen2d's per-cell emission/absorption loop (volume_em for every cell)
  * on the GPU, one workgroup per cell; results written to the host arrays of
- * `out` and kept on the device (the next c2d_set_step may still pass them).
- * Synchronous. */
+ * `out` that are non-NULL and kept on the device for a following
+ * c2d_set_step with C2D_DEV_EMISSION.  Synchronous. */
 int  c2d_volume_em(c2d_ctx* ctx, const c2d_vem_in* in, c2d_vem_out* out);
 /* Device time of the last c2d_volume_em kernel (HIP events, ms). */
 int  c2d_last_vem_ms(c2d_ctx* ctx, double* ms);
 /* Packet-steps executed by that generation-0 launch (roofline numerator). */
 int  c2d_last_gen0_steps(c2d_ctx* ctx, int64_t* steps);
+
+/* ------------------------------------------------------------------------
+ * Multi-GPU tally reduction over RCCL (xGMI), for hosts that drive one
+ * context per GPU themselves (the kept Fortran driver, one MPI rank per GPU).
+ * Replaces the per-step scalar MPI_REDUCE loops of xec_add /
+ * graphics_collect (src/xec2d.f:325-399) and cens_add_up / E_add_up
+ * (src/update2d.f:1929-2078) with ONE in-place all-reduce of the fused tally
+ * buffer (c2d_tally_layout) per step.
+ *   rank 0: c2d_comm_unique_id(id); the host broadcasts the C2D_COMM_ID_BYTES
+ *   bytes (e.g. MPI_Bcast); every rank: c2d_comm_init(ctx, id, rank, world);
+ *   per step after c2d_run_step: c2d_allreduce_tallies(ctx).
+ * ---------------------------------------------------------------------- */
+#define C2D_COMM_ID_BYTES 128
+int  c2d_comm_unique_id(void* id, int64_t cap);
+int  c2d_comm_init(c2d_ctx* ctx, const void* id, int32_t rank, int32_t world);
+/* ncclAllReduce(sum, f64) in place on the context's tally buffer, on the
+ * context's stream; synchronous.  Without c2d_comm_init: C2D_E_STATE. */
+int  c2d_allreduce_tallies(c2d_ctx* ctx);
 
 /* Diagnostics: evaluate the transport kernels' elementary functions on the
  * device (fn 0 log, 1 exp, 2 cos, 3 acos, 4 cbrt-by-pow, 5 sqrt, 6 x/3,

@@ -12,7 +12,10 @@ module compton2d
 
   integer(c_int), parameter :: C2D_OK = 0, C2D_E_ARG = -1, C2D_E_HIP = -2, &
        C2D_E_CENSUS_OVERFLOW = -3, C2D_E_EVENT_OVERFLOW = -4, C2D_E_QUEUE_OVERFLOW = -5, &
-       C2D_E_NOMEM = -6, C2D_E_STATE = -7, C2D_E_FP = -8
+       C2D_E_NOMEM = -6, C2D_E_STATE = -7, C2D_E_FP = -8, C2D_E_RCCL = -9
+  ! c2d_step_in%device_tables flags; RCCL unique-id size (c2d_comm_unique_id)
+  integer(c_int32_t), parameter :: C2D_DEV_EMISSION = 1, C2D_DEV_ELECTRONS = 2
+  integer, parameter :: C2D_COMM_ID_BYTES = 128
   integer(c_int32_t), parameter :: C2D_COMTOT_EXACT = 0, C2D_COMTOT_TABLE = 1
   integer, parameter :: C2D_NCOUNTERS = 16, C2D_CNT_STEPS = 0, C2D_CNT_ESCAPES = 1, &
        C2D_CNT_CENSUS = 2
@@ -67,6 +70,7 @@ module compton2d
           spec_l = c_null_ptr
      integer(c_int32_t) :: n_spectra = 0
      type(c_ptr) :: spectra = c_null_ptr
+     integer(c_int32_t) :: device_tables = 0     ! C2D_DEV_* flags
   end type c2d_step_in
 
   ! ---- Fokker-Planck update (c2d_fp_set_config / c2d_fp_step) ----
@@ -274,5 +278,45 @@ module compton2d
        type(c_ptr), value :: ctx, F, F2, cnt       ! [n_e, n_mu, n_t] in Fortran order
        real(c_double), intent(out) :: kernel_ms
      end function c2d_obs_result
+
+     ! ---- RCCL tally all-reduce (replaces xec_add / graphics_collect,
+     !      src/xec2d.f:325-399, and cens_add_up / E_add_up,
+     !      src/update2d.f:1929-2078): rank 0 makes the id, the host
+     !      broadcasts it (MPI_Bcast of C2D_COMM_ID_BYTES bytes) ----
+     integer(c_int) function c2d_comm_unique_id(id, cap) bind(C, name='c2d_comm_unique_id')
+       import :: c_int, c_int8_t, c_int64_t
+       integer(c_int8_t), intent(out) :: id(*)
+       integer(c_int64_t), value :: cap
+     end function c2d_comm_unique_id
+
+     integer(c_int) function c2d_comm_init(ctx, id, rank, world) bind(C, name='c2d_comm_init')
+       import :: c_int, c_ptr, c_int8_t, c_int32_t
+       type(c_ptr), value :: ctx
+       integer(c_int8_t), intent(in) :: id(*)
+       integer(c_int32_t), value :: rank, world
+     end function c2d_comm_init
+
+     integer(c_int) function c2d_allreduce_tallies(ctx) bind(C, name='c2d_allreduce_tallies')
+       import :: c_int, c_ptr
+       type(c_ptr), value :: ctx
+     end function c2d_allreduce_tallies
+
+     integer(c_int) function c2d_electron_state(ctx, f_nt, Pnt) bind(C, name='c2d_electron_state')
+       import :: c_int, c_ptr, c2d_marray3
+       type(c_ptr), value :: ctx
+       type(c2d_marray3), value :: f_nt, Pnt
+     end function c2d_electron_state
+
+     integer(c_int) function c2d_census_export_range(ctx, first, stride, d6, i5, keys, cap, n) &
+          bind(C, name='c2d_census_export_range')
+       import :: c_int, c_ptr, c_double, c_int32_t, c_int64_t
+       type(c_ptr), value :: ctx
+       integer(c_int64_t), value :: first, stride
+       real(c_double), intent(out) :: d6(6, *)
+       integer(c_int32_t), intent(out) :: i5(5, *)
+       integer(c_int64_t), intent(out) :: keys(*)
+       integer(c_int64_t), value :: cap
+       integer(c_int64_t), intent(out) :: n
+     end function c2d_census_export_range
   end interface
 end module compton2d

@@ -490,9 +490,26 @@ static double* M2(const c2d_marray2* a, int j, int k) {
   return a->data ? &a->data[j * a->s_j + k * a->s_k] : NULL;
 }
 
+static int fp_step_sel(const c2d_config* g, const c2d_fp_config* fc, const c2d_fp_step_in* in,
+                       c2d_fp_step_out* out, const int32_t* sel, int nsel);
+
 /* `update` (update2d.f:138-277) over all zones, serially in zone order. */
 int c2o_fp_step(const c2d_config* g, const c2d_fp_config* fc, const c2d_fp_step_in* in,
                 c2d_fp_step_out* out) {
+  return fp_step_sel(g, fc, in, out, NULL, 0);
+}
+
+/* The same for the listed zones only (cell = j*nr + k, ascending): tests
+ * check a sample of a large grid's zones (FP_calc's zones are independent);
+ * the E_add_up sums then cover those zones only. */
+int c2o_fp_step_zones(const c2d_config* g, const c2d_fp_config* fc, const c2d_fp_step_in* in,
+                      c2d_fp_step_out* out, const int32_t* cells, int ncells) {
+  if (!cells || ncells < 0) return C2D_E_ARG;
+  return fp_step_sel(g, fc, in, out, cells, ncells);
+}
+
+static int fp_step_sel(const c2d_config* g, const c2d_fp_config* fc, const c2d_fp_step_in* in,
+                       c2d_fp_step_out* out, const int32_t* sel, int nsel) {
   if (!g || !fc || !in || !out) return C2D_E_ARG;
   if (fc->pair_switch != 0 && fc->pair_switch != 1) return C2D_E_ARG;
   if (fc->inj_switch != 0 && fc->inj_dis != 1 && fc->inj_dis != 2) return C2D_E_ARG;
@@ -512,8 +529,13 @@ int c2o_fp_step(const c2d_config* g, const c2d_fp_config* fc, const c2d_fp_step_
   double E_old = 0.0, E_new = 0.0, hr = 0.0, hr_st = 0.0;
   double nf[NPH];
   int rc = 0;
+  int isel = 0;
   for (int j = 0; j < nz && rc == 0; j++)
     for (int k = 0; k < nr && rc == 0; k++) {
+      if (sel) {
+        if (isel >= nsel || sel[isel] != j * nr + k) continue;
+        isel++;
+      }
       fp_zone Z;
       memset(&Z, 0, sizeof Z);
       Z.j = j + 1;

@@ -18,8 +18,16 @@ c     src/vol_mpi.f:107).  After every step it dumps the transport
 c     inputs and the worker tallies in full precision (stream files)
 c     so tests can compare the C oracle against the reference itself.
 c
-c     usage: c2d_refdrv NSTEPS KLAG    (run inside a prepared case
-c            directory holding input/input.dat + input/input_JJ_KK.dat)
+c     usage: c2d_refdrv NSTEPS KLAG [NFORCEU]   (run inside a prepared
+c            case directory holding input/input.dat + input_JJ_KK.dat)
+c
+c     NFORCEU > 0 gives every upper ring with a blackbody temperature
+c     (tbbu > 0) NFORCEU packets of weight erinu/NFORCEU after imcgen2d.
+c     In src/ such a ring gets its energy erinu (imcgen2d.f:155-163) but
+c     no packets (nsurfu is set only for tbbu < 0, imcgen2d.f:436-437),
+c     so r_surf_calc's planck branch (imcsurf2d_para.f:399-401,
+c     planck2d.f) is unreachable from input.dat; this exercises the
+c     reference's own r_surf_calc + planck on such packets.
 c
       program c2d_refdrv
       implicit none
@@ -27,7 +35,8 @@ c
       include 'general.pa'
       include 'commonblock.f'
 c
-      integer nsteps, klag, n, j, k, zone, js, ks, u
+      integer nsteps, klag, n, j, k, zone, js, ks, u, nforceu
+      integer iargc
       integer seeds_sv(jmax,kmax)
       double precision kap_cur(n_vol,jmax,kmax)
       double precision kap_prev(n_vol,jmax,kmax)
@@ -44,6 +53,11 @@ c
       read(arg, *) nsteps
       call getarg(2, arg)
       read(arg, *) klag
+      nforceu = 0
+      if (iargc().ge.3) then
+         call getarg(3, arg)
+         read(arg, *) nforceu
+      endif
 c
       open(unit=4, file='log.txt')
       call reader
@@ -105,6 +119,14 @@ c        time-window index (src/imcsurf2d_para.f:55-64)
                if (t1(ti).gt.t_average) goto 21
  20         continue
  21         continue
+         endif
+         if (nforceu.gt.0) then
+            do 22 k = 1, nr
+               if (tbbu(k,ti).gt.0.d0) then
+                  nsurfu(k) = nforceu
+                  ewsurfu(k) = erinu(k)/dble(nforceu)
+               endif
+ 22         continue
          endif
 c        transport inputs of this step
          write(fn, '(a,i3.3,a)') 'in_', n, '.bin'

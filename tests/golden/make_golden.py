@@ -41,7 +41,22 @@ CASES = {
     "ec_lower": dict(case=dict(nz=2, nr=2, n_e=2.0e6, nst=1000, tbbl=-1.0), nsteps=3),
     # 3x4 grid, two angular bins
     "grid3x4": dict(case=dict(nz=3, nr=4, n_e=1.0e6, nst=1500, nmu=2), nsteps=2),
+    # EC seed spectrum on the UPPER boundary (r_surf_calc's upper-ring loop,
+    # src/imcsurf2d_para.f:362-420: wmu = -fibran(), zpre = z(nz), file_sample)
+    "ec_upper": dict(case=dict(nz=2, nr=2, n_e=2.0e6, nst=1000, tbbu=-1.0), nsteps=3),
+    # blackbody upper rings (tbbu > 0): planck (src/planck2d.f:1-141) on
+    # upper-ring packets; src/imcgen2d.f:436-437 gives such rings no packets,
+    # so the driver hands each 200 of weight erinu/200 (c2d_refdrv NFORCEU)
+    "bb_upper": dict(case=dict(nz=2, nr=2, n_e=2.0e6, nst=1000, tbbu=[2.0e-3, 5.0e-2]),
+                     nsteps=2, nforceu=200),
 }
+
+# C3: the Mrk 421 SSC deck src_20121026/input.dat:1-130 +
+# inputm.dat, transport AND Fokker-Planck, at reduced nst; see
+# compton2d_amd/synth.py C3_DECK for the deviations (splits, rand_switch)
+C3_CASE = "c3_mrk421"
+C3_NST = 20000
+C3_STEPS = 3
 
 # Fokker-Planck cases (T_const=0): the reference's update/FP_calc after each
 # transport step with ncycle > 0 (refdrv dumps fpin_/fpout_NNN.bin)
@@ -71,12 +86,13 @@ IN_KEYS = ("kappa_tot", "eps_tot", "eps_th", "f_nt", "Pnt", "n_e", "Eloss_th", "
            "ewsurfu", "ewsurfl", "tbbi", "tbbo", "tbbu", "tbbl")
 
 
-def run_case(name: str, spec: dict, out_dir: Path, work: Path) -> Path:
+def run_case(name: str, spec: dict, out_dir: Path, work: Path, fp: bool = False) -> Path:
     d = work / name
     if d.exists():
         shutil.rmtree(d)
     refcase.write_input_deck(d, spec["case"])
-    refcase.run_reference(d, spec["nsteps"], klag=1)
+    refcase.run_reference(d, spec["nsteps"], klag=1, nforceu=spec.get("nforceu", 0),
+                          timeout=7200 if fp else 600)
     cfg = refcase.read_config(d)
     arrays = {}
     meta = {k: v for k, v in cfg.items() if not isinstance(v, np.ndarray)}
@@ -100,10 +116,56 @@ def run_case(name: str, spec: dict, out_dir: Path, work: Path) -> Path:
         if nf >= 2:
             for k in ("E_file", "a1", "I_file", "F_file", "P_file"):
                 arrays["out%d_%s" % (n, k)] = so[k][:nf]
+    if fp:
+        full = dict(refcase.BASE_CASE)
+        full.update(spec["case"])
+        meta["fp_const"] = {k: full[k] for k in FP_CONST_KEYS}
+        steps = []
+        for n in range(spec["nsteps"]):
+            if not refcase.has_fp(d, n):
+                continue
+            fi, fo = refcase.read_fp_in(d, n, cfg), refcase.read_fp_out(d, n, cfg)
+            steps.append(n)
+            meta["fp%d" % n] = dict(ncycle=fi["ncycle"], time=fi["time"], dt=fi["dt"],
+                                    **{k: fo[k] for k in ("E_tot_old", "E_tot_new", "hr_total",
+                                                          "hr_st_total", "dT_max")})
+            for k, v in fi.items():
+                # the photon field/ecens FP_calc reads are this step's tallies (out%d_)
+                if isinstance(v, np.ndarray) and k not in ("n_field", "ecens"):
+                    arrays["fpin%d_%s" % (n, k)] = v
+            for k, v in fo.items():
+                if isinstance(v, np.ndarray):
+                    arrays["fpout%d_%s" % (n, k)] = v
+            assert np.array_equal(fi["n_field"], arrays["out%d_n_field" % n])
+            assert np.array_equal(fi["ecens"], arrays["out%d_ecens" % n])
+        meta["fp_steps"] = steps
+        # the electron state passes unchanged between FP and transport
+        # (fpin_n = in_n, in_n+1 = fpout_n): store each array once
+        meta["alias"] = dedupe(arrays)
     arrays["meta_json"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
     path = out_dir / (name + ".npz")
     np.savez_compressed(path, **arrays)
     return path
+
+
+def dedupe(arrays: dict) -> dict:
+    """Drop arrays equal to one stored under an earlier key; returns
+    {dropped key: kept key} (tests/golden_io.py resolves it)."""
+    alias, seen = {}, {}
+    for k in list(arrays):
+        v = arrays[k]
+        sig = (v.dtype.str, v.shape, hash(v.tobytes()))
+        if sig in seen and np.array_equal(arrays[seen[sig]], v):
+            alias[k] = seen[sig]
+            del arrays[k]
+        else:
+            seen[sig] = k
+    return alias
+
+
+def c3_spec() -> dict:
+    from compton2d_amd import synth
+    return dict(case=synth.c3_refcase(nst=C3_NST), nsteps=C3_STEPS)
 
 
 def run_fp_case(name: str, spec: dict, out_dir: Path, work: Path) -> Path:
@@ -331,6 +393,9 @@ def main() -> None:
             if args.only and name != args.only:
                 continue
             p = run_fp_case(name, spec, out, work)
+            print("wrote", p, p.stat().st_size, "bytes")
+        if not args.only or args.only == C3_CASE:
+            p = run_case(C3_CASE, c3_spec(), out, work, fp=True)
             print("wrote", p, p.stat().st_size, "bytes")
         if not args.only or args.only == "census_fmt":
             p = make_census_format(out, work)

@@ -10,18 +10,27 @@ import numpy as np
 from compton2d_amd import abi
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
-CASES = ("ssc_tau", "ec_lower", "grid3x4")
+CASES = ("ssc_tau", "ec_lower", "grid3x4", "ec_upper", "bb_upper", "c3_mrk421")
 IN_KEYS = ("kappa_tot", "eps_tot", "eps_th", "f_nt", "Pnt", "n_e", "Eloss_th", "Eloss_tot",
            "zsurf", "ewsv", "nsv", "nsurfi", "nsurfo", "ewsurfi", "ewsurfo", "nsurfu", "nsurfl",
            "ewsurfu", "ewsurfl", "tbbi", "tbbo", "tbbu", "tbbl")
 
 
+def _load(name: str):
+    """(arrays, meta) of a fixture, with de-duplicated arrays restored
+    (make_golden.dedupe: meta['alias'] maps a dropped key to its equal)."""
+    z = np.load(GOLDEN / (name + ".npz"), allow_pickle=False)
+    a = {k: z[k] for k in z.files}
+    meta = json.loads(bytes(a.pop("meta_json")).decode())
+    for k, src in meta.get("alias", {}).items():
+        a[k] = a[src]
+    return a, meta
+
+
 class GoldenCase:
     def __init__(self, name: str):
         self.name = name
-        z = np.load(GOLDEN / (name + ".npz"), allow_pickle=False)
-        self.a = {k: z[k] for k in z.files}
-        self.meta = json.loads(bytes(self.a.pop("meta_json")).decode())
+        self.a, self.meta = _load(name)
         self.nsteps = self.meta["nsteps"]
         self.nz, self.nr, self.nmu = self.meta["nz"], self.meta["nr"], self.meta["nmu"]
 
@@ -64,9 +73,7 @@ class FpGoldenCase:
 
     def __init__(self, name: str):
         self.name = name
-        z = np.load(GOLDEN / (name + ".npz"), allow_pickle=False)
-        self.a = {k: z[k] for k in z.files}
-        self.meta = json.loads(bytes(self.a.pop("meta_json")).decode())
+        self.a, self.meta = _load(name)
         self.steps = list(self.meta["fp_steps"])
         self.nz, self.nr = self.meta["nz"], self.meta["nr"]
 
@@ -86,6 +93,34 @@ class FpGoldenCase:
 
     def fp_in(self, n: int) -> dict:
         d = {k[len("fpin%d_" % n):]: v for k, v in self.a.items() if k.startswith("fpin%d_" % n)}
+        d.update({k: self.meta["fp%d" % n][k] for k in ("ncycle", "time", "dt")})
+        return d
+
+    def fp_out(self, n: int) -> dict:
+        d = {k[len("fpout%d_" % n):]: v for k, v in self.a.items() if k.startswith("fpout%d_" % n)}
+        d.update({k: self.meta["fp%d" % n][k] for k in ("E_tot_old", "E_tot_new", "hr_total",
+                                                       "hr_st_total", "dT_max")})
+        return d
+
+
+class CoupledGoldenCase(GoldenCase):
+    """Transport AND Fokker-Planck steps of one reference run (c3_mrk421:
+    the C3 deck, tests/golden/make_golden.py): per step the transport inputs
+    and tallies (GoldenCase) and, for ncycle > 0, the FP_calc inputs/outputs
+    whose photon field / ecens are that step's tallies."""
+
+    def __init__(self, name: str):
+        super().__init__(name)
+        self.fp_steps = list(self.meta["fp_steps"])
+
+    def constants(self) -> abi.FpConstants:
+        return abi.FpConstants(F_IC=fp_fic(), pair_switch=int(self.meta.get("pair_switch", 0)),
+                               **self.meta["fp_const"])
+
+    def fp_in(self, n: int) -> dict:
+        d = {k[len("fpin%d_" % n):]: v for k, v in self.a.items() if k.startswith("fpin%d_" % n)}
+        d["n_field"] = self.out(n, "n_field")
+        d["ecens"] = self.out(n, "ecens")
         d.update({k: self.meta["fp%d" % n][k] for k in ("ncycle", "time", "dt")})
         return d
 

@@ -87,6 +87,10 @@ def load(flavor: str = "ref") -> C.CDLL:
     lib.c2o_fp_step.restype = C.c_int
     lib.c2o_fp_step.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.FpConfig),
                                 C.POINTER(abi.FpStepIn), C.POINTER(abi.FpStepOut)]
+    lib.c2o_fp_step_zones.restype = C.c_int
+    lib.c2o_fp_step_zones.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.FpConfig),
+                                      C.POINTER(abi.FpStepIn), C.POINTER(abi.FpStepOut),
+                                      C.POINTER(C.c_int32), C.c_int]
     lib.c2o_gamma_bar.restype = C.c_double
     lib.c2o_gamma_bar.argtypes = [C.c_double]
     _libs[flavor] = lib
@@ -151,12 +155,19 @@ class Oracle:
 
 
 def fp_step(grid: abi.GridConfig, const: abi.FpConstants, ncycle: int, time: float, dt: float,
-            inputs: dict, state: dict, flavor: str = "det") -> dict:
-    """The oracle's `update` (oracle/c2d_fp_oracle.c): returns the new state."""
+            inputs: dict, state: dict, flavor: str = "det", cells=None) -> dict:
+    """The oracle's `update` (oracle/c2d_fp_oracle.c): returns the new state.
+    `cells` (ascending j*nr+k): solve only those zones (the others keep their
+    input state; the E_add_up sums cover the listed zones)."""
     lib = load(flavor)
     g, fc = grid.to_ctypes(), const.to_ctypes()
     call = abi.FpCall(ncycle, time, dt, inputs, state)
-    rc = lib.c2o_fp_step(C.byref(g), C.byref(fc), C.byref(call.sin), C.byref(call.sout))
+    if cells is not None:
+        sel = np.ascontiguousarray(sorted(int(x) for x in cells), np.int32)
+        rc = lib.c2o_fp_step_zones(C.byref(g), C.byref(fc), C.byref(call.sin), C.byref(call.sout),
+                                   sel.ctypes.data_as(C.POINTER(C.c_int32)), len(sel))
+    else:
+        rc = lib.c2o_fp_step(C.byref(g), C.byref(fc), C.byref(call.sin), C.byref(call.sout))
     if rc != 0:
         raise RuntimeError("c2o_fp_step failed: %d" % rc)
     return call.result()

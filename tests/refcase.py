@@ -130,11 +130,19 @@ def write_input_deck(case_dir: Path, case: dict) -> None:
         shutil.copy(src, d / c["spec_file"])
 
 
-def run_reference(case_dir: Path, nsteps: int, klag: int = 1, timeout: int = 600) -> None:
+def run_reference(case_dir: Path, nsteps: int, klag: int = 1, timeout: int = 600,
+                  nforceu: int = 0) -> None:
+    """Run c2d_refdrv; nforceu > 0 gives blackbody upper rings (tbbu > 0)
+    nforceu packets each (see oracle/ref/c2d_refdrv.f)."""
     if not REFDRV.exists():
         raise FileNotFoundError("reference driver not built: run oracle/ref/build_ref.sh")
-    subprocess.run([str(REFDRV), str(nsteps), str(klag)], cwd=str(case_dir), check=True,
-                   timeout=timeout, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    import resource
+
+    def big_stack():   # the reference needs `ulimit -s unlimited` (SURVEY.md §5)
+        resource.setrlimit(resource.RLIMIT_STACK, (resource.RLIM_INFINITY, resource.RLIM_INFINITY))
+    subprocess.run([str(REFDRV), str(nsteps), str(klag), str(nforceu)], cwd=str(case_dir),
+                   check=True, timeout=timeout, stdout=subprocess.DEVNULL,
+                   stderr=subprocess.DEVNULL, preexec_fn=big_stack)
 
 
 class _Reader:

@@ -82,6 +82,10 @@ def test_fortran_host_matches_python_host(tmp_path):
     r = subprocess.run([str(exe), str(tmp_path / "case.bin"), str(tmp_path / "out.bin")],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+    # the RCCL all-reduce through the C-ABI (c2d_comm_init/c2d_allreduce_tallies)
+    # ran every step and, with one rank, left the buffer bit for bit unchanged
+    assert r.stdout.count("allreduce: bitwise identical (1 rank)") == nsteps, r.stdout
+    assert "MISMATCH" not in r.stdout
     fort = np.fromfile(tmp_path / "out.bin", "<f8").reshape(nsteps, -1)
     eng = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, census_capacity=1048576,
                          event_capacity=1048576, queue_capacity=262144))

@@ -1,0 +1,126 @@
+"""BASELINE config C3 (the Mrk 421 SSC deck, FP on) on the GPU, against the
+oracle and the reference run on that deck (tests/golden/c3_mrk421.npz).
+
+* exact transport kernel vs the oracle (lineage RNG, det math) on the
+  reference's C3 step inputs: tests/test_gpu_parity.py (c3_mrk421 is one of
+  golden_io.CASES), bit-identical histories;
+* c2d_fp_step on the reference's C3 FP inputs (all 270 zones): bit-identical
+  to the det-math oracle on sampled zones, Te_new equal to the reference's,
+  f_nt within 1e-10;
+* c2d_volume_em on the FP-updated C3 state (the step-2 tables): equal to the
+  det oracle bit for bit, within 1e-12 of the reference's kappa/eps_tot;
+* the coupled step chained on the device (transport -> tallies -> FP
+  reading n_field/ecens from the device buffer) equals the same chain run by
+  the oracle (lineage transport + FP);
+* the device-resident coupled loop (compton2d_amd/coupled.py: tables and
+  electrons never leave the GPU) equals the host-array loop.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as OL
+from compton2d_amd import abi, synth
+from compton2d_amd.coupled import CoupledRun
+from compton2d_amd.engine import Engine
+from golden_io import CoupledGoldenCase
+from test_c3 import SAMPLE, ZONE_KEYS
+
+pytestmark = pytest.mark.gpu
+
+
+def case():
+    return CoupledGoldenCase("c3_mrk421")
+
+
+def test_gpu_c3_fp_bitwise_vs_oracle_and_reference():
+    gc = case()
+    eng = Engine(gc.grid(device=0))
+    eng.fp_set_config(gc.constants())
+    for n in gc.fp_steps:
+        fi = gc.fp_in(n)
+        g = eng.fp_step(fi["ncycle"], fi["time"], fi["dt"], fi, fi)
+        o = OL.fp_step(gc.grid(), gc.constants(), fi["ncycle"], fi["time"], fi["dt"], fi, fi,
+                       flavor="det", cells=SAMPLE)
+        for cell in SAMPLE:
+            j, k = divmod(cell, gc.nr)
+            for key in ZONE_KEYS + ("zone_diag",):
+                np.testing.assert_array_equal(g[key][j, k], o[key][j, k],
+                                              err_msg="step %d zone (%d,%d) %s" % (n, j, k, key))
+        ref = gc.fp_out(n)
+        np.testing.assert_array_equal(g["Te_new"], ref["Te_new"])
+        np.testing.assert_array_equal(g["tea"], ref["tea"])
+        assert np.max(np.abs(g["f_nt"] - ref["f_nt"])) <= 1e-10 * np.max(np.abs(ref["f_nt"]))
+        for key in ("E_tot_old", "E_tot_new", "hr_total"):
+            assert abs(g[key] - ref[key]) <= 1e-9 * abs(ref[key]), (n, key)
+    assert eng.last_fp_ms() > 0
+    eng.close()
+
+
+def test_gpu_c3_tables_from_fp_state():
+    gc = case()
+    wl = synth.c3_workload(sources=gc.meta["case"]["nst"] // 2)
+    fo = gc.fp_out(1)
+    st = dict(wl.fixed, tea=fo["tea"], n_e=fo["n_e"], f_nt=fo["f_nt"])
+    dt = gc.meta["step2"]["dt"]
+    with Engine(gc.grid(device=0)) as e:
+        g = e.volume_em(dt, st)
+    o = OL.vem_step(gc.grid(), dt, st, flavor="det")
+    for k in ("kappa_tot", "eps_tot", "eps_th", "Eloss_tot", "Eloss_sy", "B_field"):
+        assert np.array_equal(g[k], o[k]), k
+    np.testing.assert_allclose(g["kappa_tot"], gc.a["in2_kappa_tot"], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(g["eps_tot"], gc.a["in2_eps_tot"], rtol=1e-12, atol=0)
+
+
+def test_gpu_c3_transport_then_fp_from_device_tallies():
+    """Step 1 of the C3 run: exact transport on the reference's inputs, then
+    FP_calc reading the device tallies; the oracle runs the same chain."""
+    gc = case()
+    grid = gc.grid(comtot_mode=abi.COMTOT_EXACT, device=0)
+    eng = Engine(grid)
+    eng.fp_set_config(gc.constants())
+    orc = OL.Oracle(gc.grid(), OL.RNG_LINEAGE, "det")
+    for n in (0, 1):
+        si = gc.step_inputs(n)
+        eng.transport_step(si)
+        assert orc.step(si) == 0
+    to = orc.split()
+    fi = gc.fp_in(1)
+    dev = dict(fi, n_field=None, ecens=None)
+    g = eng.fp_step(1, fi["time"], fi["dt"], dev, fi)
+    host = dict(fi, n_field=np.asarray(to["n_field"]).reshape(gc.nz, gc.nr, abi.NPHFIELD),
+                ecens=np.asarray(to["ecens"]).reshape(gc.nz, gc.nr))
+    o = OL.fp_step(gc.grid(), gc.constants(), 1, fi["time"], fi["dt"], host, fi, flavor="det",
+                   cells=SAMPLE)
+    for cell in SAMPLE:
+        j, k = divmod(cell, gc.nr)
+        # the device n_field sums by atomics (order differs from the oracle at
+        # 1e-16); FP_calc carries that through thousands of sub-steps
+        np.testing.assert_allclose(g["f_nt"][j, k], o["f_nt"][j, k], rtol=1e-8,
+                                   atol=1e-12 * np.max(o["f_nt"][j, k]))
+        assert abs(g["Te_new"][j, k] - o["Te_new"][j, k]) <= 1e-8 * o["Te_new"][j, k]
+    eng.close()
+    orc.close()
+
+
+def test_gpu_c3_device_resident_loop_equals_host_loop():
+    """compton2d_amd/coupled.py with tables/electrons on the device vs the
+    same loop through host arrays: same kernels, same inputs, so the same
+    electron state up to the atomic summation order of the tallies."""
+    runs = []
+    for dev in (True, False):
+        wl = synth.c3_workload(sources=200_000, comtot_mode=abi.COMTOT_TABLE)
+        eng = Engine(wl.grid)
+        run = CoupledRun(eng, wl, device_resident=dev)
+        rows = [run.step() for _ in range(3)]
+        f, p = run.electrons()
+        runs.append((rows, f, p, dict(run.state)))
+        eng.close()
+    (ra, fa, pa, sa), (rb, fb, pb, sb) = runs
+    for a, b in zip(ra, rb):
+        assert a["volume_packets"] == b["volume_packets"]
+        assert abs(a["packet_steps"] - b["packet_steps"]) <= 1e-3 * b["packet_steps"]
+    np.testing.assert_allclose(fa, fb, rtol=1e-6, atol=1e-12 * np.max(np.abs(fb)))
+    np.testing.assert_allclose(pa, pb, rtol=1e-6, atol=1e-12)
+    np.testing.assert_array_equal(sa["tea"], sb["tea"])
+    assert rb[-1]["aborted"] == 0 and ra[-1]["aborted"] == 0
+    assert ra[-1]["mean_Te"] > 1.0e3          # FP_calc heats past the clamp, as the reference

@@ -72,3 +72,11 @@ def test_golden_cases_exercise_every_branch():
     assert ec.meta["step0"]["nfile"] >= 2              # file_sp table present
     g = GoldenCase("grid3x4")
     assert g.nmu == 2 and g.nz == 3 and g.nr == 4
+    up = GoldenCase("ec_upper")                        # upper-ring file spectrum
+    assert up.a["in1_nsurfu"].sum() > 0 and (up.a["in1_tbbu"] < 0).all()
+    bb = GoldenCase("bb_upper")                        # upper-ring planck
+    assert bb.a["in1_nsurfu"].sum() > 0 and (bb.a["in1_tbbu"] > 0).all()
+    assert bb.out(1, "census_d").shape[0] + len(bb.out(1, "events")) > 0
+    c3 = GoldenCase("c3_mrk421")                       # the C3 deck, FP on
+    assert (c3.nz, c3.nr) == (30, 9) and c3.meta["pair_switch"] == 1 and c3.meta["T_const"] == 0
+    assert c3.meta["fp_steps"] == [1, 2]

@@ -46,13 +46,15 @@ def test_budget_off_window_and_ring_counts():
     r = np.array([1.0, 2.0, 3.0, 4.0]) * 1e16
     ns, ew = S.lower_surface_budget(r, 0.0, 16000, 10.0, np.full(4, -1.0), False, 5.0)
     # packets are still allotted to EC rings outside the t0 gate, with the blackbody
-    # energy of tbb = -1 (sigma * 1), as imcgen2d.f:179 and :442 do
+    # energy of tbb = -1 (sigma * 1, sigma = 1.0267d24 in keV units, imcgen2d.f:13-14),
+    # as imcgen2d.f:179 and :442 do
     # int() truncation of the f64 expression, as the Fortran assignment does (999, not 1000)
     assert list(ns) == [int(16000 * (r[k] ** 2 - (r[k - 1] if k else 0.0) ** 2) / r[-1] ** 2)
                         for k in range(4)]
     assert abs(int(ns.sum()) - 16000) <= 4
     A = S.ring_areas(r, 0.0)
-    np.testing.assert_allclose(ew, 10.0 * A * S.SIGMA_SB / ns, rtol=1e-15)
+    assert S.SIGMA_SB == 1.0267e24
+    np.testing.assert_allclose(ew, 10.0 * A * 1.0267e24 / ns, rtol=1e-15)
     ns0, ew0 = S.lower_surface_budget(r, 0.0, 16000, 10.0, np.zeros(4), True, 5.0)
     assert ns0.sum() == 0 and ew0.sum() == 0.0
 
@@ -102,3 +104,47 @@ def test_c5_binning_equals_ext25_deck():
     for k in ("mode", "gam_bulk", "rmax", "t0", "t1", "mu0", "mu1", "E0", "E1", "dt",
               "t_offset", "t_stop"):
         np.testing.assert_array_equal(getattr(a, k), getattr(b, k))
+
+
+def test_upper_surface_budget_matches_reference():
+    """EC file spectrum on the upper rings (ec_upper: tbbu = -1)."""
+    gc = GoldenCase("ec_upper")
+    _, int_file = S.file_sp(S.seed_spectrum("blackbody_20110929"), S.EcConstants())
+    nst = gc.meta["case"]["nst"]
+    for n in range(gc.nsteps):
+        st = gc.meta["step%d" % n]
+        si = gc.step_inputs(n)
+        assert si.nsurfu.sum() > 0
+        ns, ew = S.upper_surface_budget(gc.a["cfg_r"], gc.meta["rmin"], nst, st["dt"],
+                                        np.asarray(si.tbbu, float), True, int_file)
+        np.testing.assert_array_equal(ns, si.nsurfu)
+        np.testing.assert_array_equal(ew, si.ewsurfu)
+
+
+def test_blackbody_ring_energy_matches_reference():
+    """tbbu > 0: erinu = dt*A*sigma*tbbu^4 (imcgen2d.f:155-157) but no packets
+    (imcgen2d.f:437); bb_upper's driver gave each such ring 200 packets of
+    weight erinu/200 (oracle/ref/c2d_refdrv.f NFORCEU)."""
+    gc = GoldenCase("bb_upper")
+    nst = gc.meta["case"]["nst"]
+    for n in range(gc.nsteps):
+        st = gc.meta["step%d" % n]
+        si = gc.step_inputs(n)
+        tb = np.asarray(si.tbbu, float)
+        assert (tb > 0).all()
+        ns, ew, erin = S.ring_budget(gc.a["cfg_r"], gc.meta["rmin"], nst, st["dt"], tb, True, 0.0)
+        assert ns.sum() == 0 and ew.sum() == 0.0
+        np.testing.assert_array_equal(si.nsurfu, 200)
+        np.testing.assert_array_equal(erin / 200.0, si.ewsurfu)
+
+
+@pytest.mark.parametrize("name", ["ssc_tau", "ec_lower", "grid3x4", "c3_mrk421"])
+def test_volume_budget_matches_reference(name):
+    """nsv/ewsv from Eloss_tot (imcgen2d.f:406-413, :446-456), bit for bit."""
+    gc = GoldenCase(name)
+    nst = gc.meta["case"]["nst"]
+    for n in range(gc.nsteps):
+        si = gc.step_inputs(n)
+        nsv, ewsv = S.volume_budget(nst, si.Eloss_tot)
+        np.testing.assert_array_equal(nsv, si.nsv)
+        np.testing.assert_array_equal(ewsv, si.ewsv)
