@@ -15,7 +15,8 @@ full, to a companion file `<path>.keys` (little-endian uint64, one per
 packet), so a restart from our own files resumes the exact histories while
 files written by the reference still load (keys are then derived from the
 seed column and the record index).  As in the reference, the 6 doubles keep
-e14.7 precision (8 significant digits) across a restart.
+e14.7 precision (0.ddddddd: 7 significant digits) across a restart; the exact
+lineage keys are in the `.keys` file.
 """
 from __future__ import annotations
 

@@ -135,8 +135,8 @@ struct KParams {
   const double* tbbl;           /* [nr]  lower-surface temperature (imcleak) */
   const SpecDev* spectra;
   int32_t n_spectra, nslot;
-  const float* comtab;          /* [ncell][C2D_COMTAB_N] cosig on the u grid (f32: half the
-                                   L2 footprint; 6e-8 relative, far below the cubic's error) */
+  const double* comtab;         /* [ncell][C2D_COMTAB_N] cosig on the u grid, f64 (as the
+                                   reference evaluates comtot; 16 KB per cell)               */
   double comtab_du_inv;
   /* census */
   CensusSoA cin, cout;

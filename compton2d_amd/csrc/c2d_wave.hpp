@@ -131,12 +131,12 @@ __device__ __forceinline__ int mcd_take(bool run, unsigned long long st) {
  * exposes its latency while the other issues (one wave per SIMD hides
  * nothing else).  The sums still run in n order over exactly the terms the
  * reference adds, so the result is unchanged bit for bit. */
-__device__ inline void mcdonald23_w(double z, int lane, const double* __restrict__ tab, double& K2,
-                             double& K3, long long& guard, double* scr) {
+/* The series from term n0 on (t0 = t_n0 by the reference's chain), adding
+ * to sum2/sum3 while run2/run3; returns with both series stopped. */
+__device__ inline void mcdonald23_from(double z, int lane, const double* __restrict__ tab, int n0,
+                                       double t0, double& sum2, double& sum3, bool run2, bool run3,
+                                       long long& guard, double* scr) {
   const double dt = 1.001, s = 5.0e-1 * (1.0 + dt);
-  double sum2 = 0.0, sum3 = 0.0, t0 = 1.0;
-  bool run2 = true, run3 = true;
-  int n0 = 0;
   while (run2 || run3) {
     if (n0 + 2 * FPB <= C2D_FP_MCD_N) {
       const McdTerm a = mcd_term_tab(z, n0 + lane, tab);
@@ -219,8 +219,20 @@ __device__ inline void mcdonald23_w(double z, int lane, const double* __restrict
     t0 = rl(tn, FPB - 1);
     n0 += FPB;
   }
+}
+
+/* McDonald's normalisation (volume2d.f:623-624) of the two sums */
+__device__ __forceinline__ void mcdonald23_finish(double z, double sum2, double sum3, double& K2,
+                                                  double& K3) {
   K2 = __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, 2.0) * sum2 / c2d_exp(gammln(5.0e-1 + 2.0));
   K3 = __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, 3.0) * sum3 / c2d_exp(gammln(5.0e-1 + 3.0));
+}
+
+__device__ inline void mcdonald23_w(double z, int lane, const double* __restrict__ tab, double& K2,
+                                    double& K3, long long& guard, double* scr) {
+  double sum2 = 0.0, sum3 = 0.0;
+  mcdonald23_from(z, lane, tab, 0, 1.0, sum2, sum3, true, true, guard, scr);
+  mcdonald23_finish(z, sum2, sum3, K2, K3);
 }
 
 /* gamma_bar (volume2d.f:572-594) */

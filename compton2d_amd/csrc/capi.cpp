@@ -34,8 +34,9 @@ extern "C" int c2d_transport_occupancy_exact(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t s);
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
-                                      float* tab, int ncell, hipStream_t s);
-extern "C" int c2d_launch_fp(const FpParams* P, int ncell, hipStream_t s);
+                                      double* tab, int ncell, hipStream_t s);
+extern "C" int c2d_launch_fp(const FpParams* P, int ncell, int waves, hipStream_t s);
+extern "C" int c2d_fp_waves(int ncell, int n_simd);
 extern "C" int c2d_launch_vem(const VemParams* P, int ncell, hipStream_t s);
 extern "C" int c2d_launch_obs(const ObsDev* O, const double* ev, int64_t n, int grid,
                               hipStream_t s);
@@ -111,7 +112,7 @@ struct c2d_ctx {
   SpecDev* spectra = nullptr;
   std::vector<double*> spec_bufs;
   int n_spectra = 0;
-  float* comtab = nullptr;
+  double* comtab = nullptr;
   double* comS = nullptr;
   DevCensus cens[2];
   int cur_out = 0;           /* census buffer written by the last step */
@@ -151,6 +152,7 @@ struct c2d_ctx {
          *fp_nf = nullptr, *fp_fout = nullptr, *fp_Pout = nullptr, *fp_zout = nullptr;
   int32_t* fp_err = nullptr;
   float last_fp_ms = 0.f;
+  int last_fp_waves = 0;
   /* emission / absorption tables (c2d_volume_em) */
   double *vem_zin = nullptr, *vem_fnt = nullptr, *vem_eph = nullptr, *vem_kap = nullptr,
          *vem_et = nullptr, *vem_eh = nullptr, *vem_zout = nullptr;
@@ -204,6 +206,8 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   if (cfg->split1 < 1 || cfg->split2 < 1 || cfg->split3 < 1 || cfg->world < 1 ||
       cfg->rank < 0 || cfg->rank >= cfg->world)
     return C2D_E_ARG;
+  /* the event buffer is C2D_EV_SHARDS equal shards; each must hold events */
+  if (cfg->event_capacity < C2D_EV_SHARDS) return C2D_E_ARG;
   c2d_ctx* c = new c2d_ctx();
   c->cfg = *cfg;
   c->nz = cfg->nz;
@@ -767,10 +771,16 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   if (herr & ERR_CENSUS)
     return fail(c, C2D_E_CENSUS_OVERFLOW, "too many photons: census %lld > capacity %lld",
                 (long long)ncout, (long long)cfg.census_capacity);
-  if (herr & ERR_EVENT)
+  if (herr & ERR_EVENT) {
+    unsigned long long fill = 0;
+    for (int sh = 0; sh < C2D_EV_SHARDS; sh++)
+      fill = std::max(fill, ctl[CTL_EVSH + sh * C2D_EV_SHARD_STRIDE]);
     return fail(c, C2D_E_EVENT_OVERFLOW,
-                "event buffer overflow: %llu events, capacity %lld (%d shards of %lld)", ev_reserved,
-                (long long)cfg.event_capacity, C2D_EV_SHARDS, (long long)c->ev_cap_sh);
+                "event buffer overflow: %llu events, capacity %lld = %d shards of %lld (the "
+                "fullest shard took %llu: size event_capacity >= %d x that)", ev_reserved,
+                (long long)cfg.event_capacity, C2D_EV_SHARDS, (long long)c->ev_cap_sh, fill,
+                C2D_EV_SHARDS);
+  }
   if (herr & ERR_QUEUE) return fail(c, C2D_E_QUEUE_OVERFLOW, "scatter queue overflow");
   if (herr & ERR_SPEC) return fail(c, C2D_E_ARG, "surface packet without a seed spectrum");
   return C2D_OK;
@@ -1101,7 +1111,8 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   P.P_out = el_dev ? c->Pnt : c->fp_Pout;
   P.zout = c->fp_zout; P.err = c->fp_err;
   HIPCHK(c, hipEventRecord(c->ev_g0a, st));
-  int rc = c2d_launch_fp(&P, nc, st);
+  c->last_fp_waves = c2d_fp_waves(nc, 4 * c->n_cu);
+  int rc = c2d_launch_fp(&P, nc, c->last_fp_waves, st);
   if (rc) return fail(c, C2D_E_HIP, "fp launch: %s", hipGetErrorString((hipError_t)rc));
   HIPCHK(c, hipEventRecord(c->ev_g0b, st));
   std::vector<double> zout((size_t)nc * FO_N), fout(nnt), pout(nnt);

@@ -33,6 +33,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "c2d_device.hpp"
 #include "c2d_math.h"
@@ -86,19 +87,358 @@ constexpr double C_LIGHT = 2.9979245620e10;   /* general.pa:25 */
 constexpr double LNL = 20.0;                  /* update2d.f:143 */
 constexpr int MAX_FP_STEPS = 1000000;         /* update2d.f:585-599 */
 
+/* ---- McDonald K2/K3 across the zone's workgroup ------------------------
+ * The zone's FP_calc runs on wave 0.  Its temperature search spends most of
+ * the kernel in McDonald's series (thousands of terms per gamma_bar at the
+ * Theta of a heated zone), whose terms are independent and whose stopping
+ * term depends on the term alone, while the sums must be added in order.
+ * Waves 1..MCD_PROD compute the terms, 2*64 per wave per pass, into a
+ * double-buffered LDS block (with their stop ballots); wave 0 adds them in
+ * order while the next pass is computed.  One s_barrier per pass; every wave
+ * derives "both series stopped" from the same ballots, so all leave the loop
+ * after the same barrier.  Sums, stopping terms and results are those of the
+ * single-wave mcdonald23_w bit for bit (same terms, same order). */
+/* The launch picks the waves per zone (blockDim.x / 64, 1..FP_WAVES_MAX;
+ * c2d_launch_fp): more where few zones leave SIMDs idle, one (the
+ * single-wave series, c2d_wave.hpp) where the zones alone fill the chip. */
+constexpr int FP_WAVES_MAX = 8;
+/* The kernel is instantiated for WMAX = 1 (one wave per zone, launch bounds
+ * 64: the codegen of a single-wave solve, measured 2.3x faster than the same
+ * code compiled for 512-thread workgroups) and WMAX = FP_WAVES_MAX. */
+constexpr int MCD_PROD_MAX = FP_WAVES_MAX - 1;
+constexpr int MCD_BLK = 2 * FPB;                       /* terms per producer per pass */
+constexpr int MCD_PASS_MAX = MCD_PROD_MAX * MCD_BLK;
+constexpr int MCD_BATCH = 16;                          /* divides MCD_BLK */
+enum { MCD_CMD_EXIT = 0, MCD_CMD_SERIES = 1, MCD_CMD_BATCH = 2 };
+
+/* Temperature-search candidates evaluated together (one per lane of every
+ * wave of the zone): the search of update2d.f:1440-1468 walks the chain
+ * Theta*1.005^k (or /1.005^k) and stops at the first gamma_bar crossing
+ * gbar; when it walks far (a zone heating by orders of magnitude within an
+ * MC step: C3 takes ~800 steps per zone), evaluating the next NB chain
+ * members at once replaces NB sequential McDonald pairs by one pass in
+ * which each lane sums ITS candidate's series in order.  gamma_bar is a pure
+ * function of Theta and the chain is formed by the same repeated
+ * multiplication, so every value used equals the sequential one bit for bit;
+ * members past the crossing are simply not used (or reused by the next
+ * sub-step's search, which continues the same chain). */
+constexpr int NB_MAX = FP_WAVES_MAX * FPB;
+#ifndef C2D_FP_NSINGLE
+#define C2D_FP_NSINGLE 3
+#endif
+constexpr int FP_NSINGLE = C2D_FP_NSINGLE;   /* search steps before batching */
+#ifndef C2D_FP_PREFETCH
+#define C2D_FP_PREFETCH 1
+#endif
+
+/* the producer waves' LDS (only multi-wave kernels reference it) */
+struct McdCoop {
+  alignas(16) double term[2][MCD_PASS_MAX][2];         /* [buffer][n][K2 term, K3 term] */
+  unsigned long long mask[2][MCD_PROD_MAX][4];         /* stop2 a/b, stop3 a/b ballots  */
+  double z;                                            /* SERIES: argument; BATCH: start */
+  int cmd, dir;                                        /* BATCH: +1 (x1.005) / -1 (/1.005) */
+};
+/* a batch's chain members and their gamma_bar, sized per kernel instance so
+ * the single-wave kernel keeps its LDS small (occupancy: 1024 zones must fit) */
+template <int N>
+struct McdBatch {
+  double bc[N], bg[N];
+};
+
+/* gamma_bar (volume2d.f:572-594) of this lane's Theta, McDonald's series
+ * summed sequentially by the lane (volume2d.f:598-626): n is wave-uniform, so
+ * the abscissa table reads are scalar loads; two terms per iteration give the
+ * exp/divide chains some overlap; each series stops at its own term. */
+__device__ double gamma_bar_lane(double Theta, const double* __restrict__ tab, long long& guard) {
+  double g;
+  if (Theta < F32(0.2)) {
+    g = (1. + F32(4.375) * Theta + F32(7.383) * (Theta * Theta) +
+         F32(3.384) * (Theta * Theta * Theta)) /
+            (1. + F32(1.875) * Theta + F32(.8203) * (Theta * Theta)) -
+        Theta;
+  } else {
+    const double z = 1.0 / Theta;
+    const double dt = 1.001, d = dt - 1.0, s = 5.0e-1 * (1.0 + dt);
+    double sum2 = 0.0, sum3 = 0.0, t = 1.0;
+    bool run2 = true, run3 = true;
+    int n = 0;
+#if C2D_FP_PREFETCH
+    /* the next iteration's abscissa rows are loaded before this one's terms */
+    double4 ra = *(const double4*)tab, rb = *(const double4*)(tab + 4);
+#endif
+    for (; n + 2 <= C2D_FP_MCD_N; n += 2) {
+      if (!__ballot(run2 || run3)) break;
+#if C2D_FP_PREFETCH
+      const double ta = ra.x, tsa = ra.y, p2a = ra.z, p3a = ra.w;
+      const double tb = rb.x, tsb = rb.y, p2b = rb.z, p3b = rb.w;
+      if (n + 4 <= C2D_FP_MCD_N) {
+        ra = *(const double4*)(tab + (size_t)(n + 2) * 4);
+        rb = *(const double4*)(tab + (size_t)(n + 3) * 4);
+      }
+#else
+      const double* e = tab + (size_t)n * 4;
+      const double ta = e[0], tsa = e[1], p2a = e[2], p3a = e[3];
+      const double tb = e[4], tsb = e[5], p2b = e[6], p3b = e[7];
+#endif
+      const double ya = z * tsa, yb = z * tsb;
+      double sd2a = 0.0, sd3a = 0.0, sd2b = 0.0, sd3b = 0.0;
+      if (ya < 2.25e2) {
+        const double ey = c2d_exp(ya);
+        sd2a = p2a / ey;
+        sd3a = p3a / ey;
+      }
+      if (yb < 2.25e2) {
+        const double ey = c2d_exp(yb);
+        sd2b = p2b / ey;
+        sd3b = p3b / ey;
+      }
+      const double tna = ta * dt, tnb = tb * dt;
+      if (run2) {
+        sum2 = sum2 + d * ta * sd2a;
+        if (!(tna < 2.0 || sd2a > 1.0e-8)) run2 = false;
+        else {
+          sum2 = sum2 + d * tb * sd2b;
+          if (!(tnb < 2.0 || sd2b > 1.0e-8)) run2 = false;
+        }
+      }
+      if (run3) {
+        sum3 = sum3 + d * ta * sd3a;
+        if (!(tna < 2.0 || sd3a > 1.0e-8)) run3 = false;
+        else {
+          sum3 = sum3 + d * tb * sd3b;
+          if (!(tnb < 2.0 || sd3b > 1.0e-8)) run3 = false;
+        }
+      }
+      t = tnb;
+    }
+    guard += n;
+    /* beyond the table: the abscissae by the reference's own chain */
+    while (run2 || run3) {
+      const double ts = t * s;
+      const double p2 = c2d_pow(ts * ts - 1.0, 1.5), p3 = c2d_pow(ts * ts - 1.0, 2.5);
+      const double y = z * ts;
+      double sd2 = 0.0, sd3 = 0.0;
+      if (y < 2.25e2) {
+        const double ey = c2d_exp(y);
+        sd2 = p2 / ey;
+        sd3 = p3 / ey;
+      }
+      const double tn = t * dt;
+      if (run2) {
+        sum2 = sum2 + d * t * sd2;
+        if (!(tn < 2.0 || sd2 > 1.0e-8)) run2 = false;
+      }
+      if (run3) {
+        sum3 = sum3 + d * t * sd3;
+        if (!(tn < 2.0 || sd3 > 1.0e-8)) run3 = false;
+      }
+      t = tn;
+      if (++guard > GUARD_MAX) break;
+    }
+    double K2, K3;
+    mcdonald23_finish(z, sum2, sum3, K2, K3);
+    g = K3 / K2 - Theta;
+  }
+  if (g < 1.0) g = 1.0;
+  return g;
+}
+
+/* chain member idx+1 from th0 (the search's own repeated x or / 1.005),
+ * then its gamma_bar, into the batch arrays */
+template <int N>
+__device__ __forceinline__ void batch_member(McdBatch<N>& C, double th0, int dir, int idx,
+                                             const double* __restrict__ tab, long long& guard) {
+  double c = th0;
+  for (int i = 0; i <= idx; i++) c = (dir > 0) ? c * F32(1.005) : c / F32(1.005);
+  const double g = gamma_bar_lane(c, tab, guard);
+  C.bc[idx] = c;
+  C.bg[idx] = g;
+}
+
+/* waves of this zone's workgroup (uniform) */
+template <int WMAX>
+__device__ __forceinline__ int fp_nwaves() {
+  return WMAX == 1 ? 1 : (int)(blockDim.x / FPB);
+}
+
+/* run flags after pass p's ballots (identical on every wave) */
+__device__ __forceinline__ void mcd_pass_runs(const McdCoop& C, int p, int nprod, bool& run2,
+                                              bool& run3) {
+  const unsigned long long(*m)[4] = C.mask[p & 1];
+  for (int w = 0; w < nprod; w++) {
+    if (m[w][0] | m[w][1]) run2 = false;
+    if (m[w][2] | m[w][3]) run3 = false;
+  }
+}
+
+/* producer waves: serve series requests until wave 0 posts MCD_CMD_EXIT */
+__device__ __forceinline__ void mcd_producer(McdCoop& C, McdBatch<NB_MAX>& B,
+                                             const double* __restrict__ tab, int wave, int lane) {
+  for (;;) {
+    __syncthreads();                                   /* request posted by wave 0 */
+    if (C.cmd == MCD_CMD_EXIT) return;
+    if (C.cmd == MCD_CMD_BATCH) {
+      long long g = 0;
+      batch_member(B, C.z, C.dir, wave * FPB + lane, tab, g);
+      __syncthreads();                                 /* batch complete */
+      continue;
+    }
+    const double z = C.z;
+    const int nprod = fp_nwaves<FP_WAVES_MAX>() - 1, pass = nprod * MCD_BLK;
+    const int npass = C2D_FP_MCD_N / pass;
+    bool run2 = true, run3 = true;
+    for (int p = 0; p < npass; p++) {
+      const int n0 = p * pass + (wave - 1) * MCD_BLK;
+      const McdTerm a = mcd_term_tab(z, n0 + lane, tab);
+      const McdTerm b = mcd_term_tab(z, n0 + FPB + lane, tab);
+      double(*t)[2] = C.term[p & 1] + (wave - 1) * MCD_BLK;
+      t[lane][0] = a.term2;
+      t[lane][1] = a.term3;
+      t[FPB + lane][0] = b.term2;
+      t[FPB + lane][1] = b.term3;
+      const unsigned long long s2a = __ballot(a.stop2), s2b = __ballot(b.stop2);
+      const unsigned long long s3a = __ballot(a.stop3), s3b = __ballot(b.stop3);
+      if (lane == 0) {
+        unsigned long long* m = C.mask[p & 1][wave - 1];
+        m[0] = s2a; m[1] = s2b; m[2] = s3a; m[3] = s3b;
+      }
+      __syncthreads();                                 /* pass p complete */
+      mcd_pass_runs(C, p, nprod, run2, run3);
+      if (!run2 && !run3) break;
+    }
+  }
+}
+
+/* wave 0: K2, K3 of McDonald(2, z), McDonald(3, z) with the producers */
+template <int WMAX>
+__device__ __forceinline__ void mcdonald23_coop(McdCoop& C, double z, int lane, const double* __restrict__ tab,
+                                double& K2, double& K3, long long& guard, double* scr) {
+  if (lane == 0) {
+    C.z = z;
+    C.cmd = MCD_CMD_SERIES;
+  }
+  __syncthreads();                                     /* post the request */
+  const int nprod = fp_nwaves<WMAX>() - 1, pass = nprod * MCD_BLK, npass = C2D_FP_MCD_N / pass;
+  double sum2 = 0.0, sum3 = 0.0;
+  bool run2 = true, run3 = true;
+  int p = 0;
+  for (; p < npass; p++) {
+    __syncthreads();                                   /* pass p complete */
+    const double(*t)[2] = C.term[p & 1];
+    const unsigned long long(*m)[4] = C.mask[p & 1];
+    bool clean = run2 && run3;
+    for (int w = 0; w < nprod; w++) clean = clean && !(m[w][0] | m[w][1] | m[w][2] | m[w][3]);
+    if (clean) {
+      /* operands of MCD_BATCH terms are loaded before their adds, so the
+       * chain waits for the adds alone, not one LDS latency per term */
+      for (int q0 = 0; q0 < pass; q0 += MCD_BATCH) {
+        double2 v[MCD_BATCH];
+#pragma unroll
+        for (int i = 0; i < MCD_BATCH; i++) v[i] = *(const double2*)t[q0 + i];
+#pragma unroll
+        for (int i = 0; i < MCD_BATCH; i++) {
+          sum2 = sum2 + v[i].x;
+          sum3 = sum3 + v[i].y;
+        }
+      }
+      guard += pass;
+    } else {
+      for (int h = 0; h < 2 * nprod; h++) {            /* 64-term blocks in n order */
+        const int w = h >> 1, half = h & 1;
+        const unsigned long long m2 = m[w][half], m3 = m[w][2 + half];
+        const int n2 = mcd_take(run2, m2), n3 = mcd_take(run3, m3);
+        const double(*tb)[2] = t + h * FPB;
+        for (int q = 0; q < n2; q++) sum2 = sum2 + tb[q][0];
+        for (int q = 0; q < n3; q++) sum3 = sum3 + tb[q][1];
+        if (m2) run2 = false;
+        if (m3) run3 = false;
+        guard += n2 > n3 ? n2 : n3;
+      }
+    }
+    if (!run2 && !run3) break;
+  }
+  if (run2 || run3) {                                  /* beyond the coop passes: alone */
+    const int n0 = npass * pass;
+    mcdonald23_from(z, lane, tab, n0, tab[(size_t)n0 * 4], sum2, sum3, run2, run3, guard, scr);
+  }
+  mcdonald23_finish(z, sum2, sum3, K2, K3);
+}
+
+/* wave 0: evaluate chain members 1..NB from th0 on every wave of the zone */
+template <int WMAX, int N>
+__device__ __forceinline__ void search_batch(McdCoop& C, McdBatch<N>& B, double th0, int dir, int lane,
+                                             const double* __restrict__ tab, long long& guard) {
+  if (fp_nwaves<WMAX>() > 1) {
+    if (lane == 0) {
+      C.z = th0;
+      C.dir = dir;
+      C.cmd = MCD_CMD_BATCH;
+    }
+    __syncthreads();                                   /* post the request */
+  }
+  batch_member(B, th0, dir, lane, tab, guard);
+  __syncthreads();                                     /* batch complete */
+}
+
+/* gamma_bar (volume2d.f:572-594) with the cooperative series */
+template <int WMAX>
+__device__ __forceinline__ double gamma_bar_coop(McdCoop& C, double Theta, int lane, const double* tab,
+                                 long long& guard, double* scr) {
+  double g;
+  if (Theta < F32(0.2)) {
+    g = (1. + F32(4.375) * Theta + F32(7.383) * (Theta * Theta) +
+         F32(3.384) * (Theta * Theta * Theta)) /
+            (1. + F32(1.875) * Theta + F32(.8203) * (Theta * Theta)) -
+        Theta;
+  } else {
+    double K2, K3;
+    if (fp_nwaves<WMAX>() > 1)
+      mcdonald23_coop<WMAX>(C, 1.0 / Theta, lane, tab, K2, K3, guard, scr);
+    else
+      mcdonald23_w(1.0 / Theta, lane, tab, K2, K3, guard, scr);
+    g = K3 / K2 - Theta;
+  }
+  if (g < 1.0) g = 1.0;
+  return g;
+}
+
 }  // namespace
 
-/* One zone per workgroup (= one wave).  Line numbers: src/update2d.f. */
-__global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
-  __shared__ double s_gnt[NT + 2], s_gam[NT + 2], s_fold[NT + 2], s_fnew[NT + 2];
-  __shared__ double s_dgic[NT + 2], s_dgdt[NT + 2], s_disp[NT + 2];
-  __shared__ double s_a[NT + 2], s_b[NT + 2], s_c[NT + 2];
-  __shared__ double s_mcd[4 * FPB];   /* McDonald term exchange (c2d_wave.hpp) */
-  __shared__ double s_smw[NT + 2], s_bigW[NT + 2], s_bigC[NT + 2], s_em[NT + 2], s_inj[NT + 2];
-  __shared__ double s_Pnt[NT + 2], s_nf[NPH];
+/* hand-offs of wave 0's 200-bin arrays (only wave 0 touches them) */
+template <int WMAX>
+__device__ __forceinline__ void fp_sync() {
+  if (WMAX == 1)
+    __syncthreads();
+  else
+    wave_sync();
+}
 
+/* The zone's LDS, at namespace scope so that every access is a ds_* op with
+ * a known address space (pointers to it passed into a function compile to
+ * flat accesses: 2.5x slower on this kernel). */
+__shared__ double s_gnt[NT + 2], s_gam[NT + 2], s_fold[NT + 2], s_fnew[NT + 2];
+__shared__ double s_dgic[NT + 2], s_dgdt[NT + 2], s_disp[NT + 2];
+__shared__ double s_a[NT + 2], s_b[NT + 2], s_c[NT + 2];
+__shared__ double s_mcd[4 * FPB];   /* McDonald term exchange (c2d_wave.hpp) */
+__shared__ double s_smw[NT + 2], s_bigW[NT + 2], s_bigC[NT + 2], s_em[NT + 2], s_inj[NT + 2];
+__shared__ double s_Pnt[NT + 2], s_nf[NPH];
+__shared__ McdCoop s_coop;
+__shared__ McdBatch<FPB> s_batch1;
+__shared__ McdBatch<NB_MAX> s_batch8;
+template <int WMAX>
+__device__ __forceinline__ auto& batch_lds() {
+  if constexpr (WMAX == 1)
+    return s_batch1;
+  else
+    return s_batch8;
+}
+
+/* FP_calc of one zone on one wave (the kernel's wave 0).  Only this wave
+ * touches the 200-bin arrays, so their hand-offs are wave barriers; the
+ * workgroup barriers belong to the McDonald cooperation alone. */
+template <int WMAX>
+__device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) {
   const int cell = blockIdx.x;
-  const int lane = threadIdx.x;
   const int j = cell / P.nr + 1, k = cell % P.nr + 1;
   const Geo* G = P.geo;
   const double* zin = P.zin + (size_t)cell * FZ_N;
@@ -132,7 +472,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
     s_Pnt[i + 1] = P.P_in[(size_t)cell * NT + i];
   }
   for (int i = lane; i < NPH; i += FPB) s_nf[i] = P.nf[(size_t)cell * NPH + i];
-  __syncthreads();
+  fp_sync<WMAX>();
 
   /* E_el, normalisation (:482-509) */
   double E_el = 0.0, E_pos = 0.0;
@@ -143,9 +483,9 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
   double e_new = 0.0 + ecens;
   double sum_p = seq_sum(0., 1, NT - 1, lane,
                          [&](int i) { return (s_gnt[i + 1] - s_gnt[i]) * s_fold[i]; });
-  __syncthreads();
+  fp_sync<WMAX>();
   for (int i = lane + 1; i <= NT; i += FPB) s_fold[i] = s_fold[i] / sum_p;
-  __syncthreads();
+  fp_sync<WMAX>();
   if (lane == 0) s_fold[NT] = 0.0;
 
   /* flare (:532-562) */
@@ -173,7 +513,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
   }
   if (lane == 0) s_dgic[NT] = 0.0;   /* hazard H10 */
   const double dz = G->z[j] - G->z[j - 1];          /* :628-632 */
-  __syncthreads();
+  fp_sync<WMAX>();
 
   double hr = 0.0, hr_st = 0.0, sum_E = 0.0, t_fp = 0.0;
   int fp_steps = 0;
@@ -192,12 +532,29 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
 #pragma unroll
     for (int q = 0; q < 4; q++)
       if (memo_th[q] == th) return memo_g[q];
-    const double g = gamma_bar_w(th, lane, P.mcd, guard, s_mcd);
+    const double g = gamma_bar_coop<WMAX>(s_coop, th, lane, P.mcd, guard, s_mcd);
 #pragma unroll
     for (int q = 0; q < 4; q++)
       if (q == memo_next) { memo_th[q] = th; memo_g[q] = g; }
     memo_next = (memo_next + 1) & 3;
     return g;
+  };
+  /* gamma_bar of the search's next chain member: from the last batch while
+   * the walk follows its chain, by a new batch once this search has taken
+   * FP_NSINGLE steps (it is walking far), else singly (memo / cooperative
+   * series).  bdir = 0: no usable batch. */
+  int bdir = 0, bpos = 0;
+  auto search_eval = [&](double prev, double next, int dir, int k) -> double {
+    auto& B = batch_lds<WMAX>();
+    if (bdir == dir && bpos < fp_nwaves<WMAX>() * FPB && B.bc[bpos] == next) return B.bg[bpos++];
+    if (k >= FP_NSINGLE && next >= F32(0.2)) {
+      search_batch<WMAX>(s_coop, B, prev, dir, lane, P.mcd, guard);
+      bdir = dir;
+      bpos = 1;
+      return B.bg[0];
+    }
+    bdir = 0;
+    return gamma_bar_m(next);
   };
 #ifdef C2D_FP_PROF
   long long pf_gb = 0, pf_tri = 0, pf_loop0 = clock64(), pf_t0, pf_calls = 0;
@@ -274,13 +631,13 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
       /* pairs on with no positrons (H6: n_pos = dn_pp = 0, f_pair = 0): the
        * pa_calc rates vanish, so loop 460 (:1187-1217) adds 0/ne and clips
        * f_old below 1e-50; trid_p solves for npos = 0 (:1400), unused here */
-      __syncthreads();
+      fp_sync<WMAX>();
       for (int i = lane + 1; i <= NT - 1; i += FPB) {
         double v = s_fold[i] + 0.0 / ne;
         if (v < 1.0e-50) v = 0.0;
         s_fold[i] = v;
       }
-      __syncthreads();
+      fp_sync<WMAX>();
     }
     n_positron = 0.0;                                  /* :1164-1167 / :1218 */
     ne = n_p + n_positron;
@@ -294,27 +651,27 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
         s_inj[i] = 1.0e2 * c2d_exp(-((x * x) / 2.0 / (P.inj_sigma * P.inj_sigma))) /
                    (P.inj_sigma * __builtin_sqrt(2.0 * PI_REF));
       }
-      __syncthreads();
+      fp_sync<WMAX>();
       inj_sum = seq_sum(0.0, 1, NT - 1, lane,
                         [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); });
       inj_rho = P.pick_rate * d_t;
       inj_any = true;
     }
     if (inj_any) {
-      __syncthreads();
+      fp_sync<WMAX>();
       for (int i = lane + 1; i <= NT - 1; i += FPB) {
         const double v = inj_rho * s_inj[i] / inj_sum;
         s_inj[i] = v;
         s_fold[i] = s_fold[i] + v / ne;
       }
-      __syncthreads();
+      fp_sync<WMAX>();
       n_inject = seq_sum(n_inject, 1, NT - 1, lane,
                          [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); });
     }
     if (P.inj_switch != 0) {
       const double tt = P.time + t_fp - P.inj_t;
       if (tt > dz / P.inj_v * (double)(j - 1) && tt < dz / P.inj_v * (double)j && k <= P.nr) {
-        __syncthreads();
+        fp_sync<WMAX>();
         for (int i = lane + 1; i <= NT - 1; i += FPB) {
           const double gi = s_gam[i];
           double v;
@@ -334,7 +691,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
           }
           s_inj[i] = v;
         }
-        __syncthreads();
+        fp_sync<WMAX>();
         double isum = 0.0, inj_E = 0.0;
         seq_sum2(isum, inj_E, 1, NT - 1, lane,
                  [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); },
@@ -342,13 +699,13 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
         inj_E = inj_E / isum;
         const double inj_rate = P.inj_L / 8.186e-7 / inj_E / (PI_REF * (rmax * rmax) * dz);
         const double rho = inj_rate * d_t;
-        __syncthreads();
+        fp_sync<WMAX>();
         for (int i = lane + 1; i <= NT - 1; i += FPB) {
           const double v = rho * s_inj[i] / isum;
           s_inj[i] = v;
           s_fold[i] = s_fold[i] + v / ne;
         }
-        __syncthreads();
+        fp_sync<WMAX>();
         n_inject = seq_sum(n_inject, 1, NT - 1, lane,
                            [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); });
       }
@@ -359,7 +716,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
     ne = ne * t_esc / (t_esc + d_t);                  /* escape (:1309-1313) */
     n_p = n_p * t_esc / (t_esc + d_t);
     n_lept = n_lept * t_esc / (t_esc + d_t);
-    __syncthreads();
+    fp_sync<WMAX>();
     /* Chang-Cooper coefficients (:1363-1390): smw, bigW, bigC and the
      * exp(-smw) factor for i = 1..NT-1, then a, b, c for i = 2..NT-1 */
     for (int i = lane + 1; i <= NT - 1; i += FPB) {
@@ -378,7 +735,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
       s_em[i] = bigC * smw / (1.0 - c2d_exp(-smw));   /* bigC*smw/(1-exp(-smw)) */
       s_bigC[i] = bigC;
     }
-    __syncthreads();
+    fp_sync<WMAX>();
     for (int i = lane + 2; i <= NT - 1; i += FPB) {
       const double D_gminus = s_gnt[i] - s_gnt[i - 1];
       const double D_gplus = s_gnt[i + 1] - s_gnt[i];
@@ -392,7 +749,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
       s_a[1] = 0.0; s_b[1] = 1.0; s_c[1] = 0.0;
       s_a[NT] = 0.0; s_b[NT] = 1.0; s_c[NT] = 0.0;
     }
-    __syncthreads();
+    fp_sync<WMAX>();
     PF_BEGIN();
     /* tridag (:2476-2518): the recurrences run in the reference order on
      * wave-uniform values (readlane) with each 64-bin chunk's operands staged
@@ -428,7 +785,7 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
           s_fnew[i] = umine;
         }
       }
-      __syncthreads();
+      fp_sync<WMAX>();
       if (zero) {
         for (int i = lane + 1; i <= NT; i += FPB) s_fnew[i] = 0.0;
       } else {
@@ -447,18 +804,18 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
           }
           if (in) s_fnew[i] = mine;
         }
-        __syncthreads();
+        fp_sync<WMAX>();
         for (int i = lane + 2; i <= NT; i += FPB)
           if (s_fnew[i] < 0.0) s_fnew[i] = 0.0;
       }
-      __syncthreads();
+      fp_sync<WMAX>();
     }
     PF_END(pf_tri);
     if (lane == 0) {
       s_fnew[NT] = 0.0;
       s_fnew[1] = 0.0;
     }
-    __syncthreads();
+    fp_sync<WMAX>();
     sum_p = 0.;
     double sE = 0.;
     for (int c0 = 1; c0 <= NT - 1; c0 += FPB) {       /* :1415-1419 */
@@ -481,13 +838,13 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
     sum_E = sE / sum_p;
     t_fp = t_fp + d_t;
     fp_steps = fp_steps + 1;
-    __syncthreads();
+    fp_sync<WMAX>();
     for (int i = lane + 1; i <= NT; i += FPB) {
       const double v = s_fnew[i] / sum_p;
       s_fnew[i] = v;
       s_fold[i] = v;
     }
-    __syncthreads();
+    fp_sync<WMAX>();
     /* new temperature (:1440-1468) */
     const double gbar = seq_sum(0.0, 1, NT - 1, lane, [&](int i) {
       return s_gam[i] * s_fnew[i] * (s_gnt[i + 1] - s_gnt[i]);
@@ -495,21 +852,25 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
     double The_new = Th_e;
     PF_BEGIN();
     if (gbar > g_av) {
+      int k = 0;
       while (gbar > g_av) {
+        const double prev = The_new;
         The_new = The_new * F32(1.005);
 #ifdef C2D_FP_PROF
         pf_calls++;
 #endif
-        g_av = gamma_bar_m(The_new);
+        g_av = search_eval(prev, The_new, +1, k++);
         if (guard > GUARD_MAX) break;
       }
     } else {
+      int k = 0;
       while (gbar < g_av) {
+        const double prev = The_new;
         The_new = The_new / F32(1.005);
 #ifdef C2D_FP_PROF
         pf_calls++;
 #endif
-        g_av = gamma_bar_m(The_new);
+        g_av = search_eval(prev, The_new, -1, k++);
         if (The_new < 1.0e-2) break;
         if (guard > GUARD_MAX) break;
       }
@@ -619,6 +980,29 @@ __global__ void __launch_bounds__(FPB) c2d_fp_kernel(const FpParams P) {
   }
 }
 
+/* One zone per workgroup of FP_WAVES waves.  Wave 0 runs FP_calc (its
+ * 200-bin state in LDS, one bin per lane); waves 1.. compute McDonald terms
+ * for it (mcd_producer).  Line numbers: src/update2d.f. */
+template <int WMAX>
+__global__ void __launch_bounds__(WMAX * FPB) c2d_fp_kernel(const FpParams P) {
+  /* wave-uniform by construction (readfirstlane): a scalar branch, so no
+   * wave ever steps through the other role's barriers with EXEC = 0 */
+  if (WMAX > 1) {
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x) / FPB;
+    if (wave != 0) {
+      mcd_producer(s_coop, s_batch8, P.mcd, wave, threadIdx.x % FPB);
+      return;
+    }
+  }
+  const int lane = threadIdx.x;
+  fp_zone_body<WMAX>(P, lane);
+  /* release the producers */
+  if (fp_nwaves<WMAX>() > 1) {
+    if (lane == 0) s_coop.cmd = MCD_CMD_EXIT;
+    __syncthreads();
+  }
+}
+
 }  // namespace c2d
 
 extern "C" int c2d_launch_tridag(const double* a, const double* b, const double* c,
@@ -631,8 +1015,27 @@ extern "C" int c2d_launch_tridag(const double* a, const double* b, const double*
   return (int)hipGetLastError();
 }
 
-extern "C" int c2d_launch_fp(const c2d::FpParams* P, int ncell, hipStream_t stream) {
+/* waves per zone: up to FP_WAVES_MAX while zone x waves stays near one wave
+ * per SIMD (C3: 270 zones -> 4 waves, 25 ms vs 29 ms with 8), down to 1
+ * (the single-wave series) once they fill the chip (1024 SIMDs on MI355X);
+ * C2D_FP_WAVES overrides (A/B runs) */
+extern "C" int c2d_fp_waves(int ncell, int n_simd) {
+  if (const char* e = getenv("C2D_FP_WAVES")) {
+    const int w = atoi(e);
+    if (w >= 1 && w <= c2d::FP_WAVES_MAX) return w;
+  }
+  int w = c2d::FP_WAVES_MAX;
+  while (w > 1 && (long long)ncell * w > 9LL * n_simd / 8) w /= 2;
+  return w;
+}
+
+extern "C" int c2d_launch_fp(const c2d::FpParams* P, int ncell, int waves, hipStream_t stream) {
   if (ncell <= 0) return 0;
-  hipLaunchKernelGGL(c2d::c2d_fp_kernel, dim3(ncell), dim3(64), 0, stream, *P);
+  if (waves < 1 || waves > c2d::FP_WAVES_MAX) return (int)hipErrorInvalidValue;
+  if (waves == 1)
+    hipLaunchKernelGGL(c2d::c2d_fp_kernel<1>, dim3(ncell), dim3(c2d::wave::FPB), 0, stream, *P);
+  else
+    hipLaunchKernelGGL(c2d::c2d_fp_kernel<c2d::FP_WAVES_MAX>, dim3(ncell), dim3(waves * c2d::wave::FPB),
+                       0, stream, *P);
   return (int)hipGetLastError();
 }

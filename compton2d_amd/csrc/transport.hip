@@ -280,7 +280,7 @@ __device__ __noinline__ double comtot_exact(const KParams& P, int cell, double x
 __device__ __forceinline__ double comtot_table(const KParams& P, int cell, const double xnu,
                                                const int tg, const double t) {
   if (tg == 0) return comtot_exact(P, cell, xnu);
-  const float* tb = P.comtab + (int64_t)cell * C2D_COMTAB_N + (tg - 1);
+  const double* tb = P.comtab + (int64_t)cell * C2D_COMTAB_N + (tg - 1);
   const double y0 = gld(tb), y1 = gld(tb + 1), y2 = gld(tb + 2), y3 = gld(tb + 3);
   const double tm1 = t - 1.0, tm2 = t - 2.0, tp1 = t + 1.0;
   const double cosig = -(t * tm1 * tm2) * (1.0 / 6.0) * y0 + (tp1 * tm1 * tm2) * 0.5 * y1 -
@@ -1375,7 +1375,7 @@ __global__ void __launch_bounds__(256) c2d_comtab_sigma(const double* gnt, doubl
 
 /* one 64x64 output tile per 256-thread block; K = 200 staged through LDS */
 __global__ void __launch_bounds__(256) c2d_comtab_gemm(const double* f_nt, const double* gnt,
-                                                       const double* S, float* tab, int ncell) {
+                                                       const double* S, double* tab, int ncell) {
   __shared__ double Ws[64][41];
   __shared__ double Ss[64][41];
   const int c0 = blockIdx.y * 64, g0 = blockIdx.x * 64;
@@ -1410,7 +1410,7 @@ __global__ void __launch_bounds__(256) c2d_comtab_gemm(const double* f_nt, const
 #pragma unroll
     for (int n = 0; n < 4; n++) {
       const int c = c0 + ty + 16 * m, gg = g0 + tx + 16 * n;
-      if (c < ncell && gg < C2D_COMTAB_N) tab[(int64_t)c * C2D_COMTAB_N + gg] = (float)acc[m][n];
+      if (c < ncell && gg < C2D_COMTAB_N) tab[(int64_t)c * C2D_COMTAB_N + gg] = acc[m][n];
     }
 }
 #endif
@@ -1451,7 +1451,7 @@ extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t
   return (int)hipGetLastError();
 }
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
-                                      float* tab, int ncell, hipStream_t stream) {
+                                      double* tab, int ncell, hipStream_t stream) {
   dim3 grid(C2D_COMTAB_N / 64, (ncell + 63) / 64);
   hipLaunchKernelGGL(c2d::c2d_comtab_gemm, grid, dim3(256), 0, stream, f_nt, gnt, S, tab, ncell);
   return (int)hipGetLastError();

@@ -114,6 +114,18 @@ def _unpack(rec):
     return rec[:, :6].copy(), rec[:, 6:11].astype(np.int32), keys
 
 
+def _comm_device(device):
+    """Tensors for the collectives live where the backend needs them: the
+    rank's GPU for nccl (RCCL), the host for gloo."""
+    if device is not None:
+        return device
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend() == "nccl":
+        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    return torch.device("cpu")
+
+
 def rebalance_census(d6, i5, keys, device=None):
     """Level the census record counts over the ranks (records as exported by
     Engine.census(): d6 [n,6], i5 [n,5], keys [n]).  Records move whole, so
@@ -126,6 +138,7 @@ def rebalance_census(d6, i5, keys, device=None):
     import torch
     import torch.distributed as dist
     rank, W = dist.get_rank(), dist.get_world_size()
+    device = _comm_device(device)
     n = len(keys)
     cnt = torch.tensor([n], dtype=torch.int64, device=device)
     allc = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(W)]
@@ -160,6 +173,7 @@ def rebalance_engine_census(engine, threshold: float = 0.1, device=None) -> bool
         return False
     import torch
     import torch.distributed as dist
+    device = _comm_device(device)
     n = engine.census_count()
     t = torch.tensor([float(n)], dtype=torch.float64, device=device)
     mx = t.clone()

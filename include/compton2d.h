@@ -111,7 +111,9 @@ typedef struct c2d_config {
   int32_t rank, world;            /* source sharding: this context tracks sources with
                                      (global source index % world) == rank       */
   int64_t census_capacity;        /* packets (per context)                     */
-  int64_t event_capacity;         /* escape events per step                    */
+  int64_t event_capacity;         /* escape events per step, >= C2D_EV_SHARDS (32): the
+                                     buffer is 32 equal shards, workgroup b appends to
+                                     shard b % 32, and a full shard is an overflow     */
   int64_t queue_capacity;         /* scatter records per generation            */
 } c2d_config;
 

@@ -49,7 +49,7 @@ int main(void) {
   P(c2d_fp_step_out, zone_diag) P(c2d_fp_step_out, dT_max) P(c2d_fp_step_out, p_nth)
   P(c2d_config, seed) P(c2d_config, rank) P(c2d_config, queue_capacity) P(c2d_config, mu)
   P(c2d_step_in, kappa_tot) P(c2d_step_in, nsv) P(c2d_step_in, tbbl) P(c2d_step_in, spectra)
-  P(c2d_step_in, n_spectra) P(c2d_step_in, dt)
+  P(c2d_step_in, n_spectra) P(c2d_step_in, dt) P(c2d_step_in, device_tables)
   printf("c2d_obs_bins %zu\nc2d_vem_in %zu\nc2d_vem_out %zu\n", sizeof(c2d_obs_bins),
          sizeof(c2d_vem_in), sizeof(c2d_vem_out));
   P(c2d_vem_in, ep_switch) P(c2d_vem_in, f_nt) P(c2d_vem_out, E_ph) P(c2d_vem_out, Eloss_tot)
@@ -103,3 +103,14 @@ def test_init_fails_loudly_without_gpu():
     with pytest.raises(engine.C2DError) as e:
         engine.Engine(GoldenCase("ssc_tau").grid())
     assert "C2D_E_HIP" in str(e.value)
+
+
+def test_init_rejects_event_capacity_below_shard_count():
+    """The escape-event buffer is C2D_EV_SHARDS (32) equal shards: a smaller
+    capacity would give every shard 0 slots: C2D_E_ARG before any
+    device call."""
+    from golden_io import GoldenCase
+    g = GoldenCase("ssc_tau").grid(event_capacity=31)
+    with pytest.raises(engine.C2DError) as e:
+        engine.Engine(g)
+    assert "C2D_E_ARG" in str(e.value)
