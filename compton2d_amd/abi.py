@@ -88,6 +88,7 @@ class StepIn(C.Structure):
     ]
 
 COMM_ID_BYTES = 128          # C2D_COMM_ID_BYTES
+CENSUS_REC_WORDS = 8         # C2D_CENSUS_REC_WORDS
 # c2d_step_in.device_tables (include/compton2d.h)
 DEV_EMISSION, DEV_ELECTRONS = 1, 2
 

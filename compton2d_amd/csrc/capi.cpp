@@ -933,6 +933,79 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
   return C2D_OK;
 }
 
+/* census SoA <-> packed 8-word records (C2D_CENSUS_REC_WORDS), bit-exact */
+__global__ void __launch_bounds__(256) c2d_census_pack_kernel(CensusSoA cs, int64_t first, int64_t n,
+                                                              uint64_t* __restrict__ rec) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = first + i;
+    uint64_t* r = rec + i * C2D_CENSUS_REC_WORDS;
+    r[0] = __double_as_longlong(cs.rpre[s]);
+    r[1] = __double_as_longlong(cs.zpre[s]);
+    r[2] = __double_as_longlong(cs.wmu[s]);
+    r[3] = __double_as_longlong(cs.phi[s]);
+    r[4] = __double_as_longlong(cs.ew[s]);
+    r[5] = __double_as_longlong(cs.xnu[s]);
+    r[6] = (uint64_t)cs.jk[s] | ((uint64_t)cs.bins[s] << 32);
+    r[7] = cs.key[s];
+  }
+}
+
+__global__ void __launch_bounds__(256) c2d_census_unpack_kernel(CensusSoA cs, int64_t first, int64_t n,
+                                                                const uint64_t* __restrict__ rec) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t d = first + i;
+    const uint64_t* r = rec + i * C2D_CENSUS_REC_WORDS;
+    cs.rpre[d] = __longlong_as_double(r[0]);
+    cs.zpre[d] = __longlong_as_double(r[1]);
+    cs.wmu[d] = __longlong_as_double(r[2]);
+    cs.phi[d] = __longlong_as_double(r[3]);
+    cs.ew[d] = __longlong_as_double(r[4]);
+    cs.xnu[d] = __longlong_as_double(r[5]);
+    cs.jk[d] = (uint32_t)(r[6] & 0xffffffffull);
+    cs.bins[d] = (uint32_t)(r[6] >> 32);
+    cs.key[d] = r[7];
+  }
+}
+
+extern "C" int c2d_census_pack(c2d_ctx* c, int64_t first, int64_t n, uint64_t* d_rec) {
+  if (!c || first < 0 || n < 0 || (n > 0 && !d_rec)) return C2D_E_ARG;
+  if (first + n > c->n_census)
+    return fail(c, C2D_E_ARG, "c2d_census_pack: records [%lld, %lld) beyond the census (%lld)",
+                (long long)first, (long long)(first + n), (long long)c->n_census);
+  if (n == 0) return C2D_OK;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 8);
+  hipLaunchKernelGGL(c2d_census_pack_kernel, dim3(grid), dim3(256), 0, c->stream,
+                     c->cens[c->cur_out].soa(), first, n, d_rec);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return C2D_OK;
+}
+
+extern "C" int c2d_census_append(c2d_ctx* c, const uint64_t* d_rec, int64_t n) {
+  if (!c || n < 0 || (n > 0 && !d_rec)) return C2D_E_ARG;
+  if (c->n_census + n > c->cfg.census_capacity)
+    return fail(c, C2D_E_CENSUS_OVERFLOW, "c2d_census_append: %lld + %lld > capacity %lld",
+                (long long)c->n_census, (long long)n, (long long)c->cfg.census_capacity);
+  if (n == 0) return C2D_OK;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 8);
+  hipLaunchKernelGGL(c2d_census_unpack_kernel, dim3(grid), dim3(256), 0, c->stream,
+                     c->cens[c->cur_out].soa(), c->n_census, n, d_rec);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->n_census += n;
+  return C2D_OK;
+}
+
+extern "C" int c2d_census_truncate(c2d_ctx* c, int64_t n) {
+  if (!c || n < 0 || n > c->n_census) return C2D_E_ARG;
+  c->n_census = n;
+  return C2D_OK;
+}
+
 extern "C" int c2d_fp_tridag(c2d_ctx* c, const c2d_fp_in* in, double* x) {
   if (!c || !in || !x || in->ncell < 0 || in->nt < 1) return C2D_E_ARG;
   if (in->ncell == 0) return C2D_OK;

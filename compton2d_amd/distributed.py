@@ -168,7 +168,11 @@ def rebalance_census(d6, i5, keys, device=None):
 
 def rebalance_engine_census(engine, threshold: float = 0.1, device=None) -> bool:
     """imcredist for an Engine: when the largest census exceeds the mean by
-    more than `threshold`, export, level and re-import (all ranks call it)."""
+    more than `threshold`, level the census counts (all ranks call it).  On
+    the nccl backend (RCCL) the records never leave the GPUs: the surplus tail
+    is packed on the device (c2d_census_pack), sent with RCCL send/recv and
+    appended on the receiving GPU (c2d_census_append); on gloo they go
+    through the host (export / import)."""
     if not is_dist():
         return False
     import torch
@@ -182,6 +186,43 @@ def rebalance_engine_census(engine, threshold: float = 0.1, device=None) -> bool
     mean = float(t.item()) / dist.get_world_size()
     if mean <= 0 or float(mx.item()) <= (1.0 + threshold) * mean:
         return False
-    d6, i5, keys = engine.census()
-    engine.import_census(*rebalance_census(d6, i5, keys, device=device))
+    if device.type == "cuda":
+        _rebalance_device(engine, device)
+    else:
+        d6, i5, keys = engine.census()
+        engine.import_census(*rebalance_census(d6, i5, keys, device=device))
     return True
+
+
+def _rebalance_device(engine, device) -> None:
+    """Level the census over the ranks with packed device records and RCCL
+    point-to-point transfers (replaces imcredist's master-relayed MPI copies,
+    src/imcredist.f:18-123)."""
+    import torch
+    import torch.distributed as dist
+    from . import abi
+    rank, W = dist.get_rank(), dist.get_world_size()
+    n = engine.census_count()
+    cnt = torch.tensor([n], dtype=torch.int64, device=device)
+    allc = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(W)]
+    dist.all_gather(allc, cnt)
+    plan = rebalance_plan([int(c.item()) for c in allc])
+    keep = n - sum(m for s, _, m in plan if s == rank)
+    ops, recvs, off = [], [], keep
+    for s, d, m in plan:
+        if s == rank:
+            t = torch.empty((m, abi.CENSUS_REC_WORDS), dtype=torch.int64, device=device)
+            engine.census_pack(off, m, t.data_ptr())        # synchronous on the engine's stream
+            off += m
+            ops.append(dist.P2POp(dist.isend, t, d))
+        elif d == rank:
+            t = torch.empty((m, abi.CENSUS_REC_WORDS), dtype=torch.int64, device=device)
+            recvs.append(t)
+            ops.append(dist.P2POp(dist.irecv, t, s))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    torch.cuda.synchronize(device)
+    engine.census_truncate(keep)
+    for t in recvs:
+        engine.census_append(t.data_ptr(), t.shape[0])

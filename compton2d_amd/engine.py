@@ -81,6 +81,12 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_census_export_range.argtypes = [vp, C.c_int64, C.c_int64, C.POINTER(C.c_double),
                                             C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.c_int64,
                                             C.POINTER(C.c_int64)]
+    lib.c2d_census_pack.restype = C.c_int
+    lib.c2d_census_pack.argtypes = [vp, C.c_int64, C.c_int64, C.c_void_p]
+    lib.c2d_census_append.restype = C.c_int
+    lib.c2d_census_append.argtypes = [vp, C.c_void_p, C.c_int64]
+    lib.c2d_census_truncate.restype = C.c_int
+    lib.c2d_census_truncate.argtypes = [vp, C.c_int64]
     lib.c2d_census_import.restype = C.c_int
     lib.c2d_census_import.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32),
                                       C.POINTER(C.c_uint64), C.c_int64]
@@ -240,6 +246,18 @@ class Engine:
             i5.ctypes.data_as(C.POINTER(C.c_int32)), keys.ctypes.data_as(C.POINTER(C.c_uint64)),
             m, C.byref(n)))
         return d6[:m], i5[:m], keys[:m]
+
+    # -- device-resident census records (C2D_CENSUS_REC_WORDS u64 each) ------
+    def census_pack(self, first: int, n: int, d_ptr: int) -> None:
+        """Pack records [first, first+n) into device memory at d_ptr."""
+        self._check(self.lib.c2d_census_pack(self.ctx, int(first), int(n), C.c_void_p(d_ptr)))
+
+    def census_append(self, d_ptr: int, n: int) -> None:
+        """Append n packed records from device memory at d_ptr."""
+        self._check(self.lib.c2d_census_append(self.ctx, C.c_void_p(d_ptr), int(n)))
+
+    def census_truncate(self, n: int) -> None:
+        self._check(self.lib.c2d_census_truncate(self.ctx, int(n)))
 
     def import_census(self, d6, i5, keys) -> None:
         d6 = np.ascontiguousarray(d6, np.float64)

@@ -366,6 +366,18 @@ int  c2d_census_export(c2d_ctx* ctx, double* d6, int32_t* i5, uint64_t* keys,
                        int64_t cap, int64_t* n);
 int  c2d_census_import(c2d_ctx* ctx, const double* d6, const int32_t* i5,
                        const uint64_t* keys, int64_t n);
+/* Census records in device memory, for moving census between GPUs without
+ * the host (imcredist, src/imcredist.f:5-133, as RCCL send/recv or
+ * hipMemcpyPeer of packed records): C2D_CENSUS_REC_WORDS 64-bit words per
+ * record = rpre, zpre, wmu, phi, ew, xnu (f64 bits), jk | bins << 32, key. */
+#define C2D_CENSUS_REC_WORDS 8
+/* pack records [first, first+n) into d_rec (device memory of this context's GPU) */
+int  c2d_census_pack(c2d_ctx* ctx, int64_t first, int64_t n, uint64_t* d_rec);
+/* append n packed records (device memory) to the census */
+int  c2d_census_append(c2d_ctx* ctx, const uint64_t* d_rec, int64_t n);
+/* keep the first n records (drop the tail, e.g. after packing it for a send) */
+int  c2d_census_truncate(c2d_ctx* ctx, int64_t n);
+
 /* Records first, first+stride, ... (at most cap of them) of the census:
  * checkpoints in chunks, or a strided sample of a large census. */
 int  c2d_census_export_range(c2d_ctx* ctx, int64_t first, int64_t stride, double* d6,

@@ -1,36 +1,67 @@
 """Checkpoint / restart through the reference's census record files
-(write_record -> write_cens, read_record -> read_cens, src/census2d.f):
-a context restarted from the file continues the same histories.  With the
-key file the lineage keys are exact; the 6 doubles lose precision to e14.7
-exactly as the reference's restart does, so the next step's tallies agree to
-the level of that truncation (a few census decisions may flip)."""
+(write_record -> write_cens, read_record -> read_cens, src/census2d.f;
+the record text format is pinned to the reference's own write_cens in
+tests/test_census_io.py).
+
+A run writes its census after step 0; a fresh GPU context and the oracle
+both restart from that same file (e14.7 doubles + the exact lineage keys of
+the .keys file) and run step 1 on the same inputs: the exact kernel's
+histories equal the oracle's bit for bit (counters, census records sorted by
+key, escape events); f64 tallies to the atomic summation order.  A second
+check keeps the old property: the restarted run stays within the e14.7
+truncation of the uninterrupted one."""
 import numpy as np
 import pytest
 
-from compton2d_amd import abi
+import oracle_lib as OL
+from compton2d_amd import abi, census_io
 from compton2d_amd.engine import Engine
 from golden_io import GoldenCase
 
 pytestmark = pytest.mark.gpu
 
+TALLY_KEYS = ("edep", "prdep", "ecens", "npcen", "n_field", "E_IC", "nelectron", "fout", "edout",
+              "erlki", "erlko", "erlku", "erlkl", "Ed_in")
 
-def test_restart_from_census_file(tmp_path):
-    gc = GoldenCase("ssc_tau")
+
+def sort_rows(a):
+    return a[np.lexsort(a.T[::-1])] if len(a) else a
+
+
+@pytest.mark.parametrize("name", ["ssc_tau", "c3_mrk421"])
+def test_restart_from_census_file_matches_oracle(tmp_path, name):
+    gc = GoldenCase(name)
     a = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, kappa_lag=0))
     a.transport_step(gc.step_inputs(0))
-    n = a.save_census(tmp_path / "p001_census.dat")
+    path = tmp_path / "p001_census.dat"
+    n = a.save_census(path)
     assert n == a.census_count() > 0
     b = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, kappa_lag=0))
-    assert b.load_census(tmp_path / "p001_census.dat") == n
+    assert b.load_census(path) == n
+    o = OL.Oracle(gc.grid(kappa_lag=0), OL.RNG_LINEAGE, "det")
+    assert o.import_census(*census_io.read_census(path)) == 0
     si = gc.step_inputs(1)
-    a.transport_step(si)
     b.transport_step(si)
-    ta, tb = a.tallies(), b.tallies()
+    assert o.step(si) == 0
+    tb, to = b.tallies(), o.split()
+    np.testing.assert_array_equal(tb["counters"][:8], to["counters"][:8])   # GENS is GPU-only
+    for k in TALLY_KEYS:
+        ref = np.asarray(to[k])
+        np.testing.assert_allclose(tb[k], ref, rtol=1e-11, atol=1e-13 * max(np.abs(ref).max(), 1e-300),
+                                   err_msg=k)
+    d6b, i5b, kb = b.census()
+    d6o, i5o, ko = o.census()
+    ob, oo = np.argsort(kb), np.argsort(ko)
+    np.testing.assert_array_equal(kb[ob], ko[oo])
+    np.testing.assert_array_equal(d6b[ob], d6o[oo])
+    np.testing.assert_array_equal(i5b[ob], i5o[oo])
+    np.testing.assert_array_equal(sort_rows(b.events()), sort_rows(o.events()))
+    # the uninterrupted run differs only through the e14.7 truncation
+    a.transport_step(si)
+    ta = a.tallies()
     for k in (abi.CNT_SOURCES, abi.CNT_STEPS, abi.CNT_CENSUS, abi.CNT_ESCAPES):
         x, y = ta["counters"][k], tb["counters"][k]
         assert abs(x - y) <= 1e-3 * x + 2, (k, x, y)
-    for k in ("edep", "ecens", "fout"):
-        x, y = np.sum(ta[k]), np.sum(tb[k])
-        assert abs(x - y) <= 1e-3 * abs(x), (k, x, y)
-    a.close()
-    b.close()
+    for e in (a, b):
+        e.close()
+    o.close()
