@@ -62,3 +62,33 @@ def test_fast_kernel_spectrum_within_1pct_of_reference_cpu_path(kappa_lag):
     # light curves (lcb_NN.dat, src/graphics2d.f:170-200) and the census energy too
     assert rel_l2(tg["edout"].ravel(), to["edout"].ravel()) <= 1e-2
     assert abs(tg["ecens"].sum() - to["ecens"].sum()) <= 1e-2 * to["ecens"].sum()
+
+
+def test_fast_kernel_spectrum_vs_reference_stream_fixture():
+    """The production kernel (tabulated comtot, Philox lineage streams) on the
+    north-star spectrum workload (tests/spectrum_case.py, 1e7 packets: ~9.5e6
+    escapes) against the reference algorithm WITH the reference's own
+    lagged-Fibonacci streams (tests/golden/spectrum_fib.npz: 3 seeds x 1.9e6
+    escapes, C oracle bit-exact to the Fortran, regenerated and checked in
+    tests/test_spectrum_rng.py): F(E) relative L2 <= 1 %, the synchrotron
+    light-curve bands to 1 %."""
+    from pathlib import Path
+    import spectrum_case as S
+    fx = np.load(Path(__file__).resolve().parent / "golden" / "spectrum_fib.npz", allow_pickle=False)
+    grid, si = S.workload(mode=abi.COMTOT_TABLE, n=S.LINEAGE_SOURCES)
+    eng = Engine(grid)
+    eng.transport_step(si)
+    t = eng.tallies()
+    eng.close()
+    assert t["counters"][abi.CNT_ESCAPES] >= 5e6 and t["counters"][abi.CNT_ABORTED] == 0
+    F_ref = fx["F"].mean(axis=0)
+    d = S.rel_l2(S.f_of_e(t["fout"]), F_ref)
+    floor = [S.rel_l2(fx["F"][a], fx["F"][b]) for a, b in ((0, 1), (0, 2), (1, 2))]
+    print("F(E) rel L2 fast kernel (%.3g escapes) vs reference streams: %.4f (reference floor %s)" % (
+        t["counters"][abi.CNT_ESCAPES], d, floor))
+    assert d <= 1e-2, d
+    E = np.asarray(t["edout"]).ravel()
+    E_ref = fx["edout"].mean(axis=0)
+    for i in range(E_ref.size):
+        if E_ref[i] > 0 and fx["edout"][:, i].std(ddof=1) < 2e-3 * E_ref[i]:
+            assert abs(E[i] - E_ref[i]) <= 1e-2 * E_ref[i], (i, E[i], E_ref[i])

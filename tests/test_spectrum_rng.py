@@ -1,55 +1,78 @@
-"""The RNG swap is statistically neutral: the reference's algorithm (C oracle,
-glibc libm) run with the reference's own lagged-Fibonacci zone streams
-(rand.f, rand_switch=1; bit-exact to the Fortran reference, see
-tests/test_oracle_golden.py) and with the engine's per-packet Philox lineage
-streams gives escaping spectra F(E) that differ by no more than reference runs
-with different seeds differ among themselves (the reference's
-own seed-to-seed floor).  F(E) is heavy-tailed (rare large-gain inverse-Compton
-packets), so the comparison uses 3 seeds per generator: mean pairwise L2 across
-generators vs within a generator, and medians of the escaping and census
-energies.  Inputs: the thin inputm.dat medium (compton2d_amd/synth.py), 2x2
-zones, one MC step with ncycle = 1, 1e5 volume packets."""
+"""North-star spectrum criterion on the CPU: <= 1 % relative
+L2 on F(E) of spb.dat between the reference's algorithm with the reference's
+own lagged-Fibonacci streams (C oracle, glibc, rand_switch = 1: bit-exact to
+the Fortran reference, tests/test_oracle_golden.py) and the same algorithm
+with the engine's per-packet Philox lineage streams — the RNG swap the GPU
+makes — with the reference's own seed-to-seed floor reported beside it.
+Reference side: 3 seeds x ~1.9e6 escapes, averaged; lineage side: ~9.5e6
+escapes (tests/spectrum_case.py).  Same for the light curves (edout).
+
+The three fib runs are recomputed here and must equal the committed fixture
+(tests/golden/spectrum_fib.npz, which the GPU test compares the fast kernel
+against) bit for bit; the lineage run is sharded over processes by source
+lineage (sums are the single-process run's to rounding).
+"""
 import itertools
 from multiprocessing import get_context
+from pathlib import Path
 
 import numpy as np
 
 import oracle_lib as OL
-from compton2d_amd import abi, synth
+import spectrum_case as S
 
-SEEDS = (9857, 24680, 13579)
-
-
-def run(args):
-    mode, seed, n = args
-    wl = synth.c2_workload(nz=2, nr=2, sources=n, comtot_mode=abi.COMTOT_EXACT,
-                           census_capacity=4 * n, event_capacity=4 * n, seed=seed)
-    wl.grid.kappa_lag = 0
-    si = wl.step0
-    si.ncycle = 1
-    o = OL.Oracle(wl.grid, mode, "ref", rseed=seed)
-    assert o.step(si) == 0
-    t = o.split()
-    o.close()
-    de = np.diff(synth.photon_grid())
-    return t["fout"][0, :de.size] / de, float(t["fout"].sum()), float(t["ecens"].sum())
+FIX = Path(__file__).resolve().parent / "golden" / "spectrum_fib.npz"
+SHARDS = 8
 
 
-def rel_l2(a, b):
-    s = max(np.abs(a).max(), np.abs(b).max())
-    m = (np.abs(a) > 1e-20 * s) | (np.abs(b) > 1e-20 * s)
-    return float(np.linalg.norm(a[m] - b[m]) / np.linalg.norm(b[m]))
-
-
-def test_lineage_rng_within_reference_seed_noise():
-    jobs = [(OL.RNG_FIB, s, 100_000) for s in SEEDS] + [(OL.RNG_LINEAGE, s, 100_000) for s in SEEDS]
+def test_lineage_rng_spectrum_within_1pct_of_reference_streams(capsys):
     OL.build()
-    with get_context("spawn").Pool(len(jobs)) as pool:
-        res = pool.map(run, jobs)
+    jobs = [("fib", s) for s in S.FIB_SEEDS] + [("lineage", S.LINEAGE_SEED, r, SHARDS)
+                                                for r in range(SHARDS)]
+    with get_context("spawn").Pool(8) as pool:
+        res = pool.map(S.oracle_run, jobs)
     fib, lin = res[:3], res[3:]
-    within = [rel_l2(a[0], b[0]) for grp in (fib, lin) for a, b in itertools.combinations(grp, 2)]
-    cross = [rel_l2(a[0], b[0]) for a in fib for b in lin]
-    assert np.mean(cross) <= 2.0 * np.mean(within), (cross, within)
-    med = lambda grp, k: float(np.median([r[k] for r in grp]))
-    assert abs(med(lin, 1) - med(fib, 1)) <= 0.03 * med(fib, 1)      # escaping energy
-    assert abs(med(lin, 2) - med(fib, 2)) <= 0.01 * med(fib, 2)      # census energy
+    fx = np.load(FIX, allow_pickle=False)
+    for i, r in enumerate(fib):                       # the fixture is this computation
+        np.testing.assert_array_equal(r[0], fx["F"][i])
+        np.testing.assert_array_equal(r[1], fx["edout"][i])
+    # the lineage run: the per-packet streams scale the weights by 1/(sources)
+    # through ewsv, so the sharded sum is F(E) of 1e7 packets at the same
+    # normalisation as one 2e6-packet reference run
+    F_lin = sum(r[0] for r in lin)
+    E_lin = sum(r[1] for r in lin)
+    esc_lin = sum(r[2] for r in lin)
+    F_ref = np.mean([r[0] for r in fib], axis=0)
+    E_ref = np.mean([r[1] for r in fib], axis=0)
+    assert min(r[2] for r in fib) >= 1.0e6 and esc_lin >= 5.0e6
+    cross = S.rel_l2(F_lin, F_ref)
+    floor = [S.rel_l2(a[0], b[0]) for a, b in itertools.combinations(fib, 2)]
+    # light curves per band (lcb_01.dat columns): the bands the reference
+    # reproduces between seeds to < 0.2 % at this size (the two synchrotron
+    # bands) carry the 1 % bound; the Compton bands are a few rare large-gain
+    # packets (~3 collisions per 1e6 packets in this thin medium; reference
+    # scatter 50-90 % between seeds at 2e6 packets) and must agree within
+    # that scatter.  (At n_e x 5e4 the two generators' collision counts agree
+    # to their Poisson noise: 14325 vs 14370 per 1e5 packets, 4 seeds each.)
+    E_all = np.array([r[1] for r in fib])
+    bands = [i for i in range(E_all.shape[1]) if E_all[:, i].min() > 0]
+    lc = []
+    for i in bands:
+        sd = E_all[:, i].std(ddof=1) / E_ref[i]
+        dev = abs(E_lin[i] - E_ref[i]) / E_ref[i]
+        lc.append((i, dev, sd))
+    with capsys.disabled():
+        print("\nF(E) rel L2, lineage (%.3g escapes) vs reference streams (3 x %.3g): %.4f; "
+              "reference seed-to-seed floor (pairs of %.3g): %s" % (
+                  esc_lin, fib[0][2], cross, fib[0][2], ["%.4f" % x for x in floor]))
+        print("light curves per band (band, |dev|, reference seed scatter): %s" %
+              ["(%d, %.4f, %.4f)" % x for x in lc])
+    assert cross <= 1.0e-2, cross
+    for i, dev, sd in lc:
+        if sd < 2.0e-3:
+            assert dev <= 1.0e-2, (i, dev, sd)
+        else:
+            assert dev <= 4.0 * sd * np.sqrt(1.0 / 3 + 1.0 / 5), (i, dev, sd)
+    # no bias beyond the noise: the larger-sample comparison is no further
+    # apart than two reference runs of 2e6 packets are from each other
+    assert cross <= max(floor), (cross, floor)

@@ -15,6 +15,9 @@ import os
 import sys
 from statistics import mean
 
+CLOCK = 2.4e9          # MI355X engine clock
+N_SIMD = 1024          # 256 CUs x 4 SIMDs
+
 
 def find(d, suffix):
     f = glob.glob(os.path.join(d, "**", "*" + suffix), recursive=True)
@@ -101,6 +104,36 @@ def main(root):
         wb = wk * 1024.0 / res["write"]["steps"]
         res["hbm_bytes_per_step"] = fb + wb
         print("HBM bytes per packet-step: fetch(x2) %.2f + write %.2f = %.2f" % (fb, wb, fb + wb))
+    # the FP kernel (c2d_fp_kernel<W>): last dispatch of each pass
+    fp = {}
+    for sub in ("fetch", "write", "sq"):
+        f = find(os.path.join(root, sub), "kernel_trace.csv")
+        if not f:
+            continue
+        rows = [r for r in dispatches(f) if "c2d_fp_kernel" in r["Kernel_Name"]]
+        if not rows:
+            continue
+        r = rows[-1]
+        ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        c = counters(os.path.join(root, sub), r["Dispatch_Id"])
+        fp[sub] = {"ms": ms, "counters": c, "grid": r.get("Grid_Size_X"),
+                   "workgroup": r.get("Workgroup_Size_X"), "vgpr": r.get("VGPR_Count"),
+                   "lds": r.get("LDS_Block_Size")}
+        print("[fp %s] dispatch %s: %.3f ms grid %s wg %s counters %s" % (
+            sub, r["Dispatch_Id"], ms, r.get("Grid_Size_X"), r.get("Workgroup_Size_X"), c))
+    if "sq" in fp:
+        c, ms = fp["sq"]["counters"], fp["sq"]["ms"]
+        w = c.get("SQ_WAVE_CYCLES", 0.0)
+        waves = int(fp["sq"]["grid"] or 0) // 64
+        # a wave64 VALU instruction issues over 4 cycles on a 16-lane SIMD:
+        # fraction of the chip's VALU issue slots used during the kernel
+        res["fp_valu_issue_frac"] = c.get("SQ_INSTS_VALU", 0.0) * 4.0 / (ms * 1e-3 * CLOCK * N_SIMD)
+        res["fp_wait_frac"] = c.get("SQ_WAIT_ANY", 0.0) / w if w else None
+        res["fp_waves"] = waves
+        res["fp_simd_occupancy"] = waves / float(N_SIMD)
+        print("FP kernel: %.3f ms, %d waves (%.2f per SIMD), VALU issue %.3f of the chip, wait_any %.3f" % (
+            ms, waves, waves / float(N_SIMD), res["fp_valu_issue_frac"], res["fp_wait_frac"] or 0))
+    res["fp"] = fp
     if "sq" in res:
         c = res["sq"]["counters"]
         w = c.get("SQ_WAVE_CYCLES", 0.0)
@@ -110,6 +143,10 @@ def main(root):
                 c.get("SQ_ACTIVE_INST_ANY", 0) / w, c.get("SQ_ACTIVE_INST_VALU", 0) / w))
             st = res["sq"]["steps"]
             if st:
+                res["valu_wave_insts_per_step"] = c.get("SQ_INSTS_VALU", 0) / st
+                res["transport_valu_issue_frac"] = (c.get("SQ_INSTS_VALU", 0) * 4.0 /
+                                                    (res["sq"]["ms"] * 1e-3 * CLOCK * N_SIMD))
+                print("transport VALU issue: %.3f of the chip's VALU slots" % res["transport_valu_issue_frac"])
                 print("per packet-step: VALU insts %.1f  SALU %.1f  VMEM %.2f (wave-instructions x64 / steps)" % (
                     64 * c.get("SQ_INSTS_VALU", 0) / st, 64 * c.get("SQ_INSTS_SALU", 0) / st,
                     64 * c.get("SQ_INSTS_VMEM", 0) / st))
