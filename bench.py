@@ -347,7 +347,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "c2d_transport_kernel_%s (generation 0)" % args.mode,
+            "kernel": "c2d_bundle_kernel_%s (generation 0)" % args.mode,
             "per_unit_bytes": BYTES_PER_STEP,
             "kernel_ms_avg": g0_ms / args.steps,
             "traffic_unit": "bytes per launch (PMC FETCH_SIZEx2 + WRITE_SIZE), from %s" %

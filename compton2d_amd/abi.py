@@ -23,6 +23,7 @@ NFMAX = 500
 MAXZONE = 99
 EVENT_WORDS = 7
 NCOUNTERS = 16
+TR_PROF_WORDS = 32                 # C2D_TR_PROF_WORDS (c2d_transport_prof)
 
 COMTOT_EXACT = 0
 COMTOT_TABLE = 1

@@ -75,6 +75,10 @@ struct TallyOff {
  * counter).  Readers take the shards' filled prefixes in shard order. */
 #define C2D_EV_SHARDS 32
 #define C2D_EV_SHARD_STRIDE 16
+/* generation-0 work items are split into C2D_WORK_SHARDS contiguous ranges,
+ * each with its own fetch counter (one per 128-B line); a workgroup starts
+ * on shard blockIdx % C2D_WORK_SHARDS and moves on when it is exhausted */
+#define C2D_WORK_SHARDS 64
 
 #ifndef C2D_COMTAB_N
 #define C2D_COMTAB_N 2048
@@ -162,6 +166,10 @@ struct KParams {
   unsigned long long* cnt;  /* [C2D_NCOUNTERS] */
   int32_t* err;
   int32_t lds_cells;        /* 1: cell tallies privatised in LDS */
+  unsigned long long* prof;  /* [C2D_TR_PROF_WORDS] section counters (-DC2D_TR_PROF builds) */
+  int32_t rn_lds;           /* bundle kernel: probes' second Philox halves kept in LDS */
+  int32_t rn_off;           /* ... at this double offset of the dynamic LDS            */
+  unsigned long long* cens_holes; /* bundle kernel: per wave (start, length) of its census hole */
 };
 
 /* Per-launch arguments (passed by value; KParams stays constant over a step). */
@@ -174,6 +182,7 @@ struct GenArgs {
   unsigned long long* n3_out;
   unsigned long long* n_pk;        /* scatter: secondaries written; transport: item count */
   unsigned long long* work_counter;
+  unsigned long long* work_sh;     /* bundle kernel: C2D_WORK_SHARDS counters, stride 16 */
   int64_t item_begin, item_end;    /* scatter kernel item range                   */
   int64_t n_items;                 /* transport, generation 0: census + sources    */
   int64_t n2_in, n3_in;

@@ -55,15 +55,27 @@ C2D_RHD uint32_t c2d_mulhi32(uint32_t a, uint32_t b) {
 /* Philox4x32-10 (Salmon et al., SC'11). */
 C2D_RHD void c2d_philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#ifndef C2D_PHILOX_MAD
+#define C2D_PHILOX_MAD 0
+#endif
 #ifndef C2D_PHILOX_ROUNDS
 #define C2D_PHILOX_ROUNDS 10
 #endif
 #pragma unroll
   for (int r = 0; r < C2D_PHILOX_ROUNDS; ++r) {
+#if C2D_PHILOX_MAD
+    /* one 32x32->64 product per multiplier (a single v_mad_u64_u32 on CDNA
+     * instead of separate mul_hi / mul_lo) */
+    const uint64_t p0 = (uint64_t)M0 * (uint64_t)c[0];
+    const uint64_t p1 = (uint64_t)M1 * (uint64_t)c[2];
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
+#else
     uint32_t hi0 = c2d_mulhi32(M0, c[0]), lo0 = M0 * c[0];
     uint32_t hi1 = c2d_mulhi32(M1, c[2]), lo1 = M1 * c[2];
     uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
     c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+#endif
     k0 += W0; k1 += W1;
   }
 }

@@ -32,6 +32,13 @@ extern "C" int c2d_launch_scatter_exact(const KParams* P, const GenArgs* A, int 
 extern "C" int c2d_launch_scatter_fast(const KParams* P, const GenArgs* A, int grid, hipStream_t s);
 extern "C" int c2d_transport_occupancy_exact(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds);
+extern "C" int c2d_launch_bundle_exact(const KParams* P, const GenArgs* A, int grid, size_t lds,
+                                       hipStream_t s);
+extern "C" int c2d_launch_bundle_fast(const KParams* P, const GenArgs* A, int grid, size_t lds,
+                                      hipStream_t s);
+extern "C" int c2d_bundle_occupancy_exact(int* blocks_per_cu, size_t lds);
+extern "C" int c2d_bundle_occupancy_fast(int* blocks_per_cu, size_t lds);
+extern "C" int c2d_launch_census_move(CensusSoA c, const long long* moves, int n, hipStream_t s);
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t s);
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
                                       double* tab, int ncell, hipStream_t s);
@@ -49,7 +56,9 @@ namespace {
 
 /* CTL_EVSH: the C2D_EV_SHARDS event counters, one per 128-B line */
 enum { CTL_WORK = 0, CTL_NCOUT = 1, CTL_N2 = 3, CTL_N3 = 4, CTL_NPK = 5, CTL_CNT = 8,
-       CTL_EVSH = 32, CTL_WORDS = CTL_EVSH + C2D_EV_SHARDS * C2D_EV_SHARD_STRIDE };
+       CTL_EVSH = 32, CTL_PROF = CTL_EVSH + C2D_EV_SHARDS * C2D_EV_SHARD_STRIDE,
+       CTL_WSH = CTL_PROF + C2D_TR_PROF_WORDS,
+       CTL_WORDS = CTL_WSH + C2D_WORK_SHARDS * C2D_EV_SHARD_STRIDE };
 
 /* the packet store (c2d_device.hpp PktSoA) */
 struct DevPk {
@@ -101,6 +110,13 @@ struct c2d_ctx {
   int n_cu = 0, max_grid = 0, lds_cells = 0;
   size_t lds_max = 64 * 1024;   /* LDS bytes a workgroup may allocate */
   size_t lds_bytes = 0;
+  /* generation 0 as probe bundles (c2d_bundle_kernel; C2D_BUNDLE=0: the
+   * per-copy tracker), its LDS with the probes' Philox halves, and grid */
+  int bundle = 1, rn_lds = 0, bundle_grid = 0;
+  size_t bundle_lds = 0;
+  unsigned long long* cens_holes = nullptr;   /* [bundle waves][2]: census chunk tails */
+  long long* cens_moves = nullptr;            /* [2 * bundle waves][3]: src, dst, n     */
+  std::vector<unsigned long long> h_holes;
   c2d_tally_layout L;
   /* device buffers */
   Geo* geo = nullptr;
@@ -143,6 +159,7 @@ struct c2d_ctx {
   std::vector<double> h_stage;
   double last_g0_ms = 0.0, last_all_ms = 0.0;
   float last_src_ms = 0.f;
+  unsigned long long last_prof[C2D_TR_PROF_WORDS] = {};  /* transport section counters */
   int64_t last_g0_steps = 0;
   int last_launches = 0;
   /* Fokker-Planck */
@@ -305,6 +322,26 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
                 : c2d_transport_occupancy_exact(&blocks_per_cu, c->lds_bytes);
   if (orc) return fail(c, C2D_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)orc));
   c->max_grid = c->n_cu * std::max(1, blocks_per_cu);
+  {
+    const char* e = getenv("C2D_BUNDLE");
+    c->bundle = (e && e[0] == '0') ? 0 : 1;
+    auto occ = cfg->comtot_mode == C2D_COMTOT_TABLE ? c2d_bundle_occupancy_fast
+                                                    : c2d_bundle_occupancy_exact;
+    int b0 = 0, b1 = 0;
+    const size_t rn = sizeof(double) * (size_t)std::min(cfg->split1, 32) * 512;
+    orc = occ(&b0, c->lds_bytes);
+    if (!orc) orc = occ(&b1, c->lds_bytes + rn);
+    if (orc) return fail(c, C2D_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)orc));
+    /* keep the probes' second halves in LDS only where that costs no occupancy */
+    const char* r = getenv("C2D_RN_LDS");
+    c->rn_lds = r ? (r[0] != '0') : (b1 >= b0 && b1 > 0);
+    c->bundle_lds = c->lds_bytes + (c->rn_lds ? rn : 0);
+    c->bundle_grid = c->n_cu * std::max(1, c->rn_lds ? b1 : b0);
+    const size_t waves = (size_t)c->bundle_grid * 8;
+    HIPCHK(c, dalloc(&c->cens_holes, 2 * waves));
+    HIPCHK(c, dalloc(&c->cens_moves, 6 * waves + 6));
+    c->h_holes.assign(2 * waves, 0ull);
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return C2D_OK;
 }
@@ -318,7 +355,8 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
   void* ptrs[] = {c->geo, c->gnt, c->kappa_cur, c->kappa_prev, c->eps_tot, c->eps_th, c->f_nt,
                   c->Pnt, c->n_e, c->vfrac, c->ewsv, c->surf_ew, c->surf_tbb, c->tbbl,
                   c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comS,
-                  c->ev, c->q2[0], c->q2[1], c->q3[0], c->q3[1], c->T_own, c->nf_rep, c->ctl, c->derr, c->dP};
+                  c->ev, c->q2[0], c->q2[1], c->q3[0], c->q3[1], c->T_own, c->nf_rep, c->ctl, c->derr, c->dP,
+                  c->cens_holes, c->cens_moves};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int b = 0; b < 2; b++) {
@@ -613,6 +651,10 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.cnt = c->ctl + CTL_CNT;
   P.err = c->derr;
   P.lds_cells = c->lds_cells;
+  P.prof = c->ctl + CTL_PROF;
+  P.rn_lds = c->rn_lds;
+  P.rn_off = (int32_t)(c->lds_bytes / sizeof(double));
+  P.cens_holes = c->cens_holes;
   P.n_vol_global = c->n_vol_global;
   P.n_surf_global = c->n_surf_global;
   /* this rank's share of the global source index space (lineage-sharded) */
@@ -647,6 +689,9 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   HIPCHK(c, hipMemsetAsync(c->nf_rep, 0, sizeof(double) * C2D_NF_REPL * c->ncell * C2D_NPHFIELD,
                            c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl, 0, sizeof(unsigned long long) * CTL_WORDS, c->stream));
+  if (c->cens_holes)
+    HIPCHK(c, hipMemsetAsync(c->cens_holes, 0, sizeof(unsigned long long) * c->h_holes.size(),
+                             c->stream));
   HIPCHK(c, hipMemsetAsync(c->derr, 0, sizeof(int32_t), c->stream));
 
   const bool fast = cfg.comtot_mode == C2D_COMTOT_TABLE;
@@ -679,8 +724,16 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     A.n2_out = c->ctl + CTL_N2; A.n3_out = c->ctl + CTL_N3;
     A.n_pk = c->ctl + CTL_NPK;
     A.work_counter = c->ctl + CTL_WORK;
+    A.work_sh = c->ctl + CTL_WSH;
     HIPCHK(c, hipEventRecord(c->ev_g0t, c->stream));
-    if (A.n_items > 0) {
+    if (A.n_items > 0 && c->bundle) {
+      auto launch_b = fast ? c2d_launch_bundle_fast : c2d_launch_bundle_exact;
+      const int grid = (int)std::max<int64_t>(
+          1, std::min<int64_t>(c->bundle_grid, (A.n_items + 511) / 512));
+      int rc = launch_b(c->dP, &A, grid, c->bundle_lds, c->stream);
+      if (rc) return fail(c, C2D_E_HIP, "bundle launch (gen 0): %s", hipGetErrorString((hipError_t)rc));
+      launches++;
+    } else if (A.n_items > 0) {
       int rc = launch_tr(c->dP, &A, tr_grid(A.n_items), c->lds_bytes, c->stream);
       if (rc) return fail(c, C2D_E_HIP, "transport launch (gen 0): %s", hipGetErrorString((hipError_t)rc));
       launches++;
@@ -725,6 +778,65 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     gen++;
   }
+  /* close the holes the bundle kernel's census chunks left (census stays dense) */
+  int64_t cens_dense = -1;
+  if (c->bundle && c->cens_holes) {
+    unsigned long long reserved = 0;
+    HIPCHK(c, hipMemcpyAsync(&reserved, c->ctl + CTL_NCOUT, sizeof reserved, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_holes.data(), c->cens_holes,
+                             sizeof(unsigned long long) * c->h_holes.size(), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<std::pair<int64_t, int64_t>> holes;
+    int64_t nh = 0;
+    for (size_t w = 0; w + 1 < c->h_holes.size(); w += 2) {
+      const int64_t a0 = (int64_t)c->h_holes[w], n = (int64_t)c->h_holes[w + 1];
+      if (n <= 0) continue;
+      holes.emplace_back(a0, n);
+      nh += n;
+    }
+    const int64_t R = (int64_t)reserved, W = R - nh;
+    cens_dense = W;
+    if (nh > 0 && W < cfg.census_capacity) {
+      std::sort(holes.begin(), holes.end());
+      /* destinations: hole slots below W; sources: non-hole slots in [W, R) */
+      std::vector<long long> mv;
+      size_t hi = 0;                       /* next hole (source side scan) */
+      int64_t src = W;
+      auto next_src = [&](int64_t& s, int64_t& run) {
+        /* advance s past holes; run = valid records from s before the next hole */
+        for (;;) {
+          while (hi < holes.size() && holes[hi].first + holes[hi].second <= s) hi++;
+          if (hi < holes.size() && holes[hi].first <= s) { s = holes[hi].first + holes[hi].second; continue; }
+          run = (hi < holes.size() ? holes[hi].first : R) - s;
+          return;
+        }
+      };
+      for (const auto& h : holes) {
+        if (h.first >= W) break;
+        int64_t dst = h.first, left = std::min<int64_t>(h.second, W - h.first);
+        while (left > 0) {
+          int64_t run = 0;
+          next_src(src, run);
+          const int64_t n = std::min(left, run);
+          if (n <= 0) return fail(c, C2D_E_STATE, "census compaction: inconsistent holes");
+          mv.push_back(src); mv.push_back(dst); mv.push_back(n);
+          src += n; dst += n; left -= n;
+        }
+      }
+      const int nmv = (int)(mv.size() / 3);
+      if ((size_t)nmv * 3 > 3 * c->h_holes.size() + 6)
+        return fail(c, C2D_E_STATE, "census compaction: %d moves", nmv);
+      if (nmv > 0) {
+        HIPCHK(c, hipMemcpyAsync(c->cens_moves, mv.data(), sizeof(long long) * mv.size(),
+                                 hipMemcpyHostToDevice, c->stream));
+        const int rc = c2d_launch_census_move(P.cout, c->cens_moves, nmv, c->stream);
+        if (rc) return fail(c, C2D_E_HIP, "census move: %s", hipGetErrorString((hipError_t)rc));
+        launches++;
+      }
+    }
+  }
   {
     const int64_t n = (int64_t)c->ncell * C2D_NPHFIELD;
     const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 16);
@@ -749,6 +861,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     (void)hipEventElapsedTime(&msall, c->ev_g0a, c->ev_end);
   }
   c->last_g0_ms = ms0;
+  for (int i = 0; i < C2D_TR_PROF_WORDS; i++) c->last_prof[i] = ctl[CTL_PROF + i];
   c->last_all_ms = msall;
   c->last_launches = launches;
   /* counters into the fused buffer (exact integers as f64) */
@@ -757,7 +870,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   hc[C2D_CNT_GENS] = (double)gen;
   HIPCHK(c, hipMemcpyAsync(c->T + c->L.counters, hc, sizeof hc, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const int64_t ncout = (int64_t)ctl[CTL_NCOUT];
+  const int64_t ncout = cens_dense >= 0 ? cens_dense : (int64_t)ctl[CTL_NCOUT];
   c->n_ev = 0;
   unsigned long long ev_reserved = 0;
   for (int sh = 0; sh < C2D_EV_SHARDS; sh++) {
@@ -1034,6 +1147,12 @@ extern "C" int c2d_fp_tridag(c2d_ctx* c, const c2d_fp_in* in, double* x) {
 extern "C" int c2d_last_gen0_steps(c2d_ctx* c, int64_t* steps) {
   if (!c || !steps) return C2D_E_ARG;
   *steps = c->last_g0_steps;
+  return C2D_OK;
+}
+
+extern "C" int c2d_transport_prof(c2d_ctx* c, uint64_t* out, int32_t n) {
+  if (!c || !out || n < 0) return C2D_E_ARG;
+  for (int i = 0; i < n && i < C2D_TR_PROF_WORDS; i++) out[i] = c->last_prof[i];
   return C2D_OK;
 }
 

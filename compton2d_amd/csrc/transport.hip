@@ -108,11 +108,11 @@ constexpr int MAX_REJECT = 1 << 20;
 
 /* Counters: packet-steps in a register (one per step), the rarer events
  * as LDS atomics on a per-workgroup array, flushed once at the end. */
+__shared__ uint32_t c2d_cnt_lds[C2D_NCOUNTERS];   /* the workgroup's event counters */
 struct LaneCnt {
   uint32_t steps;
-  uint32_t* sh;      /* LDS [C2D_NCOUNTERS] */
 };
-#define LC_ADD(lc, which) atomicAdd(&(lc).sh[which], 1u)
+#define LC_ADD(lc, which) atomicAdd(&c2d_cnt_lds[which], 1u)
 
 /* Tally views.  Cell tallies edep|prdep|ecens|npcen (stride ncell) and
  * escape tallies fout|edout|erlki|erlko|erlku|erlkl have the same layout in
@@ -138,6 +138,38 @@ __device__ __forceinline__ void cell_add(const KParams& P, const Tal& T, int whi
 #endif
   if (P.lds_cells) atomicAdd(&c2d_tr_lds[T.cells_off + which * P.ncell + cell], v);
   else gadd(P.T + P.off.edep + which * P.ncell + cell, v);
+}
+
+/* Rare paths (census writes, escapes, collision records, source loads) read
+ * their KParams fields through an opaque copy of the pointer: the loads
+ * stay in those paths instead of being hoisted out of the lane loop, where
+ * they would hold ~70 SGPRs for the whole launch and spill (C2D_COLD_RELOAD=0
+ * restores the hoisted form). */
+#ifndef C2D_COLD_RELOAD
+#define C2D_COLD_RELOAD 0
+#endif
+/* C2D_COLD_CALL: the rare event paths (census write, escape) as real calls,
+ * so their temporaries do not add to the lane loop's register pressure */
+/* C2D_EARLY_LOADS (fast build): issue a step's table loads at its start */
+#ifndef C2D_EARLY_LOADS
+#define C2D_EARLY_LOADS 0
+#endif
+#ifndef C2D_COLD_CALL
+#define C2D_COLD_CALL 0
+#endif
+#if C2D_COLD_CALL
+#define C2D_COLD_FN __device__ __noinline__
+#else
+#define C2D_COLD_FN __device__ __forceinline__
+#endif
+__device__ __forceinline__ const KParams& cold(const KParams& P) {
+#if C2D_COLD_RELOAD
+  const KParams* q = &P;
+  asm volatile("" : "+s"(q));
+  return *q;
+#else
+  return P;
+#endif
 }
 
 /* Next draw of the packet's stream.  Every key change sets ctr = 0, except a
@@ -277,16 +309,19 @@ __device__ __noinline__ double comtot_exact(const KParams& P, int cell, double x
 #if C2D_TABLE_COMTOT
 /* cubic Lagrange interpolation of the per-step table at the packet's cached
  * abscissa (tg, tt); tg == 0 means xnu lies outside the table: exact sum. */
-__device__ __forceinline__ double comtot_table(const KParams& P, int cell, const double xnu,
-                                               const int tg, const double t) {
-  if (tg == 0) return comtot_exact(P, cell, xnu);
-  const double* tb = P.comtab + (int64_t)cell * C2D_COMTAB_N + (tg - 1);
-  const double y0 = gld(tb), y1 = gld(tb + 1), y2 = gld(tb + 2), y3 = gld(tb + 3);
+__device__ __forceinline__ double comtot_interp(double y0, double y1, double y2, double y3,
+                                                double ne, double t) {
   const double tm1 = t - 1.0, tm2 = t - 2.0, tp1 = t + 1.0;
   const double cosig = -(t * tm1 * tm2) * (1.0 / 6.0) * y0 + (tp1 * tm1 * tm2) * 0.5 * y1 -
                        (tp1 * t * tm2) * 0.5 * y2 + (tp1 * t * tm1) * (1.0 / 6.0) * y3;
   if (cosig < 1.0e-40) return 1.0e-40;
-  return gld(P.n_e + cell) * cosig;
+  return ne * cosig;
+}
+__device__ __forceinline__ double comtot_table(const KParams& P, int cell, const double xnu,
+                                               const int tg, const double t) {
+  if (tg == 0) return comtot_exact(P, cell, xnu);
+  const double* tb = P.comtab + (int64_t)cell * C2D_COMTAB_N + (tg - 1);
+  return comtot_interp(gld(tb), gld(tb + 1), gld(tb + 2), gld(tb + 3), gld(P.n_e + cell), t);
 }
 #endif
 
@@ -457,7 +492,8 @@ __device__ __forceinline__ int compb2d(const KParams& P, const Geo* g, double* n
 /* ------------------------------------------------------------------ */
 /* escapes (src/imcleak2d.f:2-320, cr_sent = 0)                          */
 /* ------------------------------------------------------------------ */
-__device__ __forceinline__ void push_event(const KParams& P, double tb, const Pkt& p, LaneCnt& lc) {
+__device__ __forceinline__ void push_event(const KParams& P0, double tb, const Pkt& p, LaneCnt& lc) {
+  const KParams& P = cold(P0);
   const unsigned sh = blockIdx.x % C2D_EV_SHARDS;
   const unsigned long long slot = wave_reserve(P.n_ev_sh + sh * C2D_EV_SHARD_STRIDE);
   if (slot < (unsigned long long)P.cap_ev_sh) {
@@ -470,14 +506,16 @@ __device__ __forceinline__ void push_event(const KParams& P, double tb, const Pk
   LC_ADD(lc, C2D_CNT_EVENTS);
 }
 
-__device__ __forceinline__ void escape_tally(const KParams& P, const Tal& T, const Pkt& p) {
+__device__ __forceinline__ void escape_tally(const KParams& P0, const Tal& T, const Pkt& p) {
+  const KParams& P = cold(P0);
   if (p.jgplc > 0) atomicAdd(&T_EDOUT(P, T)[(p.jgpmu - 1) * C2D_NPHLCMAX + (p.jgplc - 1)], p.ew / P.dt);
   if (p.jgpsp > 0 && P.spec_switch == 0)
     atomicAdd(&T_FOUT(P, T)[(p.jgpmu - 1) * C2D_NPHOMAX + (p.jgpsp - 1)], p.ew);
 }
 
 /* returns idead: 1 = left the system, 0 = continue (axis pass-through) */
-__device__ __forceinline__ int imcleak(const KParams& P, const Tal& T, Pkt& p, LaneCnt& lc) {
+C2D_COLD_FN int imcleak(const KParams& P0, const Tal& T, Pkt& p, LaneCnt& lc) {
+  const KParams& P = cold(P0);
   if (p.kph == 0) {
     if (P.rmin > 1.0e-10) {
       atomicAdd(&T_ERLKI(P, T)[p.jph - 1], p.ew);
@@ -517,8 +555,49 @@ __device__ __forceinline__ int imcleak(const KParams& P, const Tal& T, Pkt& p, L
   return 1;
 }
 
+/* Census slots of the bundle kernel come from wave-private chunks of
+ * CENS_CHUNK slots, reserved with one atomic on the census counter (a single
+ * address every wave appends to: per-write reservations were the kernel's
+ * limiter).  A wave's last chunk leaves a hole [used, CENS_CHUNK), recorded
+ * in P.cens_holes and closed after the step by moving records from the end
+ * of the census (c2d_census_move), so the census stays dense. */
+constexpr uint32_t CENS_CHUNK = 256;
+/* per wave of the workgroup, in LDS (updated by the lanes that write) */
+__shared__ unsigned long long c2d_cch_base[16];
+__shared__ uint32_t c2d_cch_used[16];
+struct CensChunk {
+  int dummy;
+};
+__device__ __forceinline__ unsigned long long census_slot_chunk(const KParams& P0, CensChunk&) {
+  const KParams& P = cold(P0);
+  const int w = (int)(threadIdx.x >> 6);
+  const unsigned long long mask = __ballot(1);
+  const uint32_t leader = (uint32_t)(__ffsll((long long)mask) - 1);
+  const uint32_t lane = lane_id();
+  const unsigned long long lt = (lane == 0) ? 0ull : (mask & ((~0ull) >> (64 - lane)));
+  const uint32_t rank = (uint32_t)__popcll(lt), k = (uint32_t)__popcll(mask);
+  const unsigned long long base = c2d_cch_base[w];
+  const uint32_t used = c2d_cch_used[w];
+  const uint32_t rem = CENS_CHUNK - used;
+  if (k <= rem) {
+    if (lane == leader) c2d_cch_used[w] = used + k;
+    return base + used + rank;
+  }
+  unsigned long long nb = 0;
+  if (lane == leader)
+    nb = __hip_atomic_fetch_add((C2D_GLOBAL unsigned long long*)P.n_cout, (unsigned long long)CENS_CHUNK,
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)nb, leader);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(nb >> 32), leader);
+  nb = ((unsigned long long)hi << 32) | lo;
+  if (lane == leader) { c2d_cch_base[w] = nb; c2d_cch_used[w] = k - rem; }
+  return rank < rem ? base + used + rank : nb + (rank - rem);
+}
+
 /* census write (src/imctrk2d.f:528-578) */
-__device__ __forceinline__ void census_write(const KParams& P, const Tal& T, const Pkt& p, LaneCnt& lc) {
+C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, LaneCnt& lc,
+                              CensChunk* cch = nullptr) {
+  const KParams& P = cold(P0);
   const Geo* g = T.g;
   int cell = (p.jph - 1) * P.nr + (p.kph - 1);
   cell_add(P, T, TC_NPCEN, cell, 1.0);
@@ -532,7 +611,7 @@ __device__ __forceinline__ void census_write(const KParams& P, const Tal& T, con
 #endif
     gadd(&P.nf_rep[(int64_t)(blockIdx.x % C2D_NF_REPL) * P.ncell * C2D_NPHFIELD +
                    (int64_t)cell * C2D_NPHFIELD + (i - 1)], 6.25e8 * p.ew / p.xnu);
-  unsigned long long slot = wave_reserve(P.n_cout);
+  unsigned long long slot = cch ? census_slot_chunk(P, *cch) : wave_reserve(P.n_cout);
   if (slot < (unsigned long long)P.cap_cout) {
     gst(P.cout.rpre + slot, p.rpre);
     gst(P.cout.zpre + slot, p.zpre);
@@ -549,7 +628,8 @@ __device__ __forceinline__ void census_write(const KParams& P, const Tal& T, con
   LC_ADD(lc, C2D_CNT_CENSUS);
 }
 
-__device__ __forceinline__ void push_scat(const KParams& P, ScatRec* q, unsigned long long* n, const ScatRec& r) {
+__device__ __forceinline__ void push_scat(const KParams& P0, ScatRec* q, unsigned long long* n, const ScatRec& r) {
+  const KParams& P = cold(P0);
   unsigned long long slot = wave_reserve(n);
   if (slot < (unsigned long long)P.cap_q) {
     q[slot] = r;
@@ -618,9 +698,52 @@ struct ComCache {
   double v0, v1;
 };
 
-__device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, ComCache& cc, LaneCnt& lc) {
+/* -DC2D_TR_PROF: wave-level section timers (shader clock) and event counts,
+ * read back with c2d_transport_prof (tools/tr_prof.py).  Sections: */
+enum : int {
+  TP_REFILL = 0,    /* work fetch (ballot loop)                          */
+  TP_START = 1,     /* load_source / load_pk, cache_energy, set_phi       */
+  TP_GEOM = 2,      /* flight: colmfp, comtot, geometry                   */
+  TP_ABS = 3,       /* flight: absorption, wmustar sampling, deposits     */
+  TP_EVENT = 4,     /* flight: acos, census write, escape, collision      */
+  TP_POST = 5,      /* push_scat, probe restart from the source record    */
+  TP_ITER = 8,      /* loop iterations (waves)                            */
+  TP_LANES = 9,     /* sum of lanes in flight over iterations             */
+  TP_GOT_W = 10, TP_GOT_L = 11,       /* new items: waves, lanes        */
+  TP_CENS_W = 12, TP_CENS_L = 13,     /* census writes                  */
+  TP_LEAK_W = 14, TP_LEAK_L = 15,     /* imcleak calls                  */
+  TP_COLL_W = 16, TP_COLL_L = 17,     /* collisions                     */
+  TP_RST_W = 18, TP_RST_L = 19,       /* probe restarts                 */
+  TP_NWAVE = 20
+};
+struct Prof {
+#ifdef C2D_TR_PROF
+  uint64_t acc[C2D_TR_PROF_WORDS];
+  uint64_t t;
+#endif
+};
+#ifdef C2D_TR_PROF
+#define TP_MARK(pf, i) do { const uint64_t _n = clock64(); (pf).acc[i] += _n - (pf).t; (pf).t = _n; } while (0)
+#define TP_COUNT(pf, iw, il) do { (pf).acc[iw] += 1; (pf).acc[il] += __popcll(__ballot(1)); } while (0)
+#else
+#define TP_MARK(pf, i) do { } while (0)
+#define TP_COUNT(pf, iw, il) do { } while (0)
+#endif
+
+__device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, ComCache& cc, LaneCnt& lc,
+                                      Prof& pf) {
   const double lim8 = 9.9999999e-1, lim9 = 0.999999999;
   const Geo* g = T.g;
+#if C2D_TABLE_COMTOT && C2D_EARLY_LOADS
+  /* the step's table reads (comtot interpolation points, n_e, kappa) are
+   * issued before the colmfp draw, so their latency overlaps the Philox
+   * block and the log instead of following them */
+  const int cell_e = (p.jph - 1) * P.nr + (p.kph - 1);
+  const double* tb_e = P.comtab + (int64_t)cell_e * C2D_COMTAB_N + (p.tg > 0 ? p.tg - 1 : 0);
+  const double ey0 = gld(tb_e), ey1 = gld(tb_e + 1), ey2 = gld(tb_e + 2), ey3 = gld(tb_e + 3);
+  const double ene = gld(P.n_e + cell_e);
+  const double ekap = gld((p.kap ? P.kappa_s : P.kappa_cv) + (int64_t)cell_e * C2D_N_VOL + (p.ie - 1));
+#endif
   /* mode 0 uses mb_ran = 1e-10 (imctrk2d.f:150) but never reads colmfp (dcol below) */
   double colmfp = 0.0;
   if (p.mode != 0) colmfp = -c2d_log(U(p));   /* Philox uniform is never 0: no `goto 100` redraw */
@@ -633,7 +756,11 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
   double comac = 0.0;
   if (p.mode != 0) {
-#if C2D_TABLE_COMTOT
+#if C2D_TABLE_COMTOT && C2D_EARLY_LOADS
+    comac = (p.tg == 0) ? comtot_exact(P, cell, p.xnu)
+                        : comtot_interp(ey0, ey1, ey2, ey3, ene, p.tt);
+    (void)cc;
+#elif C2D_TABLE_COMTOT
     comac = comtot_table(P, cell, p.xnu, p.tg, p.tt);
     (void)cc;
 #else
@@ -720,9 +847,14 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
     rnew = __builtin_sqrt(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
     znew = zpre + trld * wmu;
   }
+  TP_MARK(pf, TP_GEOM);
   /* absorption (imctrk2d.f:382-462); gamma-gamma opacity inert (H6) */
+#if C2D_TABLE_COMTOT && C2D_EARLY_LOADS
+  double sigabs = 1.0e-40 + 1.0 * ekap;
+#else
   const double* kap = p.kap ? P.kappa_s : P.kappa_cv;
   double sigabs = 1.0e-40 + 1.0 * gld(kap + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
+#endif
   if (sigabs < 1.0e-40) sigabs = 1.0e-40;
   const double xabs = sigabs * trld;
   const double ewnew = (xabs < 100.0) ? p.ew * c2d_exp(-xabs) : 0.0;
@@ -748,6 +880,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
     cell_add(P, T, TC_EDEP, cell, deleabs);
     cell_add(P, T, TC_PRDEP, cell, delpr);
   }
+  TP_MARK(pf, TP_ABS);
   if (ewnew <= p.wtmin) {
     LC_ADD(lc, C2D_CNT_KILLED);
     return FL_END;
@@ -774,6 +907,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
       p.jph = jnew;
       p.kph = knew;
       if (p.mode == -1) return FL_END;
+      TP_COUNT(pf, TP_LEAK_W, TP_LEAK_L);
       if (imcleak(P, T, p, lc) == 1) return FL_END;
       set_phi(p, p.phi);                        /* axis pass-through set phi = 1e-6 */
       return FL_CONT;
@@ -783,10 +917,14 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
     return FL_CONT;
   }
   if (ikind == 2) {
-    if (p.mode != -1) census_write(P, T, p, lc);
+    if (p.mode != -1) {
+      TP_COUNT(pf, TP_CENS_W, TP_CENS_L);
+      census_write(P, T, p, lc);
+    }
     return FL_END;
   }
   LC_ADD(lc, C2D_CNT_COLLIDE);
+  TP_COUNT(pf, TP_COLL_W, TP_COLL_L);
   if (p.mode == -1) {   /* probes read phi too (the collision record) */
 #if C2D_TABLE_COMTOT
     p.phi = c2d_acos(Eta);
@@ -1021,10 +1159,10 @@ __device__ __forceinline__ void init_counters(uint32_t* sh) {
 /* after the final __syncthreads of the kernel */
 __device__ __forceinline__ void flush_counters(const KParams& P, LaneCnt& lc, uint32_t lane) {
   const uint32_t st = wave_sum(lc.steps);
-  if (lane == 0 && st) atomicAdd(&lc.sh[C2D_CNT_STEPS], st);
+  if (lane == 0 && st) atomicAdd(&c2d_cnt_lds[C2D_CNT_STEPS], st);
   __syncthreads();
-  if (threadIdx.x < C2D_NCOUNTERS && lc.sh[threadIdx.x])
-    atomicAdd(&P.cnt[threadIdx.x], (unsigned long long)lc.sh[threadIdx.x]);
+  if (threadIdx.x < C2D_NCOUNTERS && c2d_cnt_lds[threadIdx.x])
+    atomicAdd(&P.cnt[threadIdx.x], (unsigned long long)c2d_cnt_lds[threadIdx.x]);
 }
 
 __device__ __forceinline__ void store_pk(const PktSoA& s, int64_t i, const Pkt& p) {
@@ -1105,15 +1243,14 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
   __shared__ double eic_lds[C2D_NUM_NT + 2];
   for (int i = threadIdx.x; i < GEO_DOUBLES; i += SBLOCK)
     geo_lds[i] = reinterpret_cast<const double*>(P.geo)[i];
-  __shared__ uint32_t cnt_lds[C2D_NCOUNTERS];
   for (int i = threadIdx.x; i < C2D_NUM_NT + 2; i += SBLOCK) {
     nel_lds[i] = 0.0;
     eic_lds[i] = 0.0;
   }
-  init_counters(cnt_lds);
+  init_counters(c2d_cnt_lds);
   __syncthreads();
   const Geo* g = reinterpret_cast<const Geo*>(geo_lds);
-  LaneCnt lc = {0u, cnt_lds};
+  LaneCnt lc = {0u};
   const double twopi = 2.0 * PI_REF;
   const int64_t n2items = A.n2_in * P.split2;
   const int64_t stride = (int64_t)gridDim.x * SBLOCK;
@@ -1177,7 +1314,8 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
 
 /* a generation-0 source record: census packet (imcfield2d.f:98-117) or a
  * sampled volume/surface packet from the packet store */
-__device__ __forceinline__ void load_source(const KParams& P, Pkt& p, long long item) {
+__device__ __forceinline__ void load_source(const KParams& P0, Pkt& p, long long item) {
+  const KParams& P = cold(P0);
   if (item < P.n_cens_items) {
     const int64_t i = item;
     p.rpre = gld(P.cin.rpre + i); p.zpre = gld(P.cin.zpre + i);
@@ -1219,8 +1357,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
     for (int i = tid; i < GEO_DOUBLES; i += BLOCK) lds[i] = gld(gsrc + i);
     for (int i = tid; i < n_cells_lds + n_esc; i += BLOCK) cells_lds[i] = 0.0;
   }
-  __shared__ uint32_t cnt_lds[C2D_NCOUNTERS];
-  init_counters(cnt_lds);
+  init_counters(c2d_cnt_lds);
   __syncthreads();
   const long long n_items = A.gen == 0 ? (long long)A.n_items : (long long)rfl64(*A.n_pk);
 
@@ -1235,9 +1372,14 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
 #endif
   int32_t state = ST_IDLE, probe = 0, nscat = 0;
   ComCache cc = {-1, -1, 0.0, 0.0};
-  LaneCnt lc = {0u, cnt_lds};
+  LaneCnt lc = {0u};
   long long chunk_base = 0, chunk_end = 0;
   bool exhausted = false;
+  Prof pf;
+#ifdef C2D_TR_PROF
+  for (int i = 0; i < C2D_TR_PROF_WORDS; i++) pf.acc[i] = 0;
+  pf.t = clock64();
+#endif
 
   for (;;) {
     /* ---- refill idle lanes: chunked, wave-aggregated work fetch ---- */
@@ -1266,7 +1408,12 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
         needm = __ballot(state == ST_IDLE && !got);
       }
     }
+    TP_MARK(pf, TP_REFILL);
+#ifdef C2D_TR_PROF
+    pf.acc[TP_ITER] += 1;
+#endif
     if (got) {
+      TP_COUNT(pf, TP_GOT_W, TP_GOT_L);
       if (A.gen == 0) {
         /* imctrk2d(-1) entry (imctrk2d.f:91,106-123): first probe copy */
         LC_ADD(lc, C2D_CNT_SOURCES);
@@ -1282,7 +1429,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
         state = ST_PROBE;
       } else {
         /* a scatter secondary, tracked as imctrk2d(1) (imctrk2d.f:662-679) */
-        load_pk(p, P.pk, item);
+        load_pk(p, cold(P).pk, item);
         rng_sync(p);
         p.mode = 1;
         p.wtmin = 1.0e-10 * p.ew;
@@ -1297,8 +1444,13 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
 #endif
     }
     if (exhausted && __ballot(state != ST_IDLE) == 0ull) break;
+    TP_MARK(pf, TP_START);
     if (state != ST_IDLE) {
-      const int out = flight(P, T, p, cc, lc);
+#ifdef C2D_TR_PROF
+      pf.acc[TP_LANES] += __popcll(__ballot(1));
+#endif
+      const int out = flight(P, T, p, cc, lc, pf);
+      TP_MARK(pf, TP_EVENT);
       if (out != FL_CONT) {
         if (out == FL_COLLIDE) {
           push_scat(P, A.q2_out, A.n2_out, make_rec(p, p.key, p.ctr));
@@ -1307,6 +1459,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
         if (state == ST_PROBE) {
           probe++;
           if (probe < P.split1 || P.split1 - nscat > 0) {
+            TP_COUNT(pf, TP_RST_W, TP_RST_L);
             load_source(P, p, src_item);
             const double ew0 = p.ew;
             const double s_ew = ew0 / P.split1;
@@ -1337,7 +1490,14 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
         }
       }
     }
+    TP_MARK(pf, TP_POST);
   }
+#ifdef C2D_TR_PROF
+  pf.acc[TP_NWAVE] = 1;
+  if (lane == 0)
+    for (int i = 0; i < C2D_TR_PROF_WORDS; i++)
+      if (pf.acc[i]) atomicAdd(&P.prof[i], (unsigned long long)pf.acc[i]);
+#endif
 
   /* ---- flush: LDS tallies and counters ---- */
   __syncthreads();
@@ -1357,6 +1517,520 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
   }
   flush_counters(P, lc, lane);
 }
+
+/* ------------------------------------------------------------------ */
+/* generation 0 as probe bundles                                        */
+/* ------------------------------------------------------------------ */
+/* The split1 probe copies of a source (imctrk2d(-1), imctrk2d.f:106-123)
+ * and its recombined copy (imctrk2d(0), :690-704) start from the same
+ * record and differ only in weight and random numbers: they fly the same
+ * path until a probe collides.  A bundle carries up to BUNDLE_MAX probes
+ * and the recombined copy along one shared path: comtot, the geometry, the
+ * absorption factor and the position update are evaluated once per shared
+ * step, while every probe draws its own colmfp (the collision test) and its
+ * own absorption point (prdep) from its own stream.  A colliding probe
+ * leaves through its own partial step (flight()'s ikind = 3 branch).
+ *
+ * The recombined copy's weight (split1 - nscat) * s_ew needs the source's
+ * final collision count, so it flies with the bundle of the last probes on
+ * the assumption that they do not collide; a collision in that bundle
+ * cancels it (the packet-steps it was counted for are taken back) and it
+ * flies alone from the source afterwards.  Its absorption-point draws are
+ * only counted (its prdep is never tallied).  Every copy's arithmetic,
+ * draws, records and tallies are the per-copy tracker's; only the order in
+ * which cell tallies are summed differs. */
+constexpr int BUNDLE_MAX = 32;
+enum : int32_t {
+  BF_TRACK = 1,     /* the recombined copy is on the path               */
+  BF_SPEC = 2,      /* ... with a weight that assumes no more collisions */
+  BF_RERUN = 4,     /* a collision cancelled it: refly alone afterwards  */
+  BF_TKILL = 8,     /* it ended KILLED / ABORTED: counted at the bundle end */
+  BF_TABORT = 16
+};
+struct Bundle {
+  Pkt p;              /* shared path; p.ew, p.wtmin, p.ctr: the recombined copy's */
+  double ewp, wtminp; /* the probes' common weight and kill threshold               */
+  long long src;      /* source item                                             */
+  uint32_t alive;     /* probes g0 + i still on the path (bit i)                 */
+  uint32_t pctr;      /* draws consumed by each probe on the path               */
+  int32_t g0;         /* first probe of this bundle (== split1: refly alone)     */
+  int32_t nscat;      /* probes of the source that collided                      */
+  int32_t flags;
+  int32_t tsteps;     /* packet-steps counted for a speculative recombined copy  */
+};
+
+/* the probes' second Philox halves (draw pctr when pctr is odd), per lane in
+ * LDS when the plan has room (P.rn_lds), else recomputed */
+__device__ __forceinline__ double* rn_slot(const KParams& P, int i) {
+  return c2d_tr_lds + P.rn_off + i * BLOCK + (int)threadIdx.x;
+}
+
+/* start (or restart) the bundle at probe g0 of source b.src */
+__device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bundle& b) {
+  Pkt& p = b.p;
+  load_source(P, p, b.src);
+  const double ew0 = p.ew;
+  const double s_ew = ew0 / P.split1;          /* imctrk2d.f:106-123 */
+  const int G = min(P.split1 - b.g0, BUNDLE_MAX);
+  b.ewp = s_ew;
+  b.wtminp = 1.0e-10 * ew0;
+  b.alive = G >= 32 ? 0xffffffffu : ((1u << G) - 1u);
+  b.pctr = 0;
+  b.flags = 0;
+  b.tsteps = 0;
+  p.nflight = 0;
+  p.mode = 0;
+  if (b.g0 + G == P.split1 && P.split1 - b.nscat > 0) {
+    /* recombined unscattered copies, imctrk2d(0) (imctrk2d.f:690-704) */
+    p.ew = (double)(P.split1 - b.nscat) * s_ew;
+    p.wtmin = 1.0e-10 * p.ew;
+    p.sub = C2D_SUB_RECOMB;
+    p.ctr = 0;
+    b.flags = BF_TRACK | (G > 0 ? BF_SPEC : 0);
+  }
+  cache_energy(P, T.g, p);
+  set_phi(p, p.phi);
+}
+
+/* a probe whose colmfp falls inside the shared step: its own partial step
+ * to the collision point (flight(), ikind = 3), then the collision record */
+__device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, const GenArgs& A,
+                                              Bundle& b, uint32_t sub, double dcol, bool odd,
+                                              double hi, double sigabs, double Eta, double swmu,
+                                              int eta_switch, int cell, LaneCnt& lc) {
+  const double lim9 = 0.999999999;
+  const Pkt& p = b.p;
+  const double rpre = p.rpre, zpre = p.zpre, wmu = p.wmu;
+  const double trld = dcol;
+  const double f = trld * swmu;
+  const double rnew = __builtin_sqrt(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
+  const double znew = zpre + trld * wmu;
+  const double xabs = sigabs * trld;
+  const double ewnew = (xabs < 100.0) ? b.ewp * c2d_exp(-xabs) : 0.0;
+  double deleabs = b.ewp - ewnew;
+  if (deleabs < 1.0e-50) deleabs = 1.0e-50;
+  uint32_t ctr = b.pctr + 1u;
+  double wmustar;
+  if (xabs <= 0.00001) {
+    wmustar = wmu;
+  } else {
+    /* one draw: mr < 1 <= ew / deleabs always holds (ew >= 1e-40) */
+    const double mr = odd ? c2d_draw_s(p.key, sub, b.pctr + 1u) : hi;
+    ctr++;
+    const double sstar = -c2d_log(1.0 - mr * deleabs / b.ewp) / sigabs;
+    const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
+    wmustar = (wmu * rpre + sstar) / denom;
+  }
+  cell_add(P, T, TC_EDEP, cell, deleabs);
+  cell_add(P, T, TC_PRDEP, cell, deleabs * wmustar * C_LIGHT);
+  if (ewnew <= b.wtminp) {
+    LC_ADD(lc, C2D_CNT_KILLED);
+    return;
+  }
+  LC_ADD(lc, C2D_CNT_COLLIDE);
+  double Eta2 = clampd((trld + Eta * rpre) / rnew, lim9);   /* H1 */
+  double phi = c2d_acos(Eta2);
+  if (eta_switch == -1) phi = 2.0 * PI_REF - phi;
+  ScatRec r;
+  r.rpre = rnew; r.zpre = znew; r.wmu = wmu; r.phi = phi; r.ew = ewnew; r.xnu = p.xnu;
+  r.dcen = p.dcen - trld;
+  r.jk = ((uint32_t)p.jph << 16) | (uint32_t)p.kph;
+  r.ctr = ctr;
+  r.key = p.key;
+  r.kap = (uint32_t)p.kap;
+  r.sub = sub;
+  push_scat(P, A.q2_out, A.n2_out, r);
+  b.nscat++;
+  if (b.flags & BF_SPEC) {
+    /* the recombined copy's weight assumed no collision: cancel it, and the
+     * packet-steps it was counted for (it may have ended already) */
+    lc.steps -= (uint32_t)b.tsteps;
+    b.flags = (b.flags & ~(BF_TRACK | BF_SPEC | BF_TKILL | BF_TABORT)) | BF_RERUN;
+  }
+}
+
+/* one shared step of the bundle (flight() for every copy on the path) */
+__device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, const GenArgs& A,
+                                            Bundle& b, ComCache& cc, LaneCnt& lc, Prof& pf,
+                                            CensChunk* cch) {
+  const double lim8 = 9.9999999e-1, lim9 = 0.999999999;
+  const Geo* g = T.g;
+  Pkt& p = b.p;
+  if (b.alive && b.ewp < 1.0e-40) b.alive = 0;
+  if ((b.flags & BF_TRACK) && p.ew < 1.0e-40) b.flags &= ~BF_TRACK;
+  if (!b.alive && !(b.flags & BF_TRACK)) return;
+  if (++p.nflight > MAX_FLIGHTS) {
+    atomicAdd(&c2d_cnt_lds[C2D_CNT_ABORTED], (uint32_t)__popc(b.alive));
+    b.alive = 0;
+    if (b.flags & BF_TRACK) b.flags = (b.flags & ~BF_TRACK) | BF_TKILL | BF_TABORT;
+    return;
+  }
+  p.wmu = clampd(p.wmu, lim8);
+  const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
+  double sigsc = 1.0;
+  if (b.alive) {
+#if C2D_TABLE_COMTOT
+    sigsc = comtot_table(P, cell, p.xnu, p.tg, p.tt);
+    (void)cc;
+#else
+    if (cc.cell0 == cell) {
+      sigsc = cc.v0;
+    } else if (cc.cell1 == cell) {
+      sigsc = cc.v1;
+    } else {
+      sigsc = comtot_exact(P, cell, p.xnu);
+      cc.cell1 = cc.cell0; cc.v1 = cc.v0;
+      cc.cell0 = cell; cc.v0 = sigsc;
+    }
+#endif
+  }
+  /* geometry (imctrk2d.f:228-379), shared */
+  const double rkm1 = (p.kph == 1) ? P.rmin : g->r[p.kph - 1];
+  const double xqsqleft = rkm1 * rkm1;
+#if C2D_TABLE_COMTOT
+  double Eta = p.eta;
+  const int eta_switch = p.esw;
+#else
+  double Eta = c2d_cos(p.phi);
+  const int eta_switch = (p.phi <= PI_REF && p.phi >= 1.0e-10) ? 1 : -1;
+#endif
+  Eta = clampd(Eta, lim8);
+  const double rpre = p.rpre, zpre = p.zpre, wmu = p.wmu;
+  const double disp = Eta * rpre;
+  const double psq = rpre * rpre * (1.0 - Eta * Eta);
+  int kbnd, inout, knew, jnew;
+  double rbnd, Zbnd;
+  if (Eta < 0.0 && psq < xqsqleft) {
+    kbnd = p.kph - 1;
+    inout = -1;
+    rbnd = rkm1;
+  } else {
+    kbnd = p.kph;
+    inout = 1;
+    rbnd = g->r[p.kph];
+  }
+  double dpbsq = rbnd * rbnd - psq;
+  if (dpbsq < 1.0e-6) dpbsq = 1.0e-6;
+  const double disbr = (double)inout * __builtin_sqrt(dpbsq) - disp;
+  const double swmu = __builtin_sqrt(1.0 - wmu * wmu);
+  double trldb = disbr / swmu;
+  const double Zr = zpre + wmu * trldb;
+  const double zlow = (p.jph == 1) ? P.zmin : g->z[p.jph - 1];
+  const double zup = g->z[p.jph];
+  if (Zr > zup || Zr < zlow) {
+    Zbnd = (Zr > zup) ? zup : zlow;
+    knew = p.kph;
+    jnew = (Zr > zup) ? p.jph + 1 : p.jph - 1;
+    const double f = (Zbnd - zpre) * swmu / wmu;
+    rbnd = __builtin_sqrt(rpre * rpre + f * f + 2.0 * rpre * f * Eta);
+    trldb = __builtin_sqrt(f * f + (Zbnd - zpre) * (Zbnd - zpre));
+  } else {
+    knew = p.kph + inout;
+    jnew = p.jph;
+    rbnd = (kbnd > 0) ? g->r[kbnd] : P.rmin;
+    Zbnd = Zr;
+  }
+  /* every copy that does not collide: boundary if trldb < dcen, else census */
+  const bool bnd = trldb < p.dcen;
+  const double trld = bnd ? trldb : p.dcen;
+#if C2D_TABLE_COMTOT && C2D_EARLY_LOADS
+  double sigabs = 1.0e-40 + 1.0 * gld((p.kap ? P.kappa_s : P.kappa_cv) + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
+#else
+  const double* kap = p.kap ? P.kappa_s : P.kappa_cv;
+  double sigabs = 1.0e-40 + 1.0 * gld(kap + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
+#endif
+  if (sigabs < 1.0e-40) sigabs = 1.0e-40;
+  const double xabs = sigabs * trld;
+  const double ex = (xabs < 100.0) ? c2d_exp(-xabs) : 0.0;
+  const bool two = xabs > 0.00001;      /* the absorption point is sampled */
+  TP_MARK(pf, TP_GEOM);
+  /* ---- probes (mode -1) ---- */
+  if (b.alive) {
+    const double ewnew = (xabs < 100.0) ? b.ewp * ex : 0.0;
+    double deleabs = b.ewp - ewnew;
+    if (deleabs < 1.0e-50) deleabs = 1.0e-50;
+    const bool odd = (b.pctr & 1u) != 0u;
+    double sum_edep = 0.0, sum_prdep = 0.0;
+    int nsurv = 0;
+    const int G = min(P.split1 - b.g0, BUNDLE_MAX);
+    for (int i = 0; i < G; i++) {
+      if (!((b.alive >> i) & 1u)) continue;
+      const uint32_t sub = 1u + (uint32_t)(b.g0 + i);
+      lc.steps++;
+      double u1, hi = 0.0;
+      if (!odd) u1 = c2d_draw_pair(p.key, sub, b.pctr, &hi);
+      else u1 = P.rn_lds ? *rn_slot(P, i) : c2d_draw_s(p.key, sub, b.pctr);
+      const double colmfp = -c2d_log(u1);      /* Philox uniform is never 0 */
+      const double dcol = colmfp / sigsc;
+      if (dcol < p.dcen && !(trldb < dcol)) {
+        b.alive &= ~(1u << i);
+        probe_collide(P, T, A, b, sub, dcol, odd, hi, sigabs, Eta, swmu, eta_switch, cell, lc);
+        continue;
+      }
+      nsurv++;
+      double wmustar = wmu;
+      if (two) {
+        double mr;
+        if (!odd) {
+          mr = hi;
+        } else {
+          double h2;
+          mr = c2d_draw_pair(p.key, sub, b.pctr + 1u, &h2);
+          if (P.rn_lds) *rn_slot(P, i) = h2;
+        }
+        const double sstar = -c2d_log(1.0 - mr * deleabs / b.ewp) / sigabs;
+        const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
+        wmustar = (wmu * rpre + sstar) / denom;
+      } else if (!odd && P.rn_lds) {
+        *rn_slot(P, i) = hi;
+      }
+      sum_edep += deleabs;
+      sum_prdep += deleabs * wmustar * C_LIGHT;
+    }
+    if (nsurv > 0) {
+      cell_add(P, T, TC_EDEP, cell, sum_edep);
+      cell_add(P, T, TC_PRDEP, cell, sum_prdep);
+      b.pctr += two ? 2u : 1u;
+      if (ewnew <= b.wtminp) {
+        atomicAdd(&c2d_cnt_lds[C2D_CNT_KILLED], (uint32_t)nsurv);
+        b.alive = 0;
+      } else {
+        b.ewp = ewnew;
+      }
+    }
+  }
+  TP_MARK(pf, TP_ABS);
+  /* ---- the recombined copy (mode 0) ---- */
+  if (b.flags & BF_TRACK) {
+    lc.steps++;
+    if (b.flags & BF_SPEC) b.tsteps++;
+    const double ewnew = (xabs < 100.0) ? p.ew * ex : 0.0;
+    if (two) p.ctr++;                 /* its absorption-point draw: prdep is not tallied */
+    if (ewnew <= p.wtmin) b.flags = (b.flags & ~BF_TRACK) | BF_TKILL;
+    else p.ew = ewnew;
+  }
+  if (!b.alive && !(b.flags & BF_TRACK)) return;
+  /* ---- the shared move ---- */
+  double rnew, znew;
+  if (bnd) {
+    rnew = rbnd;
+    znew = Zbnd;
+  } else {
+    jnew = p.jph;
+    knew = p.kph;
+    const double f = trld * swmu;
+    rnew = __builtin_sqrt(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
+    znew = zpre + trld * wmu;
+  }
+  p.dcen = p.dcen - trld;
+  Eta = (trld + Eta * rpre) / rnew;          /* hazard H1: trld, not f (imctrk2d.f:472) */
+  Eta = clampd(Eta, lim9);
+  const bool leaves = bnd && (jnew == P.nz + 1 || jnew == 0 || knew == P.nr + 1 || knew == 0);
+#if C2D_TABLE_COMTOT
+  p.eta = Eta;
+  if ((b.flags & BF_TRACK) && (!bnd || leaves)) {   /* an event will read phi */
+    p.phi = c2d_acos(Eta);
+    if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
+  }
+#else
+  p.phi = c2d_acos(Eta);
+  if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
+#endif
+  p.rpre = rnew;
+  p.zpre = znew;
+  if (bnd) {
+    if (leaves) {
+      b.alive = 0;                            /* probes leaving end (no tally) */
+      p.jph = jnew;
+      p.kph = knew;
+      if (b.flags & BF_TRACK) {
+        TP_COUNT(pf, TP_LEAK_W, TP_LEAK_L);
+        if (imcleak(P, T, p, lc) == 1) b.flags &= ~BF_TRACK;
+        else set_phi(p, p.phi);               /* axis pass-through set phi = 1e-6 */
+      }
+      return;
+    }
+    p.kph = knew;
+    p.jph = jnew;
+    return;
+  }
+  /* census (imctrk2d.f:528-578): probes end, the recombined copy is written */
+  b.alive = 0;
+  if (b.flags & BF_TRACK) {
+    TP_COUNT(pf, TP_CENS_W, TP_CENS_L);
+    census_write(P, T, p, lc, cch);
+    b.flags &= ~BF_TRACK;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(const KParams* __restrict__ Pg,
+                                                                   const GenArgs A) {
+  const KParams& P = *Pg;
+  double* const lds = c2d_tr_lds;
+  const int tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  Tal T;
+  T.g = reinterpret_cast<const Geo*>(lds);
+  T.cells_off = GEO_DOUBLES;
+  const int n_cells_lds = P.lds_cells ? 4 * P.ncell : 0;
+  T.esc_off = GEO_DOUBLES + n_cells_lds;
+  const int n_esc = P.nmu * (C2D_NPHOMAX + C2D_NPHLCMAX) + 2 * P.nz + 2 * P.nr;
+  double* const cells_lds = lds + T.cells_off;
+  double* const esc_lds = lds + T.esc_off;
+  {
+    const double* gsrc = reinterpret_cast<const double*>(P.geo);
+    for (int i = tid; i < GEO_DOUBLES; i += BLOCK) lds[i] = gld(gsrc + i);
+    for (int i = tid; i < n_cells_lds + n_esc; i += BLOCK) cells_lds[i] = 0.0;
+  }
+  init_counters(c2d_cnt_lds);
+  __syncthreads();
+  const long long n_items = (long long)A.n_items;
+
+  Bundle b;
+  b.p.mode = 0; b.p.kap = 0; b.p.ctr = 0; b.p.key = 0; b.p.sub = 0; b.p.nflight = 0;
+  b.alive = 0; b.flags = 0; b.src = 0; b.g0 = 0; b.nscat = 0; b.pctr = 0; b.tsteps = 0;
+  bool busy = false;
+  ComCache cc = {-1, -1, 0.0, 0.0};
+  LaneCnt lc = {0u};
+  long long chunk_base = 0, chunk_end = 0;
+  bool exhausted = false;
+  int shard_try = 0;
+  const int shard0 = (int)(blockIdx.x % C2D_WORK_SHARDS);
+  Prof pf;
+#ifdef C2D_TR_PROF
+  for (int i = 0; i < C2D_TR_PROF_WORDS; i++) pf.acc[i] = 0;
+  pf.t = clock64();
+#endif
+  CensChunk cch = {0};
+  if (lane == 0) { c2d_cch_base[tid >> 6] = 0ull; c2d_cch_used[tid >> 6] = CENS_CHUNK; }
+
+  for (;;) {
+    /* ---- refill idle lanes: chunked, wave-aggregated work fetch from the
+     * workgroup's shard of the item range, then from the following ones ---- */
+    bool got = false;
+    long long item = -1;
+    if (!exhausted) {
+      unsigned long long needm = __ballot(!busy);
+      while (needm != 0ull) {
+        if (chunk_base >= chunk_end) {
+          for (;;) {
+            if (shard_try >= C2D_WORK_SHARDS) { exhausted = true; break; }
+            const int s = (shard0 + shard_try) % C2D_WORK_SHARDS;
+            const long long lo = n_items * s / C2D_WORK_SHARDS;
+            const long long hi = n_items * (s + 1) / C2D_WORK_SHARDS;
+            unsigned long long nb = 0;
+            if (lane == 0)
+              nb = atomicAdd(A.work_sh + (size_t)s * C2D_EV_SHARD_STRIDE, (unsigned long long)CHUNK);
+            nb = rfl64(nb);
+            if (lo + (long long)nb < hi) {
+              chunk_base = lo + (long long)nb;
+              chunk_end = chunk_base + CHUNK < hi ? chunk_base + CHUNK : hi;
+              break;
+            }
+            shard_try++;
+          }
+          if (exhausted) break;
+        }
+        const long long avail = chunk_end - chunk_base;
+        const unsigned long long lt = (lane == 0) ? 0ull : (needm & ((~0ull) >> (64 - lane)));
+        const long long rank = __popcll(lt);
+        const long long nneed = __popcll(needm);
+        if (((needm >> lane) & 1ull) && rank < avail) {
+          item = chunk_base + rank;
+          got = true;
+        }
+        chunk_base += (nneed < avail ? nneed : avail);
+        needm = __ballot(!busy && !got);
+      }
+    }
+    TP_MARK(pf, TP_REFILL);
+#ifdef C2D_TR_PROF
+    pf.acc[TP_ITER] += 1;
+#endif
+    if (got) {
+      TP_COUNT(pf, TP_GOT_W, TP_GOT_L);
+      LC_ADD(lc, C2D_CNT_SOURCES);      /* imctrk2d(-1) entry (imctrk2d.f:91,106-123) */
+      b.src = item;
+      b.g0 = 0;
+      b.nscat = 0;
+      cc.cell0 = -1; cc.cell1 = -1;
+      bundle_begin(P, T, b);
+      busy = true;
+    }
+    if (exhausted && __ballot(busy) == 0ull) break;
+    TP_MARK(pf, TP_START);
+    if (busy) {
+#ifdef C2D_TR_PROF
+      pf.acc[TP_LANES] += __popcll(__ballot(1));
+#endif
+      bundle_step(P, T, A, b, cc, lc, pf, &cch);
+      TP_MARK(pf, TP_EVENT);
+      if (!b.alive && !(b.flags & BF_TRACK)) {
+        if ((b.flags & (BF_TKILL | BF_RERUN)) == BF_TKILL)
+          LC_ADD(lc, (b.flags & BF_TABORT) ? C2D_CNT_ABORTED : C2D_CNT_KILLED);
+        const int G = min(P.split1 - b.g0, BUNDLE_MAX);
+        if (b.g0 + G < P.split1) {
+          TP_COUNT(pf, TP_RST_W, TP_RST_L);
+          b.g0 += G;                        /* next bundle of probes */
+          bundle_begin(P, T, b);
+        } else if ((b.flags & BF_RERUN) && P.split1 - b.nscat > 0) {
+          TP_COUNT(pf, TP_RST_W, TP_RST_L);
+          b.g0 = P.split1;                  /* the recombined copy alone */
+          bundle_begin(P, T, b);
+        } else {
+          busy = false;
+        }
+      }
+    }
+    TP_MARK(pf, TP_POST);
+  }
+#ifdef C2D_TR_PROF
+  pf.acc[TP_NWAVE] = 1;
+  if (lane == 0)
+    for (int i = 0; i < C2D_TR_PROF_WORDS; i++)
+      if (pf.acc[i]) atomicAdd(&P.prof[i], (unsigned long long)pf.acc[i]);
+#endif
+
+  /* the unused tail of this wave's last census chunk */
+  if (lane == 0 && c2d_cch_used[tid >> 6] < CENS_CHUNK) {
+    const size_t w = (size_t)blockIdx.x * (BLOCK / 64) + (size_t)(tid >> 6);
+    P.cens_holes[2 * w] = c2d_cch_base[tid >> 6] + c2d_cch_used[tid >> 6];
+    P.cens_holes[2 * w + 1] = CENS_CHUNK - c2d_cch_used[tid >> 6];
+  }
+
+  /* ---- flush: LDS tallies and counters ---- */
+  __syncthreads();
+  if (P.lds_cells) {
+    double* gdst = P.T + P.off.edep;
+    for (int i = tid; i < n_cells_lds; i += BLOCK) {
+      double v = cells_lds[i];
+      if (v != 0.0) atomicAdd(&gdst[i], v);
+    }
+  }
+  {
+    double* gdst = P.T + P.off.fout;
+    for (int i = tid; i < n_esc; i += BLOCK) {
+      double v = esc_lds[i];
+      if (v != 0.0) atomicAdd(&gdst[i], v);
+    }
+  }
+  flush_counters(P, lc, lane);
+}
+
+#if C2D_TABLE_COMTOT
+/* close the census holes: move n records src -> dst per workgroup (one move
+ * each, n <= CENS_CHUNK); moves never overlap */
+__global__ void __launch_bounds__(256) c2d_census_move(CensusSoA c, const long long* mv) {
+  const long long src = mv[3 * blockIdx.x], dst = mv[3 * blockIdx.x + 1], n = mv[3 * blockIdx.x + 2];
+  for (long long i = threadIdx.x; i < n; i += 256) {
+    c.rpre[dst + i] = c.rpre[src + i]; c.zpre[dst + i] = c.zpre[src + i];
+    c.wmu[dst + i] = c.wmu[src + i]; c.phi[dst + i] = c.phi[src + i];
+    c.ew[dst + i] = c.ew[src + i]; c.xnu[dst + i] = c.xnu[src + i];
+    c.jk[dst + i] = c.jk[src + i]; c.bins[dst + i] = c.bins[src + i];
+    c.key[dst + i] = c.key[src + i];
+  }
+}
+#endif
 
 #if C2D_TABLE_COMTOT
 /* Per-step comtot table: tab[cell][g] = sum_i sigma_E(i, x_g) f_nt(cell,i) dg_i
@@ -1427,6 +2101,26 @@ extern "C" int C2D_SFX(c2d_launch_transport)(const c2d::KParams* P_dev, const c2
   return (int)hipGetLastError();
 }
 
+static int C2D_SFX(bundle_lds_attr)(size_t lds_bytes) {
+  if (lds_bytes <= 64 * 1024) return 0;
+  return (int)hipFuncSetAttribute((const void*)C2D_SFX(c2d::c2d_bundle_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+}
+
+extern "C" int C2D_SFX(c2d_launch_bundle)(const c2d::KParams* P_dev, const c2d::GenArgs* A, int grid,
+                                          size_t lds_bytes, hipStream_t stream) {
+  if (int e = C2D_SFX(bundle_lds_attr)(lds_bytes)) return e;
+  hipLaunchKernelGGL(C2D_SFX(c2d::c2d_bundle_kernel), dim3(grid), dim3(c2d::BLOCK), lds_bytes,
+                     stream, P_dev, *A);
+  return (int)hipGetLastError();
+}
+
+extern "C" int C2D_SFX(c2d_bundle_occupancy)(int* blocks_per_cu, size_t lds_bytes) {
+  if (C2D_SFX(bundle_lds_attr)(lds_bytes) != 0) { *blocks_per_cu = 0; return 0; }
+  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      blocks_per_cu, C2D_SFX(c2d::c2d_bundle_kernel), c2d::BLOCK, lds_bytes);
+}
+
 extern "C" int C2D_SFX(c2d_launch_source)(const c2d::KParams* P_dev, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(C2D_SFX(c2d::c2d_source_kernel), dim3(grid), dim3(c2d::SBLOCK), 0, stream, P_dev);
   return (int)hipGetLastError();
@@ -1446,6 +2140,11 @@ extern "C" int C2D_SFX(c2d_transport_occupancy)(int* blocks_per_cu, size_t lds_b
 }
 
 #if C2D_TABLE_COMTOT
+extern "C" int c2d_launch_census_move(c2d::CensusSoA c, const long long* moves, int n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(c2d::c2d_census_move, dim3(n), dim3(256), 0, stream, c, moves);
+  return (int)hipGetLastError();
+}
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t stream) {
   hipLaunchKernelGGL(c2d::c2d_comtab_sigma, dim3(C2D_COMTAB_N), dim3(256), 0, stream, gnt, S);
   return (int)hipGetLastError();

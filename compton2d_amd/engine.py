@@ -100,6 +100,8 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_last_kernel_ms.restype = C.c_int
     lib.c2d_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                        C.POINTER(C.c_int32)]
+    lib.c2d_transport_prof.restype = C.c_int
+    lib.c2d_transport_prof.argtypes = [vp, C.POINTER(C.c_uint64), C.c_int32]
     lib.c2d_fp_set_config.restype = C.c_int
     lib.c2d_fp_set_config.argtypes = [vp, C.POINTER(abi.FpConfig)]
     lib.c2d_fp_step.restype = C.c_int
@@ -288,6 +290,13 @@ class Engine:
         g0, al, nl = C.c_double(), C.c_double(), C.c_int32()
         self._check(self.lib.c2d_last_kernel_ms(self.ctx, C.byref(g0), C.byref(al), C.byref(nl)))
         return g0.value, al.value, nl.value
+
+    def transport_prof(self) -> np.ndarray:
+        """Section counters of the last step's transport launches (zeros unless
+        the library was built with -DC2D_TR_PROF; tools/tr_prof.py)."""
+        out = (C.c_uint64 * abi.TR_PROF_WORDS)()
+        self._check(self.lib.c2d_transport_prof(self.ctx, out, abi.TR_PROF_WORDS))
+        return np.array(out[:], dtype=np.uint64)
 
     def last_gen0_steps(self) -> int:
         n = C.c_int64()

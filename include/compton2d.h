@@ -401,6 +401,11 @@ int  c2d_fp_step(c2d_ctx* ctx, const c2d_fp_step_in* in, c2d_fp_step_out* out);
  * milliseconds and launches, measured with HIP events on the library's
  * own stream. */
 int  c2d_last_kernel_ms(c2d_ctx* ctx, double* gen0_ms, double* all_ms, int32_t* launches);
+/* Diagnostic: section counters of the last step's transport launches
+ * (wave-level shader cycles and event counts, tools/tr_prof.py).  All zero
+ * unless the library was built with -DC2D_TR_PROF (FAST_FLAGS / EXACT). */
+#define C2D_TR_PROF_WORDS 32
+int  c2d_transport_prof(c2d_ctx* ctx, uint64_t* out, int32_t n);
 /* Start an observer-frame histogram (zeroed on the device): sums of ew, of
  * ew^2 and counts per [n_t][n_mu][n_e] bin. */
 int  c2d_obs_begin(c2d_ctx* ctx, const c2d_obs_bins* bins);

@@ -36,7 +36,7 @@ def gen0_ids(rows):
         k = r["Kernel_Name"]
         if "c2d_source_kernel" in k:
             after_src = True
-        elif "c2d_transport_kernel" in k and after_src:
+        elif ("c2d_transport_kernel" in k or "c2d_bundle_kernel" in k) and after_src:
             ids.append(r["Dispatch_Id"])
             after_src = False
     return ids
