@@ -98,6 +98,44 @@ C2D_HD double c2d_log(double x) {
   return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
 }
 
+/* c2d_log for finite x > 0 without branches: every path of c2d_log is
+ * evaluated and the result selected, so a wavefront does not diverge.  The
+ * k == 0 forms of c2d_log are the general forms with dk = 0 (0 * ln2 = 0,
+ * a - b = -(b - a) exactly), so the result is bit-identical to c2d_log
+ * (tests/test_math_rng.py). */
+C2D_HD double c2d_log_pos(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+               two54 = 1.80143985094819840000e+16,
+               Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  const int sub = c2d_hi(x) < 0x00100000;    /* x < 2^-1022 */
+  x = sub ? x * two54 : x;
+  int32_t hx = c2d_hi(x);
+  int32_t k = (sub ? -54 : 0) + (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  const int32_t i = (hx + 0x95f64) & 0x100000;
+  x = c2d_with_hi(x, hx | (i ^ 0x3ff00000));
+  k += (i >> 20);
+  const double f = x - 1.0;
+  const double dk = (double)k;
+  /* -2^-20 <= f < 2^-20 */
+  const double Rs = f * f * (0.5 - 0.33333333333333333 * f);
+  const double small = dk * ln2_hi - ((Rs - dk * ln2_lo) - f);
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  const double w = z * z;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double big_a = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  const double big_b = dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+  const double big = ((hx - 0x6147a) | (0x6b851 - hx)) > 0 ? big_a : big_b;
+  return ((0x000fffff & (2 + hx)) < 3) ? small : big;
+}
+
 /* exponential (fdlibm e_exp.c) */
 C2D_HD double c2d_exp(double x) {
   const double o_threshold = 7.09782712893383973096e+02,

@@ -1617,7 +1617,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
     /* one draw: mr < 1 <= ew / deleabs always holds (ew >= 1e-40) */
     const double mr = odd ? c2d_draw_s(p.key, sub, b.pctr + 1u) : hi;
     ctr++;
-    const double sstar = -c2d_log(1.0 - mr * deleabs / b.ewp) / sigabs;
+    const double sstar = -c2d_log_pos(1.0 - mr * deleabs / b.ewp) / sigabs;
     const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
     wmustar = (wmu * rpre + sstar) / denom;
   }
@@ -1750,6 +1750,12 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
     double deleabs = b.ewp - ewnew;
     if (deleabs < 1.0e-50) deleabs = 1.0e-50;
     const bool odd = (b.pctr & 1u) != 0u;
+    /* no collision (dcol > min(dcen, trldb)) is certain when u1 < ulim: then
+     * -log(u1) exceeds sigsc * min(dcen, trldb) by a margin (1e-9 relative,
+     * 1e-12 absolute) far above every rounding of the exact test, which runs
+     * only otherwise -- so a probe that flies on needs no log and no divide */
+    const double thr = p.dcen < trldb ? p.dcen : trldb;
+    const double ulim = c2d_exp(-(sigsc * thr) * (1.0 + 1.0e-9)) * (1.0 - 1.0e-12);
     double sum_edep = 0.0, sum_prdep = 0.0;
     int nsurv = 0;
     const int G = min(P.split1 - b.g0, BUNDLE_MAX);
@@ -1760,9 +1766,14 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
       double u1, hi = 0.0;
       if (!odd) u1 = c2d_draw_pair(p.key, sub, b.pctr, &hi);
       else u1 = P.rn_lds ? *rn_slot(P, i) : c2d_draw_s(p.key, sub, b.pctr);
-      const double colmfp = -c2d_log(u1);      /* Philox uniform is never 0 */
-      const double dcol = colmfp / sigsc;
-      if (dcol < p.dcen && !(trldb < dcol)) {
+      double dcol = 0.0;
+      bool collide = false;
+      if (!(u1 < ulim)) {
+        const double colmfp = -c2d_log_pos(u1);      /* Philox uniform is never 0 */
+        dcol = colmfp / sigsc;
+        collide = dcol < p.dcen && !(trldb < dcol);
+      }
+      if (collide) {
         b.alive &= ~(1u << i);
         probe_collide(P, T, A, b, sub, dcol, odd, hi, sigabs, Eta, swmu, eta_switch, cell, lc);
         continue;
@@ -1778,7 +1789,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
           mr = c2d_draw_pair(p.key, sub, b.pctr + 1u, &h2);
           if (P.rn_lds) *rn_slot(P, i) = h2;
         }
-        const double sstar = -c2d_log(1.0 - mr * deleabs / b.ewp) / sigabs;
+        const double sstar = -c2d_log_pos(1.0 - mr * deleabs / b.ewp) / sigabs;
         const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
         wmustar = (wmu * rpre + sstar) / denom;
       } else if (!odd && P.rn_lds) {

@@ -1504,6 +1504,11 @@ void c2o_unit_math(int fn, const double* x, double* y, int64_t n) {
       case 1: y[i] = EXP(x[i]); break;
       case 2: y[i] = COS(x[i]); break;
       case 3: y[i] = ACOS(x[i]); break;
+#ifdef C2O_DETMATH
+      case 5: y[i] = c2d_log_pos(x[i]); break;   /* the GPU's branch-free log */
+#else
+      case 5: y[i] = LOG(x[i]); break;
+#endif
       default: y[i] = POW(x[i], 1.0 / 3.0); break;
     }
   }

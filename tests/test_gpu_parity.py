@@ -95,6 +95,15 @@ def test_device_math_bitwise_equals_host(fn, lo, hi):
     np.testing.assert_array_equal(yd.view(np.uint64), y.view(np.uint64))
 
 
+def test_device_branch_free_log_equals_host():
+    from test_math_rng import log_pos_inputs
+    x = log_pos_inputs()
+    y = np.zeros_like(x)
+    OL.load("det").c2o_unit_math(0, x.ctypes.data_as(abi.PD), y.ctypes.data_as(abi.PD), x.size)
+    yd = device_math(8, x)
+    np.testing.assert_array_equal(yd.view(np.uint64), y.view(np.uint64))
+
+
 def test_device_philox_equals_host():
     keys = np.array([0, 1, 0x5EEDC2D, 2 ** 53 - 1], np.float64)
     x = np.repeat(keys, 1000)

@@ -40,6 +40,31 @@ def test_det_math_vs_glibc(fn, lo, hi, maxulp):
     assert ulp_diff(yd, yr).max() <= maxulp
 
 
+def log_pos_inputs():
+    """Positive finite doubles that reach every path of c2d_log: wide range,
+    near 1 (|f| < 2^-20 and both sides of the sqrt(2) split), powers of two,
+    subnormals, (0, 1) uniforms as the transport draws them."""
+    rng = np.random.default_rng(77)
+    parts = [np.exp(rng.uniform(np.log(1e-308), np.log(1e308), 200000)),
+             1.0 + rng.uniform(-2.0 ** -19, 2.0 ** -19, 50000),
+             np.ldexp(1.0 + rng.uniform(0.0, 1.0, 50000), rng.integers(-1000, 1000, 50000)),
+             np.ldexp(1.0, np.arange(-1074, 1024)).astype(np.float64),
+             rng.uniform(0.0, 1.0, 100000), 1.0 - rng.uniform(0.0, 1e-6, 50000),
+             np.array([5e-324, 1e-310, 2.2250738585072014e-308, 1.0, 2.0, 0.5, 1.4142135623730951,
+                       0.7071067811865476, 1.7976931348623157e308])]
+    return np.concatenate(parts)
+
+
+def test_branch_free_log_bitwise_equals_log():
+    """c2d_log_pos (the bundle kernel's log, no branches) == c2d_log bit for bit."""
+    x = log_pos_inputs()
+    y0, y5 = np.zeros_like(x), np.zeros_like(x)
+    lib = OL.load("det")
+    lib.c2o_unit_math(0, x.ctypes.data_as(abi.PD), y0.ctypes.data_as(abi.PD), x.size)
+    lib.c2o_unit_math(5, x.ctypes.data_as(abi.PD), y5.ctypes.data_as(abi.PD), x.size)
+    np.testing.assert_array_equal(y5.view(np.uint64), y0.view(np.uint64))
+
+
 def test_philox_known_answers():
     lib = OL.load("det")
     # Random123 kat_vectors, philox4x32-10: (ctr, key) -> out
