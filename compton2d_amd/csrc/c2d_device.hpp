@@ -74,6 +74,11 @@ struct TallyOff {
  * are the most frequent append: +14 % transport throughput over one shared
  * counter).  Readers take the shards' filled prefixes in shard order. */
 #define C2D_EV_SHARDS 32
+/* threads per workgroup of the transport/bundle kernels (build-time knob:
+ * with C2D_WAVES_PER_EU it sets how many waves per SIMD can be resident) */
+#ifndef C2D_TR_BLOCK
+#define C2D_TR_BLOCK 512
+#endif
 #define C2D_EV_SHARD_STRIDE 16
 /* generation-0 work items are split into C2D_WORK_SHARDS contiguous ranges,
  * each with its own fetch counter (one per 128-B line); a workgroup starts
@@ -167,8 +172,6 @@ struct KParams {
   int32_t* err;
   int32_t lds_cells;        /* 1: cell tallies privatised in LDS */
   unsigned long long* prof;  /* [C2D_TR_PROF_WORDS] section counters (-DC2D_TR_PROF builds) */
-  int32_t rn_lds;           /* bundle kernel: probes' second Philox halves kept in LDS */
-  int32_t rn_off;           /* ... at this double offset of the dynamic LDS            */
   unsigned long long* cens_holes; /* bundle kernel: per wave (start, length) of its census hole */
 };
 

@@ -20,6 +20,9 @@
  *   surface source   = derive(S, TAG_SURF+side, n, surface)   side 0..3 = i,o,u,l
  *   census source    = key stored in the census record
  *   probe copy p     = (K_src, sub 1+p)                       (imctrk2d.f:125 split1 loop)
+ *   probe bundle g0  = (K_src, sub C2D_SUB_BUNDLE | g0)       probes g0.. tracked together:
+ *                      their collision decisions and absorption points;
+ *                      a collider's record carries (K_src, sub 1+p, bundle ctr)
  *   recombined       = (K_src, sub C2D_SUB_RECOMB)            (imctrk2d.f:690-704)
  *   scatter copy ii  = derive(K_par, TAG_SCAT2, ii, ctr_par; sub_par)  (imctrk2d.f:611)
  *   split3 copy ii2  = derive(K_chd, TAG_SCAT3, ii2, ctr_chd)          (imctrk2d.f:633)
@@ -87,6 +90,7 @@ C2D_RHD double c2d_u01_bits(uint32_t a, uint32_t b) {
 }
 
 #define C2D_SUB_RECOMB  0xFFFFFFu   /* 24-bit sub-stream ids: probes use 1 .. split1 */
+#define C2D_SUB_BUNDLE  0x800000u   /* | g0: the stream of the probe bundle starting at g0 */
 
 /* Draw number n of stream (key, sub).  One Philox block gives two uniforms:
  * draws 2m and 2m+1 are the low and high halves of block m, so a tracker

@@ -110,9 +110,8 @@ struct c2d_ctx {
   int n_cu = 0, max_grid = 0, lds_cells = 0;
   size_t lds_max = 64 * 1024;   /* LDS bytes a workgroup may allocate */
   size_t lds_bytes = 0;
-  /* generation 0 as probe bundles (c2d_bundle_kernel; C2D_BUNDLE=0: the
-   * per-copy tracker), its LDS with the probes' Philox halves, and grid */
-  int bundle = 1, rn_lds = 0, bundle_grid = 0;
+  /* generation 0 as probe bundles (c2d_bundle_kernel): its LDS and grid */
+  int bundle = 1, bundle_grid = 0;
   size_t bundle_lds = 0;
   unsigned long long* cens_holes = nullptr;   /* [bundle waves][2]: census chunk tails */
   long long* cens_moves = nullptr;            /* [2 * bundle waves][3]: src, dst, n     */
@@ -323,21 +322,14 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   if (orc) return fail(c, C2D_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)orc));
   c->max_grid = c->n_cu * std::max(1, blocks_per_cu);
   {
-    const char* e = getenv("C2D_BUNDLE");
-    c->bundle = (e && e[0] == '0') ? 0 : 1;
     auto occ = cfg->comtot_mode == C2D_COMTOT_TABLE ? c2d_bundle_occupancy_fast
                                                     : c2d_bundle_occupancy_exact;
-    int b0 = 0, b1 = 0;
-    const size_t rn = sizeof(double) * (size_t)std::min(cfg->split1, 32) * 512;
+    int b0 = 0;
     orc = occ(&b0, c->lds_bytes);
-    if (!orc) orc = occ(&b1, c->lds_bytes + rn);
     if (orc) return fail(c, C2D_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)orc));
-    /* keep the probes' second halves in LDS only where that costs no occupancy */
-    const char* r = getenv("C2D_RN_LDS");
-    c->rn_lds = r ? (r[0] != '0') : (b1 >= b0 && b1 > 0);
-    c->bundle_lds = c->lds_bytes + (c->rn_lds ? rn : 0);
-    c->bundle_grid = c->n_cu * std::max(1, c->rn_lds ? b1 : b0);
-    const size_t waves = (size_t)c->bundle_grid * 8;
+    c->bundle_lds = c->lds_bytes;
+    c->bundle_grid = c->n_cu * std::max(1, b0);
+    const size_t waves = (size_t)c->bundle_grid * (C2D_TR_BLOCK / 64);
     HIPCHK(c, dalloc(&c->cens_holes, 2 * waves));
     HIPCHK(c, dalloc(&c->cens_moves, 6 * waves + 6));
     c->h_holes.assign(2 * waves, 0ull);
@@ -652,8 +644,6 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.err = c->derr;
   P.lds_cells = c->lds_cells;
   P.prof = c->ctl + CTL_PROF;
-  P.rn_lds = c->rn_lds;
-  P.rn_off = (int32_t)(c->lds_bytes / sizeof(double));
   P.cens_holes = c->cens_holes;
   P.n_vol_global = c->n_vol_global;
   P.n_surf_global = c->n_surf_global;
@@ -703,7 +693,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(aux_grid_max, (n + 255) / 256));
   };
   auto tr_grid = [&](int64_t n) {
-    return (int)std::max<int64_t>(1, std::min<int64_t>(c->max_grid, (n + 511) / 512));
+    return (int)std::max<int64_t>(1, std::min<int64_t>(c->max_grid, (n + C2D_TR_BLOCK - 1) / C2D_TR_BLOCK));
   };
   HIPCHK(c, hipMemcpyAsync(c->dP, &P, sizeof(KParams), hipMemcpyHostToDevice, c->stream));
   int gen = 0, qin = 0, launches = 0;
@@ -729,7 +719,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     if (A.n_items > 0 && c->bundle) {
       auto launch_b = fast ? c2d_launch_bundle_fast : c2d_launch_bundle_exact;
       const int grid = (int)std::max<int64_t>(
-          1, std::min<int64_t>(c->bundle_grid, (A.n_items + 511) / 512));
+          1, std::min<int64_t>(c->bundle_grid, (A.n_items + C2D_TR_BLOCK - 1) / C2D_TR_BLOCK));
       int rc = launch_b(c->dP, &A, grid, c->bundle_lds, c->stream);
       if (rc) return fail(c, C2D_E_HIP, "bundle launch (gen 0): %s", hipGetErrorString((hipError_t)rc));
       launches++;

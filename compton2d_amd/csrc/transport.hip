@@ -74,7 +74,7 @@ constexpr double C_LIGHT = 2.9979245620e10;    /* general.pa:25 */
 constexpr double RAD_CP = 3.333564097e-11;     /* general.pa:23 */
 constexpr double EMASSKEV = 5.11e2;
 constexpr double SIGTHOM = 6.6516e-25;
-constexpr int BLOCK = 512;        /* transport kernel */
+constexpr int BLOCK = C2D_TR_BLOCK;   /* transport and bundle kernels */
 constexpr int SBLOCK = 256;       /* source / scatter kernels */
 constexpr long long CHUNK = 64;
 
@@ -1527,18 +1527,31 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
  * path until a probe collides.  A bundle carries up to BUNDLE_MAX probes
  * and the recombined copy along one shared path: comtot, the geometry, the
  * absorption factor and the position update are evaluated once per shared
- * step, while every probe draws its own colmfp (the collision test) and its
- * own absorption point (prdep) from its own stream.  A colliding probe
- * leaves through its own partial step (flight()'s ikind = 3 branch).
+ * step.
+ *
+ * Collisions: each probe's collision process along the path has the same
+ * rate sigsc, so (superposition) the first collision among the n probes on
+ * the path comes after an optical depth tau ~ Exp(n) per probe, the collider
+ * is uniform among the n, and by memorylessness the others fly on unchanged
+ * -- the per-copy tracker's process (a fresh colmfp per copy and step,
+ * imctrk2d.f:150-160) with other random numbers.  The bundle draws from its
+ * own stream (source key, C2D_SUB_BUNDLE | g0): tau at the start; per
+ * collision the collider, its absorption point, the others' new tau; per
+ * step the survivors' absorption points (only where xabs > 1e-5) in probe
+ * order.  A step needs no random number unless a probe collides in it or
+ * absorption is sampled.  The collider leaves through its own partial step
+ * (flight()'s ikind = 3 branch) and its collision record carries its own
+ * sub-stream (source key, 1 + probe).  The oracle's lineage mode tracks
+ * probes the same way (oracle/c2d_oracle.c probe_bundle); DESIGN.md §2c.
  *
  * The recombined copy's weight (split1 - nscat) * s_ew needs the source's
  * final collision count, so it flies with the bundle of the last probes on
  * the assumption that they do not collide; a collision in that bundle
  * cancels it (the packet-steps it was counted for are taken back) and it
  * flies alone from the source afterwards.  Its absorption-point draws are
- * only counted (its prdep is never tallied).  Every copy's arithmetic,
- * draws, records and tallies are the per-copy tracker's; only the order in
- * which cell tallies are summed differs. */
+ * only counted (its prdep is never tallied).  Geometry, absorption,
+ * deposits, records and counters are the per-copy tracker's; the cell
+ * tallies are summed in another order. */
 constexpr int BUNDLE_MAX = 32;
 enum : int32_t {
   BF_TRACK = 1,     /* the recombined copy is on the path               */
@@ -1550,19 +1563,24 @@ enum : int32_t {
 struct Bundle {
   Pkt p;              /* shared path; p.ew, p.wtmin, p.ctr: the recombined copy's */
   double ewp, wtminp; /* the probes' common weight and kill threshold               */
+  double tau;         /* optical depth (per probe) to the next collision among them */
+  double brnext;      /* second half of the bundle stream's last Philox block       */
   long long src;      /* source item                                             */
   uint32_t alive;     /* probes g0 + i still on the path (bit i)                 */
-  uint32_t pctr;      /* draws consumed by each probe on the path               */
+  uint32_t bctr;      /* draws consumed from the bundle stream                   */
   int32_t g0;         /* first probe of this bundle (== split1: refly alone)     */
   int32_t nscat;      /* probes of the source that collided                      */
   int32_t flags;
   int32_t tsteps;     /* packet-steps counted for a speculative recombined copy  */
 };
 
-/* the probes' second Philox halves (draw pctr when pctr is odd), per lane in
- * LDS when the plan has room (P.rn_lds), else recomputed */
-__device__ __forceinline__ double* rn_slot(const KParams& P, int i) {
-  return c2d_tr_lds + P.rn_off + i * BLOCK + (int)threadIdx.x;
+/* next draw of the bundle stream (source key, C2D_SUB_BUNDLE | g0) */
+__device__ __forceinline__ double UB(Bundle& b) {
+  double v;
+  if (b.bctr & 1u) v = b.brnext;
+  else v = c2d_draw_pair(b.p.key, C2D_SUB_BUNDLE | (uint32_t)b.g0, b.bctr, &b.brnext);
+  b.bctr++;
+  return v;
 }
 
 /* start (or restart) the bundle at probe g0 of source b.src */
@@ -1575,9 +1593,11 @@ __device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bun
   b.ewp = s_ew;
   b.wtminp = 1.0e-10 * ew0;
   b.alive = G >= 32 ? 0xffffffffu : ((1u << G) - 1u);
-  b.pctr = 0;
+  b.bctr = 0;
   b.flags = 0;
   b.tsteps = 0;
+  b.tau = 0.0;
+  if (G > 0) b.tau = -c2d_log_pos(UB(b)) / (double)G;
   p.nflight = 0;
   p.mode = 0;
   if (b.g0 + G == P.split1 && P.split1 - b.nscat > 0) {
@@ -1592,12 +1612,12 @@ __device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bun
   set_phi(p, p.phi);
 }
 
-/* a probe whose colmfp falls inside the shared step: its own partial step
- * to the collision point (flight(), ikind = 3), then the collision record */
+/* probe g0 + i collides at dcol inside the shared step: its own partial
+ * step to the collision point (flight(), ikind = 3), then the record */
 __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, const GenArgs& A,
-                                              Bundle& b, uint32_t sub, double dcol, bool odd,
-                                              double hi, double sigabs, double Eta, double swmu,
-                                              int eta_switch, int cell, LaneCnt& lc) {
+                                              Bundle& b, int i, double dcol, double sigabs,
+                                              double Eta, double swmu, int eta_switch, int cell,
+                                              LaneCnt& lc) {
   const double lim9 = 0.999999999;
   const Pkt& p = b.p;
   const double rpre = p.rpre, zpre = p.zpre, wmu = p.wmu;
@@ -1609,14 +1629,12 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
   const double ewnew = (xabs < 100.0) ? b.ewp * c2d_exp(-xabs) : 0.0;
   double deleabs = b.ewp - ewnew;
   if (deleabs < 1.0e-50) deleabs = 1.0e-50;
-  uint32_t ctr = b.pctr + 1u;
   double wmustar;
   if (xabs <= 0.00001) {
     wmustar = wmu;
   } else {
     /* one draw: mr < 1 <= ew / deleabs always holds (ew >= 1e-40) */
-    const double mr = odd ? c2d_draw_s(p.key, sub, b.pctr + 1u) : hi;
-    ctr++;
+    const double mr = UB(b);
     const double sstar = -c2d_log_pos(1.0 - mr * deleabs / b.ewp) / sigabs;
     const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
     wmustar = (wmu * rpre + sstar) / denom;
@@ -1635,10 +1653,10 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
   r.rpre = rnew; r.zpre = znew; r.wmu = wmu; r.phi = phi; r.ew = ewnew; r.xnu = p.xnu;
   r.dcen = p.dcen - trld;
   r.jk = ((uint32_t)p.jph << 16) | (uint32_t)p.kph;
-  r.ctr = ctr;
+  r.ctr = b.bctr;
   r.key = p.key;
   r.kap = (uint32_t)p.kap;
-  r.sub = sub;
+  r.sub = 1u + (uint32_t)(b.g0 + i);
   push_scat(P, A.q2_out, A.n2_out, r);
   b.nscat++;
   if (b.flags & BF_SPEC) {
@@ -1746,64 +1764,46 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
   TP_MARK(pf, TP_GEOM);
   /* ---- probes (mode -1) ---- */
   if (b.alive) {
-    const double ewnew = (xabs < 100.0) ? b.ewp * ex : 0.0;
-    double deleabs = b.ewp - ewnew;
-    if (deleabs < 1.0e-50) deleabs = 1.0e-50;
-    const bool odd = (b.pctr & 1u) != 0u;
-    /* no collision (dcol > min(dcen, trldb)) is certain when u1 < ulim: then
-     * -log(u1) exceeds sigsc * min(dcen, trldb) by a margin (1e-9 relative,
-     * 1e-12 absolute) far above every rounding of the exact test, which runs
-     * only otherwise -- so a probe that flies on needs no log and no divide */
-    const double thr = p.dcen < trldb ? p.dcen : trldb;
-    const double ulim = c2d_exp(-(sigsc * thr) * (1.0 + 1.0e-9)) * (1.0 - 1.0e-12);
-    double sum_edep = 0.0, sum_prdep = 0.0;
-    int nsurv = 0;
-    const int G = min(P.split1 - b.g0, BUNDLE_MAX);
-    for (int i = 0; i < G; i++) {
-      if (!((b.alive >> i) & 1u)) continue;
-      const uint32_t sub = 1u + (uint32_t)(b.g0 + i);
-      lc.steps++;
-      double u1, hi = 0.0;
-      if (!odd) u1 = c2d_draw_pair(p.key, sub, b.pctr, &hi);
-      else u1 = P.rn_lds ? *rn_slot(P, i) : c2d_draw_s(p.key, sub, b.pctr);
-      double dcol = 0.0;
-      bool collide = false;
-      if (!(u1 < ulim)) {
-        const double colmfp = -c2d_log_pos(u1);      /* Philox uniform is never 0 */
-        dcol = colmfp / sigsc;
-        collide = dcol < p.dcen && !(trldb < dcol);
-      }
-      if (collide) {
-        b.alive &= ~(1u << i);
-        probe_collide(P, T, A, b, sub, dcol, odd, hi, sigabs, Eta, swmu, eta_switch, cell, lc);
-        continue;
-      }
-      nsurv++;
-      double wmustar = wmu;
-      if (two) {
-        double mr;
-        if (!odd) {
-          mr = hi;
-        } else {
-          double h2;
-          mr = c2d_draw_pair(p.key, sub, b.pctr + 1u, &h2);
-          if (P.rn_lds) *rn_slot(P, i) = h2;
-        }
-        const double sstar = -c2d_log_pos(1.0 - mr * deleabs / b.ewp) / sigabs;
-        const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
-        wmustar = (wmu * rpre + sstar) / denom;
-      } else if (!odd && P.rn_lds) {
-        *rn_slot(P, i) = hi;
-      }
-      sum_edep += deleabs;
-      sum_prdep += deleabs * wmustar * C_LIGHT;
+    int n = __popc(b.alive);
+    lc.steps += (uint32_t)n;
+    /* collisions inside the step (ikind 3: dcol < dcen, not trldb < dcol) */
+    double dpos = 0.0;
+    for (;;) {
+      const double dcol = dpos + b.tau / sigsc;
+      if (!(dcol < p.dcen && !(trldb < dcol))) break;
+      int k = (int)(UB(b) * (double)n);
+      if (k > n - 1) k = n - 1;
+      uint32_t m = b.alive;
+      for (; k > 0; k--) m &= m - 1u;
+      const int i = __ffs(m) - 1;
+      b.alive &= ~(1u << i);
+      n--;
+      probe_collide(P, T, A, b, i, dcol, sigabs, Eta, swmu, eta_switch, cell, lc);
+      dpos = dcol;
+      if (n == 0) break;
+      b.tau = -c2d_log_pos(UB(b)) / (double)n;
     }
-    if (nsurv > 0) {
-      cell_add(P, T, TC_EDEP, cell, sum_edep);
+    if (n > 0) {
+      b.tau = b.tau - sigsc * (trld - dpos);
+      /* the n probes that fly the whole step (imctrk2d.f:382-462) */
+      const double ewnew = (xabs < 100.0) ? b.ewp * ex : 0.0;
+      double deleabs = b.ewp - ewnew;
+      if (deleabs < 1.0e-50) deleabs = 1.0e-50;
+      double sum_prdep = 0.0;
+      if (two) {
+        for (int t = 0; t < n; t++) {
+          const double mr = UB(b);
+          const double sstar = -c2d_log_pos(1.0 - mr * deleabs / b.ewp) / sigabs;
+          const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
+          sum_prdep += deleabs * ((wmu * rpre + sstar) / denom) * C_LIGHT;
+        }
+      } else {
+        sum_prdep = (double)n * (deleabs * wmu * C_LIGHT);
+      }
+      cell_add(P, T, TC_EDEP, cell, (double)n * deleabs);
       cell_add(P, T, TC_PRDEP, cell, sum_prdep);
-      b.pctr += two ? 2u : 1u;
       if (ewnew <= b.wtminp) {
-        atomicAdd(&c2d_cnt_lds[C2D_CNT_KILLED], (uint32_t)nsurv);
+        atomicAdd(&c2d_cnt_lds[C2D_CNT_KILLED], (uint32_t)n);
         b.alive = 0;
       } else {
         b.ewp = ewnew;
@@ -1899,7 +1899,8 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
 
   Bundle b;
   b.p.mode = 0; b.p.kap = 0; b.p.ctr = 0; b.p.key = 0; b.p.sub = 0; b.p.nflight = 0;
-  b.alive = 0; b.flags = 0; b.src = 0; b.g0 = 0; b.nscat = 0; b.pctr = 0; b.tsteps = 0;
+  b.alive = 0; b.flags = 0; b.src = 0; b.g0 = 0; b.nscat = 0; b.bctr = 0; b.tsteps = 0;
+  b.tau = 0.0; b.brnext = 0.0; b.ewp = 0.0; b.wtminp = 0.0;
   bool busy = false;
   ComCache cc = {-1, -1, 0.0, 0.0};
   LaneCnt lc = {0u};

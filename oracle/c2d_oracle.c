@@ -318,6 +318,7 @@ typedef struct c2o_ctx {
   double hu[C2D_NPHOMAX + 2], Elcmin[C2D_NPHLCMAX + 1], Elcmax[C2D_NPHLCMAX + 1];
   double mu[C2D_NMUMAX + 1];
   int split1, split2, split3, spl3_trg;
+  int probe_bundles;            /* lineage mode: split1 probes as bundles (C2O_PROBE_BUNDLES=0: per copy) */
   int spec_switch, cr_sent, pair_switch, kappa_lag, rand_switch;
   int rng_mode, h4_stale;
   int rank, world;              /* lineage-sharded sources (global index % world == rank) */
@@ -901,6 +902,195 @@ static int flight_loop(c2o_ctx* c, pkt_t* p, int s, rng_t* g, double wtmin) {
   }
 }
 
+/* Lineage mode: the split1 probe copies of a source (imctrk2d(-1),
+ * imctrk2d.f:106-123) as probe bundles, the way the GPU's bundle kernel
+ * tracks them.  The probes of a source differ only in their
+ * random numbers, so they fly one shared path until a probe collides.  Their
+ * collision processes are independent with the same rate sigsc, so the first
+ * collision among n of them is exponential with rate n*sigsc; the collider is
+ * uniform among them; by memorylessness the others continue unchanged.  A
+ * bundle of G = min(split1 - g0, C2O_BUNDLE_MAX) probes draws from one stream
+ * (source key, C2D_SUB_BUNDLE | g0):
+ *   at the start              tau = -log(u)/n   (optical depth, per probe, to the
+ *                                                next collision among the n)
+ *   per collision             u -> the collider (k-th of the n alive, k = int(u*n)),
+ *                             u -> its absorption point (xabs > 1e-5 only),
+ *                             u -> tau of the n-1 others from the collision point
+ *   per step, survivors       u -> each one's absorption point (xabs > 1e-5), in
+ *                             probe order
+ * Per copy, the geometry, absorption, deposits, collision records and
+ * counters are the per-copy tracker's (flight_loop with s = -1); only the
+ * random numbers that decide the collisions are drawn per bundle instead of
+ * per copy and step.  Returns the probes that scattered. */
+#define C2O_BUNDLE_MAX 32
+static int probe_bundle(c2o_ctx* c, const pkt_t* src, double s_ew, double wtmin, int g0, int G,
+                        const rng_t* g) {
+  const double lim8 = 9.9999999e-1, lim9 = 0.999999999;
+  rng_t gb = rng_sub(g, C2D_SUB_BUNDLE | (uint32_t)g0);
+  pkt_t p = *src;
+  p.ew = s_ew;
+  uint32_t alive = G >= 32 ? 0xffffffffu : ((1u << G) - 1u);
+  int n = G, nscat = 0;
+  double tau = -LOG(U(&gb)) / (double)n;
+  for (;;) {
+    if (p.ew < 1.0e-40) return nscat;                  /* label 110, every probe */
+    p.wmu = clampd(p.wmu, lim8);
+    int cell = CELL(c, p.jph, p.kph);
+    double comac;
+    if (c->comac_stamp[cell] == c->comac_call) {
+      comac = c->comac_ar[cell];
+    } else {
+      comac = comtot_cell(c, cell, p.xnu);
+      c->comac_ar[cell] = comac;
+      c->comac_stamp[cell] = c->comac_call;
+    }
+    const double sigsc = comac;
+    TALLY(c, counters + C2D_CNT_STEPS) += (double)n;
+    /* geometry (imctrk2d.f:228-379), shared */
+    double xqsqleft = (p.kph == 1) ? c->rmin * c->rmin : c->r[p.kph - 1] * c->r[p.kph - 1];
+    double Eta = COS(p.phi);
+    int eta_switch = (p.phi <= PI_REF && p.phi >= 1.0e-10) ? 1 : -1;
+    Eta = clampd(Eta, lim8);
+    const double rpre = p.rpre, zpre = p.zpre, wmu = p.wmu;
+    double disp = Eta * rpre;
+    double psq = rpre * rpre * (1.0 - Eta * Eta);
+    int kbnd, inout, knew, jnew;
+    double rbnd, Zbnd, f;
+    if (Eta < 0.0 && psq < xqsqleft) {
+      kbnd = p.kph - 1;
+      inout = -1;
+      rbnd = (p.kph > 1) ? c->r[p.kph - 1] : c->rmin;
+    } else {
+      kbnd = p.kph;
+      inout = 1;
+      rbnd = c->r[p.kph];
+    }
+    double dpbsq = rbnd * rbnd - psq;
+    if (dpbsq < 1.0e-6) dpbsq = 1.0e-6;
+    double disbr = (double)inout * SQRT(dpbsq) - disp;
+    double trldb = disbr / SQRT(1.0 - wmu * wmu);
+    double Zr = zpre + wmu * trldb;
+    double zlow = (p.jph == 1) ? c->zmin : c->z[p.jph - 1];
+    if (Zr > c->z[p.jph] || Zr < zlow) {
+      Zbnd = (Zr > c->z[p.jph]) ? c->z[p.jph] : zlow;
+      knew = p.kph;
+      jnew = (Zr > c->z[p.jph]) ? p.jph + 1 : p.jph - 1;
+      f = (Zbnd - zpre) * SQRT(1.0 - wmu * wmu) / wmu;
+      rbnd = SQRT(rpre * rpre + f * f + 2.0 * rpre * f * Eta);
+      trldb = SQRT(f * f + (Zbnd - zpre) * (Zbnd - zpre));
+    } else {
+      knew = p.kph + inout;
+      jnew = p.jph;
+      rbnd = (kbnd > 0) ? c->r[kbnd] : c->rmin;
+      Zbnd = Zr;
+    }
+    /* a copy that does not collide: boundary (ikind 1) or census (ikind 2) */
+    const int bnd = trldb < p.dcen;
+    const double trld = bnd ? trldb : p.dcen;
+    int ie;
+    for (ie = 1; ie <= C2D_N_VOL - 1; ie++)
+      if (p.xnu < c->E_ph[ie + 1]) break;
+    double sigabs = 1.0e-40 + 1.0 * c->kappa_use[(int64_t)cell * C2D_N_VOL + (ie - 1)];
+    if (sigabs < 1.0e-40) sigabs = 1.0e-40;
+    /* collisions inside the step (ikind 3: dcol < dcen and not trldb < dcol) */
+    double dpos = 0.0;
+    while (n > 0) {
+      const double dcol = dpos + tau / sigsc;
+      if (!(dcol < p.dcen && !(trldb < dcol))) break;
+      int k = (int)(U(&gb) * (double)n);
+      if (k > n - 1) k = n - 1;
+      int i = 0;
+      for (uint32_t m = alive;; m &= m - 1u) {
+        if (k-- == 0) { i = __builtin_ctz(m); break; }
+      }
+      alive &= ~(1u << i);
+      n--;
+      /* the collider's partial step to dcol (flight_loop, ikind = 3) */
+      pkt_t q = p;
+      const double trc = dcol;
+      const double fc = trc * SQRT(1.0 - wmu * wmu);
+      const double rnew = SQRT(fc * fc + rpre * rpre + 2.0 * fc * rpre * Eta);
+      const double znew = zpre + trc * wmu;
+      const double xabs = sigabs * trc;
+      const double ewnew = (xabs < 100.0) ? p.ew * EXP(-xabs) : 0.0;
+      double deleabs = p.ew - ewnew;
+      if (deleabs < 1.0e-50) deleabs = 1.0e-50;
+      double wmustar = wmu;
+      if (xabs > 0.00001) {
+        const double mr = U(&gb);                      /* mr < 1 <= ew/deleabs */
+        const double sstar = -LOG(1.0 - mr * deleabs / p.ew) / sigabs;
+        const double denom = SQRT(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
+        wmustar = (wmu * rpre + sstar) / denom;
+      }
+      c->T[c->L.edep + cell] = c->T[c->L.edep + cell] + deleabs;
+      c->T[c->L.prdep + cell] = c->T[c->L.prdep + cell] + deleabs * wmustar * C_LIGHT;
+      if (ewnew <= wtmin) {
+        TALLY(c, counters + C2D_CNT_KILLED) += 1.0;
+      } else {
+        q.ew = ewnew;
+        q.dcen = p.dcen - trc;
+        double Eta2 = clampd((trc + Eta * rpre) / rnew, lim9);   /* H1 */
+        q.phi = ACOS(Eta2);
+        if (eta_switch == -1) q.phi = 2.0 * PI_REF - q.phi;
+        q.rpre = rnew;
+        q.zpre = znew;
+        rng_t gp = rng_sub(g, 1u + (uint32_t)(g0 + i));
+        gp.ctr = gb.ctr;                                /* collision record: (key, probe sub, ctr) */
+        collision(c, &q, -1, &gp);
+        nscat++;
+      }
+      dpos = dcol;
+      if (n > 0) tau = -LOG(U(&gb)) / (double)n;
+    }
+    if (n == 0) return nscat;
+    tau = tau - sigsc * (trld - dpos);
+    /* the n probes that fly the whole step (imctrk2d.f:382-462) */
+    const double xabs = sigabs * trld;
+    const double ewnew = (xabs < 100.0) ? p.ew * EXP(-xabs) : 0.0;
+    double deleabs = p.ew - ewnew;
+    if (deleabs < 1.0e-50) deleabs = 1.0e-50;
+    for (uint32_t m = alive; m; m &= m - 1u) {
+      double wmustar = wmu;
+      if (xabs > 0.00001) {
+        const double mr = U(&gb);
+        const double sstar = -LOG(1.0 - mr * deleabs / p.ew) / sigabs;
+        const double denom = SQRT(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
+        wmustar = (wmu * rpre + sstar) / denom;
+      }
+      c->T[c->L.edep + cell] = c->T[c->L.edep + cell] + deleabs;
+      c->T[c->L.prdep + cell] = c->T[c->L.prdep + cell] + deleabs * wmustar * C_LIGHT;
+    }
+    if (ewnew <= wtmin) {
+      TALLY(c, counters + C2D_CNT_KILLED) += (double)n;
+      return nscat;
+    }
+    p.ew = ewnew;
+    /* the shared move */
+    double rnew, znew;
+    if (bnd) {
+      rnew = rbnd;
+      znew = Zbnd;
+    } else {
+      jnew = p.jph;
+      knew = p.kph;
+      f = trld * SQRT(1.0 - wmu * wmu);
+      rnew = SQRT(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
+      znew = zpre + trld * wmu;
+    }
+    p.dcen = p.dcen - trld;
+    Eta = (trld + Eta * rpre) / rnew;                  /* hazard H1 */
+    Eta = clampd(Eta, lim9);
+    p.phi = ACOS(Eta);
+    if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
+    p.rpre = rnew;
+    p.zpre = znew;
+    if (!bnd) return nscat;                            /* census: probes end */
+    if (jnew == c->nz + 1 || jnew == 0 || knew == c->nr + 1 || knew == 0) return nscat;
+    p.jph = jnew;
+    p.kph = knew;
+  }
+}
+
 static void imctrk2d(c2o_ctx* c, pkt_t* p, int scat_flag, rng_t* g) {
   double wtmin = 1.0e-10 * p->ew;
   int nscat = 0;
@@ -908,6 +1098,19 @@ static void imctrk2d(c2o_ctx* c, pkt_t* p, int scat_flag, rng_t* g) {
   if (scat_flag == -1) {
     sv.ew = p->ew / c->split1;
     c->comac_call++;
+  }
+  if (scat_flag == -1 && g->mode == C2O_RNG_LINEAGE && c->probe_bundles) {
+    for (int g0 = 0; g0 < c->split1; g0 += C2O_BUNDLE_MAX) {
+      const int G = (c->split1 - g0 < C2O_BUNDLE_MAX) ? c->split1 - g0 : C2O_BUNDLE_MAX;
+      nscat += probe_bundle(c, &sv, sv.ew, wtmin, g0, G, g);
+    }
+    if (c->split1 - nscat > 0) {
+      *p = sv;
+      p->ew = (double)(c->split1 - nscat) * sv.ew;
+      rng_t gr = rng_sub(g, C2D_SUB_RECOMB);
+      imctrk2d(c, p, 0, &gr);
+    }
+    return;
   }
   int niter = (scat_flag == -1) ? c->split1 : 1;
   for (int it = 0; it < niter; it++) {
@@ -1210,6 +1413,13 @@ c2o_ctx* c2o_create(const c2d_config* cfg, int rng_mode, int rand_switch, int32_
   c->nmu = cfg->nmu;
   for (int n = 1; n <= c->nmu; n++) c->mu[n] = cfg->mu[n - 1];
   c->split1 = cfg->split1;
+  {
+    /* test knob: C2O_PROBE_BUNDLES=0 tracks the lineage-mode probes one copy
+     * at a time with per-copy colmfp draws, (key, 1 + probe) streams -- the
+     * statistical reference for the bundles (tests/test_bundle_statistics.py) */
+    const char* e = getenv("C2O_PROBE_BUNDLES");
+    c->probe_bundles = !(e && e[0] == '0');
+  }
   c->split2 = cfg->split2;
   c->split3 = cfg->split3;
   c->spl3_trg = cfg->spl3_trg;

@@ -73,6 +73,10 @@ FP_CASES = {
     # 460 run with the MPI build's inert positrons (hazard H6)
     "fp_pair": dict(case=dict(nz=2, nr=2, n_e=4.0e6, nst=400, T_const=0, pick_sw=1,
                               turb_lev=1.0e-2, pair_switch=1), nsteps=3),
+    # shock injection of a Gaussian (inj_dis = 1, src/update2d.f:1254-1258)
+    # centred at the deck's inj_gg/inj_sigma, without the flare
+    "fp_gauss": dict(case=dict(nz=2, nr=2, n_e=4.0e6, nst=400, T_const=0, inj_switch=1, inj_dis=1,
+                               inj_t=0.0, inj_L=5e40, inj_gg=3.0e2, inj_sigma=3.0e1), nsteps=3),
 }
 FP_CONST_KEYS = ("cf_sentinel", "r_flare", "z_flare", "t_flare", "sigma_r", "sigma_z", "sigma_t",
                  "flare_amp", "r_esc", "r_acc", "inj_switch", "inj_dis", "g2var_switch", "pick_sw",

@@ -59,7 +59,7 @@ class GoldenCase:
         return self.a["out%d_%s" % (n, key)]
 
 
-FP_CASES = ("fp_pick", "fp_inj", "fp_pair")
+FP_CASES = ("fp_pick", "fp_inj", "fp_pair", "fp_gauss")
 
 
 def fp_fic() -> np.ndarray:

@@ -17,6 +17,7 @@ SOURCES = 2_000_000                  # per reference (fib) run: ~1.9e6 escapes
 LINEAGE_SOURCES = 10_000_000         # the lineage-stream run: ~9.5e6 escapes
 FIB_SEEDS = (9857, 24680, 13579)
 LINEAGE_SEED = 0x5EEDC2D
+SHARDS = 8                           # the lineage run in 8 lineage shards
 DT_FACTOR = 30.0
 
 
@@ -34,6 +35,18 @@ def workload(mode=abi.COMTOT_EXACT, seed=LINEAGE_SEED, rank=0, world=1, n=SOURCE
 def f_of_e(fout):
     de = np.diff(synth.photon_grid())
     return np.asarray(fout)[..., :de.size].sum(axis=0) / de
+
+
+def band_errors(edout_fib, edout_shards):
+    """Relative 1-sigma statistical error of each light-curve band of the
+    fib mean (seed scatter / sqrt(seeds)) and of the lineage shard sum
+    (shard scatter * sqrt(shards)), combined."""
+    f, sh = np.asarray(edout_fib, float), np.asarray(edout_shards, float)
+    m, tot = f.mean(axis=0), sh.sum(axis=0)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        sd_f = f.std(axis=0, ddof=1) / np.sqrt(f.shape[0]) / m
+        sd_l = sh.std(axis=0, ddof=1) * np.sqrt(sh.shape[0]) / tot
+    return np.hypot(sd_f, sd_l)
 
 
 def rel_l2(a, b):

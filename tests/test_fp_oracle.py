@@ -111,3 +111,26 @@ def test_fp_pair_switch_rejects_positron_population():
     with pytest.raises(RuntimeError):
         OL.fp_step(case.grid(), case.constants(), fi["ncycle"], fi["time"], fi["dt"], fi, fi,
                    flavor="ref")
+
+
+def test_fp_gaussian_injection_branch_is_exercised():
+    """fp_gauss runs the reference with inj_switch = 1, inj_dis = 1: the shock
+    injects a Gaussian in gamma (src/update2d.f:1254-1258) into the zones the
+    front crosses (:1249-1251).  Its outputs are bit-exact (tests above); here:
+    the branch really ran on the fixture -- the same solve without injection,
+    and the same solve with the power-law profile (inj_dis = 2), both differ
+    from the reference's output."""
+    case = FpGoldenCase("fp_gauss")
+    assert case.constants().inj_dis == 1 and case.constants().inj_switch == 1
+    for variant in ("off", "powerlaw"):
+        differs = False
+        for n in case.steps:
+            fi = case.fp_in(n)
+            c = case.constants()
+            if variant == "off":
+                c.inj_switch = 0
+            else:
+                c.inj_dis = 2
+            r = OL.fp_step(case.grid(), c, fi["ncycle"], fi["time"], fi["dt"], fi, fi, flavor="ref")
+            differs |= not np.array_equal(r["f_nt"], case.fp_out(n)["f_nt"])
+        assert differs, variant

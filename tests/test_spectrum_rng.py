@@ -22,7 +22,7 @@ import oracle_lib as OL
 import spectrum_case as S
 
 FIX = Path(__file__).resolve().parent / "golden" / "spectrum_fib.npz"
-SHARDS = 8
+SHARDS = S.SHARDS
 
 
 def test_lineage_rng_spectrum_within_1pct_of_reference_streams(capsys):
@@ -36,6 +36,8 @@ def test_lineage_rng_spectrum_within_1pct_of_reference_streams(capsys):
     for i, r in enumerate(fib):                       # the fixture is this computation
         np.testing.assert_array_equal(r[0], fx["F"][i])
         np.testing.assert_array_equal(r[1], fx["edout"][i])
+    for i, r in enumerate(lin):
+        np.testing.assert_array_equal(r[1], fx["lineage_edout_shards"][i])
     # the lineage run: the per-packet streams scale the weights by 1/(sources)
     # through ewsv, so the sharded sum is F(E) of 1e7 packets at the same
     # normalisation as one 2e6-packet reference run
@@ -47,32 +49,34 @@ def test_lineage_rng_spectrum_within_1pct_of_reference_streams(capsys):
     assert min(r[2] for r in fib) >= 1.0e6 and esc_lin >= 5.0e6
     cross = S.rel_l2(F_lin, F_ref)
     floor = [S.rel_l2(a[0], b[0]) for a, b in itertools.combinations(fib, 2)]
-    # light curves per band (lcb_01.dat columns): the bands the reference
-    # reproduces between seeds to < 0.2 % at this size (the two synchrotron
-    # bands) carry the 1 % bound; the Compton bands are a few rare large-gain
-    # packets (~3 collisions per 1e6 packets in this thin medium; reference
-    # scatter 50-90 % between seeds at 2e6 packets) and must agree within
-    # that scatter.  (At n_e x 5e4 the two generators' collision counts agree
-    # to their Poisson noise: 14325 vs 14370 per 1e5 packets, 4 seeds each.)
+    # light curves per band (lcb_01.dat columns).  Each band's statistical
+    # error is estimated from both sides: the reference's seed-to-seed
+    # scatter (3 runs) and the lineage run's shard-to-shard scatter (8 shards
+    # of 1.25e6 sources).  The synchrotron bands are carried by the
+    # unscattered copies (errors < 0.2 %) and hold the 1 % bound; a band that
+    # rare Compton events reach (~3 collisions per 1e6 packets in this thin
+    # medium, each handing split2 x split3 secondaries a large gain) has a
+    # heavy tail that 3 reference seeds under-sample, so it must agree within
+    # 4 sigma of the combined error.  (At n_e x 5e4 the two generators'
+    # collision counts agree to their Poisson noise: 14325 vs 14370 per 1e5
+    # packets, 4 seeds each.)
     E_all = np.array([r[1] for r in fib])
+    sig_b = S.band_errors(E_all, [r[1] for r in lin])
     bands = [i for i in range(E_all.shape[1]) if E_all[:, i].min() > 0]
     lc = []
     for i in bands:
-        sd = E_all[:, i].std(ddof=1) / E_ref[i]
         dev = abs(E_lin[i] - E_ref[i]) / E_ref[i]
-        lc.append((i, dev, sd))
+        lc.append((i, dev, float(sig_b[i])))
     with capsys.disabled():
         print("\nF(E) rel L2, lineage (%.3g escapes) vs reference streams (3 x %.3g): %.4f; "
               "reference seed-to-seed floor (pairs of %.3g): %s" % (
                   esc_lin, fib[0][2], cross, fib[0][2], ["%.4f" % x for x in floor]))
-        print("light curves per band (band, |dev|, reference seed scatter): %s" %
+        print("light curves per band (band, |dev|, combined 1-sigma error): %s" %
               ["(%d, %.4f, %.4f)" % x for x in lc])
     assert cross <= 1.0e-2, cross
-    for i, dev, sd in lc:
-        if sd < 2.0e-3:
-            assert dev <= 1.0e-2, (i, dev, sd)
-        else:
-            assert dev <= 4.0 * sd * np.sqrt(1.0 / 3 + 1.0 / 5), (i, dev, sd)
+    for i, dev, sig in lc:
+        assert dev <= max(1.0e-2, 4.0 * sig), (i, dev, sig)
+    assert lc[0][2] < 2.0e-3 and lc[0][1] <= 1.0e-2     # the first synchrotron band: 1 %
     # no bias beyond the noise: the larger-sample comparison is no further
     # apart than two reference runs of 2e6 packets are from each other
     assert cross <= max(floor), (cross, floor)

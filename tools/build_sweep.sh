@@ -1,13 +1,13 @@
 #!/bin/bash
 # Build tuning variants of libcompton2d.so into compton2d_amd/sweep/<tag>/
 # (select one at run time with C2D_LIBRARY=...).
-# Usage: tools/build_sweep.sh tag:WPE:CONTRACT[:FLAG,FLAG...] ...
+# Usage: tools/build_sweep.sh tag:WPE:CONTRACT[:FLAG,FLAG...[:TRBLOCK]] ...
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 for spec in "$@"; do
-  IFS=: read -r tag wpe con flags <<< "$spec"
+  IFS=: read -r tag wpe con flags trb <<< "$spec"
   out=$ROOT/compton2d_amd/sweep/$tag
   mkdir -p "$out"
   make -s -C "$ROOT/compton2d_amd/csrc" OUT="$out/libcompton2d.so" BUILD="$ROOT/build/sweep/$tag" \
-       WPE="$wpe" FAST_CONTRACT="$con" FAST_FLAGS="${flags//,/ }" -j4
+       WPE="$wpe" FAST_CONTRACT="$con" FAST_FLAGS="${flags//,/ }" TRBLOCK="${trb:-512}" -j4
 done

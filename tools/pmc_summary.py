@@ -151,7 +151,25 @@ def main(root):
                     64 * c.get("SQ_INSTS_VALU", 0) / st, 64 * c.get("SQ_INSTS_SALU", 0) / st,
                     64 * c.get("SQ_INSTS_VMEM", 0) / st))
     json.dump(res, open(os.path.join(root, "summary.json"), "w"), indent=1)
+    return res
+
+
+def latest(res, workload_key, source):
+    """The per-packet-step figures bench.py reads (profiles/pmc_latest.json)."""
+    return {"workload_key": workload_key,
+            "hbm_bytes_per_step": res.get("hbm_bytes_per_step"),
+            "valu_wave_insts_per_step": res.get("valu_wave_insts_per_step"),
+            "transport_valu_issue_frac": res.get("transport_valu_issue_frac"),
+            "fp_valu_issue_frac": res.get("fp_valu_issue_frac"),
+            "fp_wait_frac": res.get("fp_wait_frac"),
+            "fp_simd_occupancy": res.get("fp_simd_occupancy"),
+            "fp_waves": res.get("fp_waves"),
+            "source": source}
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    # pmc_summary.py <profile dir> [--latest <workload_key> <source text>]
+    r = main(sys.argv[1])
+    if len(sys.argv) > 3 and sys.argv[2] == "--latest":
+        out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "pmc_latest.json")
+        json.dump(latest(r, sys.argv[3], " ".join(sys.argv[4:])), open(out, "w"), indent=1)
