@@ -11,6 +11,7 @@
 namespace c2d {
 
 /* Run-constant grids, 1-based like the reference COMMON arrays. */
+#define C2D_IDX_BUCKETS 2048       /* 128 octaves at 1/16 octave */
 struct Geo {
   double z[C2D_MAXZONE + 1];          /* z[0] = zmin, z[1..nz]           */
   double r[C2D_MAXZONE + 1];          /* r[0] = rmin, r[1..nr]           */
@@ -20,6 +21,14 @@ struct Geo {
   double Elcmin[C2D_NPHLCMAX + 1];
   double Elcmax[C2D_NPHLCMAX + 1];
   double mu[C2D_NMUMAX + 1];
+  /* bin lookup without bisection (grid_lookup): the top 16 bits of a
+   * positive double (exponent + 4 mantissa bits, 1/16 octave) minus those of
+   * the grid's first value select a bucket; *_start[bucket] = the bin of the
+   * bucket's smallest double, from which an upward scan of <= 2 bins finds
+   * the bin of x.  Built on the host with the bisection's semantics. */
+  int16_t eph_start[C2D_IDX_BUCKETS];
+  int16_t efl_start[C2D_IDX_BUCKETS];
+  int32_t eph_k0, efl_k0;
 };
 /* LDS image of Geo (everything but nothing else). */
 constexpr int GEO_DOUBLES = (int)(sizeof(Geo) / sizeof(double));
@@ -77,7 +86,7 @@ struct TallyOff {
 /* threads per workgroup of the transport/bundle kernels (build-time knob:
  * with C2D_WAVES_PER_EU it sets how many waves per SIMD can be resident) */
 #ifndef C2D_TR_BLOCK
-#define C2D_TR_BLOCK 512
+#define C2D_TR_BLOCK 256
 #endif
 #define C2D_EV_SHARD_STRIDE 16
 /* generation-0 work items are split into C2D_WORK_SHARDS contiguous ranges,
@@ -243,6 +252,11 @@ struct FpParams {
   double* P_out;
   double* zout;            /* [ncell][FO_N]                                    */
   int32_t* err;
+  /* gamma_bar memo shared by every zone and step (fp.hip GbMemo): keys are
+   * the bits of Theta (0 = empty), values gamma_bar (0 = not yet written) */
+  unsigned long long* gb_key;
+  double* gb_val;
+  uint32_t gb_mask;        /* slots - 1 (power of two)                         */
 };
 
 /* ---- observer-frame binning (observe.hip) ---- */

@@ -167,6 +167,8 @@ struct c2d_ctx {
   double *fp_FT = nullptr, *fp_mcd = nullptr, *fp_zin = nullptr, *fp_fin = nullptr, *fp_Pin = nullptr,
          *fp_nf = nullptr, *fp_fout = nullptr, *fp_Pout = nullptr, *fp_zout = nullptr;
   int32_t* fp_err = nullptr;
+  unsigned long long* fp_gb_key = nullptr;   /* gamma_bar memo (fp.hip GbMemo) */
+  double* fp_gb_val = nullptr;
   float last_fp_ms = 0.f;
   int last_fp_waves = 0;
   /* emission / absorption tables (c2d_volume_em) */
@@ -209,6 +211,35 @@ static hipError_t dalloc(T** p, size_t n) {
 extern "C" const char* c2d_version(void) { return "compton2d_amd 0.1.0 (gfx950)"; }
 
 extern "C" const char* c2d_last_error(c2d_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+/* Geo bucket tables of grid_lookup (c2d_device.hpp): bucket b holds the
+ * bin (smallest i in [1, n] with x < E[i+1], the bisection's answer) of the
+ * smallest double whose top 16 bits are k0 + b. */
+static int grid_bin_host(const double* E, int n, double x) {
+  int lo = 1, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (x < E[mid + 1]) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+static void build_lookup(const double* E, int n, int16_t* start, int32_t* k0) {
+  uint64_t u;
+  std::memcpy(&u, &E[1], sizeof u);
+  *k0 = (int32_t)(u >> 48);
+  for (int b = 0; b < C2D_IDX_BUCKETS; b++) {
+    const uint64_t k = (uint64_t)(*k0 + b);
+    double x = 0.0;
+    if (k < 0x7ff0) {
+      const uint64_t v = k << 48;
+      std::memcpy(&x, &v, sizeof x);
+      start[b] = (int16_t)grid_bin_host(E, n, x);
+    } else {
+      start[b] = (int16_t)(b > 0 ? start[b - 1] : 1);
+    }
+  }
+}
 
 extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   if (!cfg || !out) return C2D_E_ARG;
@@ -254,6 +285,8 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   for (int k = 0; k < c->nr; k++) g.r[k + 1] = cfg->r[k];
   for (int i = 0; i < C2D_N_VOL; i++) g.E_ph[i + 1] = cfg->E_ph[i];
   for (int i = 0; i < C2D_NPHFIELD; i++) g.E_field[i + 1] = cfg->E_field[i];
+  build_lookup(g.E_ph, C2D_N_VOL, g.eph_start, &g.eph_k0);
+  build_lookup(g.E_field, C2D_NPHFIELD, g.efl_start, &g.efl_k0);
   for (int i = 0; i <= cfg->nphtotal; i++) g.hu[i + 1] = cfg->hu[i];
   for (int m = 0; m < cfg->nph_lc; m++) {
     g.Elcmin[m + 1] = cfg->Elcmin[m];
@@ -366,7 +399,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
   for (void* q : vptrs)
     if (q) (void)hipFree(q);
   void* fptrs[] = {c->fp_FT, c->fp_mcd, c->fp_zin, c->fp_fin, c->fp_Pin, c->fp_nf, c->fp_fout, c->fp_Pout,
-                   c->fp_zout, c->fp_err};
+                   c->fp_zout, c->fp_err, c->fp_gb_key, c->fp_gb_val};
   for (void* p : fptrs)
     if (p) (void)hipFree(p);
   c->pk.release();
@@ -1161,6 +1194,7 @@ extern "C" int c2d_last_kernel_ms(c2d_ctx* c, double* gen0_ms, double* all_ms, i
  * (c2d_wave.hpp): t_n by repeated multiplication exactly as the reference
  * loop forms it, with the argument-independent factors of each term (same
  * c2d_math code and rounding as the kernels).  Built once per context. */
+#define C2D_FP_MEMO_SLOTS (1u << 16)
 static int ensure_mcd(c2d_ctx* c) {
   if (c->fp_mcd) return C2D_OK;
   std::vector<double> mt((size_t)C2D_FP_MCD_N * 4);
@@ -1176,6 +1210,15 @@ static int ensure_mcd(c2d_ctx* c) {
   }
   HIPCHK(c, dalloc(&c->fp_mcd, mt.size()));
   HIPCHK(c, hipMemcpy(c->fp_mcd, mt.data(), mt.size() * sizeof(double), hipMemcpyHostToDevice));
+  /* the gamma_bar memo lives as long as the context (gamma_bar is a pure
+   * function of Theta); C2D_FP_MEMO=0 disables it (A/B) */
+  const char* e = getenv("C2D_FP_MEMO");
+  if (!(e && e[0] == '0')) {
+    HIPCHK(c, dalloc(&c->fp_gb_key, C2D_FP_MEMO_SLOTS));
+    HIPCHK(c, dalloc(&c->fp_gb_val, C2D_FP_MEMO_SLOTS));
+    HIPCHK(c, hipMemset(c->fp_gb_key, 0, sizeof(unsigned long long) * C2D_FP_MEMO_SLOTS));
+    HIPCHK(c, hipMemset(c->fp_gb_val, 0, sizeof(double) * C2D_FP_MEMO_SLOTS));
+  }
   return C2D_OK;
 }
 
@@ -1292,6 +1335,7 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   P.f_out = el_dev ? c->f_nt : c->fp_fout;
   P.P_out = el_dev ? c->Pnt : c->fp_Pout;
   P.zout = c->fp_zout; P.err = c->fp_err;
+  P.gb_key = c->fp_gb_key; P.gb_val = c->fp_gb_val; P.gb_mask = C2D_FP_MEMO_SLOTS - 1u;
   HIPCHK(c, hipEventRecord(c->ev_g0a, st));
   c->last_fp_waves = c2d_fp_waves(nc, 4 * c->n_cu);
   int rc = c2d_launch_fp(&P, nc, c->last_fp_waves, st);

@@ -243,14 +243,73 @@ __device__ double gamma_bar_lane(double Theta, const double* __restrict__ tab, l
   return g;
 }
 
+/* gamma_bar memo shared by every zone of the launch and by later steps
+ * (FpParams.gb_*, allocated with the McDonald table).  gamma_bar is a pure
+ * function of Theta, and the temperature searches of zones that start from
+ * the same Theta (C3: every zone from the 1000 keV tea clamp, update2d.f:
+ * 266-276) walk the same chain Theta*1.005^k bit for bit, so one zone's
+ * McDonald pairs serve all of them, step after step.  Open addressing on the
+ * bits of Theta; a slot's key is claimed once by CAS (0 -> key) and its
+ * value written once, by the claimer, so a reader that finds the key and a
+ * non-zero value (gamma_bar >= 1) has the exact value; anything else (stale
+ * line, value not yet written, table full) is a miss and the caller computes
+ * -- results are bit-identical either way. */
+constexpr int GB_PROBES = 8;
+struct GbMemo {
+  unsigned long long* key;
+  double* val;
+  uint32_t mask;
+};
+__device__ __forceinline__ uint32_t gb_hash(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  return (uint32_t)k;
+}
+__device__ __forceinline__ bool gb_lookup(const GbMemo& M, double th, double& g) {
+  if (!M.key) return false;
+  const unsigned long long k = c2d_bits(th);
+  uint32_t h = gb_hash(k) & M.mask;
+  for (int i = 0; i < GB_PROBES; i++) {
+    const unsigned long long kk = __hip_atomic_load(M.key + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (kk == k) {
+      const double v = __hip_atomic_load(M.val + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v != 0.0) { g = v; return true; }
+      return false;
+    }
+    if (kk == 0ull) return false;
+    h = (h + 1u) & M.mask;
+  }
+  return false;
+}
+__device__ __forceinline__ void gb_insert(const GbMemo& M, double th, double g) {
+  if (!M.key) return;
+  const unsigned long long k = c2d_bits(th);
+  uint32_t h = gb_hash(k) & M.mask;
+  for (int i = 0; i < GB_PROBES; i++) {
+    const unsigned long long prev = atomicCAS(M.key + h, 0ull, k);
+    if (prev == 0ull) {
+      __hip_atomic_store(M.val + h, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (prev == k) return;
+    h = (h + 1u) & M.mask;
+  }
+}
+
 /* chain member idx+1 from th0 (the search's own repeated x or / 1.005),
  * then its gamma_bar, into the batch arrays */
 template <int N>
 __device__ __forceinline__ void batch_member(McdBatch<N>& C, double th0, int dir, int idx,
-                                             const double* __restrict__ tab, long long& guard) {
+                                             const double* __restrict__ tab, long long& guard,
+                                             const GbMemo& M) {
   double c = th0;
   for (int i = 0; i <= idx; i++) c = (dir > 0) ? c * F32(1.005) : c / F32(1.005);
-  const double g = gamma_bar_lane(c, tab, guard);
+  double g;
+  if (!gb_lookup(M, c, g)) {
+    g = gamma_bar_lane(c, tab, guard);
+    gb_insert(M, c, g);
+  }
   C.bc[idx] = c;
   C.bg[idx] = g;
 }
@@ -273,13 +332,14 @@ __device__ __forceinline__ void mcd_pass_runs(const McdCoop& C, int p, int nprod
 
 /* producer waves: serve series requests until wave 0 posts MCD_CMD_EXIT */
 __device__ __forceinline__ void mcd_producer(McdCoop& C, McdBatch<NB_MAX>& B,
-                                             const double* __restrict__ tab, int wave, int lane) {
+                                             const double* __restrict__ tab, int wave, int lane,
+                                             const GbMemo& M) {
   for (;;) {
     __syncthreads();                                   /* request posted by wave 0 */
     if (C.cmd == MCD_CMD_EXIT) return;
     if (C.cmd == MCD_CMD_BATCH) {
       long long g = 0;
-      batch_member(B, C.z, C.dir, wave * FPB + lane, tab, g);
+      batch_member(B, C.z, C.dir, wave * FPB + lane, tab, g, M);
       __syncthreads();                                 /* batch complete */
       continue;
     }
@@ -367,7 +427,8 @@ __device__ __forceinline__ void mcdonald23_coop(McdCoop& C, double z, int lane, 
 /* wave 0: evaluate chain members 1..NB from th0 on every wave of the zone */
 template <int WMAX, int N>
 __device__ __forceinline__ void search_batch(McdCoop& C, McdBatch<N>& B, double th0, int dir, int lane,
-                                             const double* __restrict__ tab, long long& guard) {
+                                             const double* __restrict__ tab, long long& guard,
+                                             const GbMemo& M) {
   if (fp_nwaves<WMAX>() > 1) {
     if (lane == 0) {
       C.z = th0;
@@ -376,7 +437,7 @@ __device__ __forceinline__ void search_batch(McdCoop& C, McdBatch<N>& B, double 
     }
     __syncthreads();                                   /* post the request */
   }
-  batch_member(B, th0, dir, lane, tab, guard);
+  batch_member(B, th0, dir, lane, tab, guard, M);
   __syncthreads();                                     /* batch complete */
 }
 
@@ -526,13 +587,23 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
    * arguments (T oscillating across the crossing). gamma_bar is a pure
    * function of Theta: a 4-entry memo keyed on the exact bits returns the
    * value it would recompute (bit-identical), skipping its McDonald pair. */
+  const GbMemo memo{P.gb_key, P.gb_val, P.gb_mask};
   double memo_th[4] = {-1.0, -1.0, -1.0, -1.0}, memo_g[4] = {0.0, 0.0, 0.0, 0.0};
   int memo_next = 0;
   auto gamma_bar_m = [&](double th) -> double {
 #pragma unroll
     for (int q = 0; q < 4; q++)
       if (memo_th[q] == th) return memo_g[q];
-    const double g = gamma_bar_coop<WMAX>(s_coop, th, lane, P.mcd, guard, s_mcd);
+    double g;
+    double gm = 0.0;
+    const bool hit = gb_lookup(memo, th, gm);
+    if (__builtin_amdgcn_readfirstlane((int)hit)) {
+      g = c2d_from_bits(((unsigned long long)__builtin_amdgcn_readfirstlane((int)(c2d_bits(gm) >> 32)) << 32) |
+                        (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)c2d_bits(gm)));
+    } else {
+      g = gamma_bar_coop<WMAX>(s_coop, th, lane, P.mcd, guard, s_mcd);
+      if (lane == 0) gb_insert(memo, th, g);
+    }
 #pragma unroll
     for (int q = 0; q < 4; q++)
       if (q == memo_next) { memo_th[q] = th; memo_g[q] = g; }
@@ -548,7 +619,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
     auto& B = batch_lds<WMAX>();
     if (bdir == dir && bpos < fp_nwaves<WMAX>() * FPB && B.bc[bpos] == next) return B.bg[bpos++];
     if (k >= FP_NSINGLE && next >= F32(0.2)) {
-      search_batch<WMAX>(s_coop, B, prev, dir, lane, P.mcd, guard);
+      search_batch<WMAX>(s_coop, B, prev, dir, lane, P.mcd, guard, memo);
       bdir = dir;
       bpos = 1;
       return B.bg[0];
@@ -990,7 +1061,7 @@ __global__ void __launch_bounds__(WMAX * FPB) c2d_fp_kernel(const FpParams P) {
   if (WMAX > 1) {
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x) / FPB;
     if (wave != 0) {
-      mcd_producer(s_coop, s_batch8, P.mcd, wave, threadIdx.x % FPB);
+      mcd_producer(s_coop, s_batch8, P.mcd, wave, threadIdx.x % FPB, GbMemo{P.gb_key, P.gb_val, P.gb_mask});
       return;
     }
   }

@@ -365,6 +365,17 @@ __device__ __forceinline__ int grid_index(const double* E, int n, double x) {
   }
   return lo;
 }
+/* grid_index through the Geo bucket table (c2d_device.hpp): the same bin,
+ * one LDS read and an upward scan of <= 2 bins instead of a 9-deep chain of
+ * dependent LDS reads.  x > 0. */
+__device__ __forceinline__ int grid_lookup(const double* E, int n, const int16_t* start, int32_t k0,
+                                           double x) {
+  int b = (int)(c2d_bits(x) >> 48) - k0;
+  b = b < 0 ? 0 : (b > C2D_IDX_BUCKETS - 1 ? C2D_IDX_BUCKETS - 1 : b);
+  int i = start[b];
+  while (i < n && !(x < E[i + 1])) i++;
+  return i;
+}
 /* `i=0; do i=i+1 while (cdf(i) < rnum .and. i < n)` (imcvol2d_para.f:170-172) */
 __device__ __forceinline__ int cdf_index(const double* cdf /*0-based*/, int n, double rnum,
                                          int linear) {
@@ -602,7 +613,7 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
   int cell = (p.jph - 1) * P.nr + (p.kph - 1);
   cell_add(P, T, TC_NPCEN, cell, 1.0);
   cell_add(P, T, TC_ECENS, cell, p.ew);
-  int i = grid_index(g->E_field, C2D_NPHFIELD, p.xnu);
+  int i = grid_lookup(g->E_field, C2D_NPHFIELD, g->efl_start, g->efl_k0, p.xnu);
   double Egg_min = (g->E_field[1] * g->E_field[1]) / g->E_field[2];
 #ifdef C2D_ABLATE_NFIELD                /* profiling ablation only (tools/build_sweep.sh) */
   if (p.xnu < 0.0)
@@ -664,7 +675,7 @@ __device__ __forceinline__ void load_rec(Pkt& p, const ScatRec& r) {
 /* E_ph bin and comtot-table position depend on xnu only: computed when a
  * packet starts (source, probe restart, secondary) instead of every step. */
 __device__ __forceinline__ void cache_energy(const KParams& P, const Geo* g, Pkt& p) {
-  p.ie = grid_index(g->E_ph, C2D_N_VOL, p.xnu);
+  p.ie = grid_lookup(g->E_ph, C2D_N_VOL, g->eph_start, g->eph_k0, p.xnu);
 #if C2D_TABLE_COMTOT
   const double s = (c2d_log(p.xnu) - C2D_COMTAB_U0) * P.comtab_du_inv;
   if (s >= 1.0 && s < (double)(C2D_COMTAB_N - 3)) {
