@@ -24,9 +24,11 @@ sources per GPU (1e9 per step on 8 GPUs).
 
 Rank 0 prints ONE JSON line.  `value` = packet-steps of all ranks / the max
 over ranks of the wall time of the K timed steps.  `roofline` prices the
-dominant kernel (generation-0 transport launch) at 160 algorithmic bytes per
-packet-step and carries its VALU-issue fraction from the
-committed PMC profile; `kernels` reports the FP and table kernels beside it;
+dominant kernel (generation-0 transport launch) at 160 algorithmic bytes
+(an 80-B packet record in + out) per lane path-step, the
+pass through the geometry block that a probe bundle shares among its copies,
+and carries its measured HBM bytes and VALU-issue fraction from the committed
+PMC profile of the same command; `kernels` reports the FP and table kernels beside it;
 `cpu_baseline` times the C oracle (a port of the reference's algorithm) on
 the host's CPU share, on a strided sample of the GPU's own final census plus
 the same fraction of the step's volume sources, and the FP_calc of sampled
@@ -252,7 +254,9 @@ def main():
             return dict(packet_steps=float(c[abi.CNT_STEPS]), sources=float(c[abi.CNT_SOURCES]),
                         census=float(c[abi.CNT_CENSUS]), escapes=float(c[abi.CNT_ESCAPES]),
                         aborted=float(c[abi.CNT_ABORTED]), transport_gen0_ms=g0,
-                        transport_all_ms=al, gen0_steps=float(eng.last_gen0_steps()))
+                        transport_all_ms=al, gen0_steps=float(eng.last_gen0_steps()),
+                        gen0_paths=float(eng.last_path_steps()[0]),
+                        all_paths=float(eng.last_path_steps()[1]))
         desc = wl.description.replace("C2:", "C4 (C2 medium, per GPU):") if wk == "c4" else wl.description
 
     for _ in range(args.warmup):
@@ -276,26 +280,40 @@ def main():
         return
     g0_ms = sum(r["transport_gen0_ms"] for r in rows)
     g0_steps = sum(r["gen0_steps"] for r in rows)
+    g0_paths = sum(r["gen0_paths"] for r in rows)
     value = steps_global / elapsed
-    achieved = g0_steps * BYTES_PER_STEP / (g0_ms * 1e-3) / 1e9 if g0_ms > 0 else 0.0
+    # algorithmic bytes: SURVEY.md §8(d)'s 80-B packet record in + out per
+    # pass of a packet through the geometry block.  A probe bundle carries all
+    # the copies on its path through ONE pass, so the bytes a
+    # streamed design would move for this launch are 160 B per lane
+    # path-step; the per-copy count (the metric's unit) would exceed the
+    # chip's peak and is reported beside it only as `survey_formula_frac`.
+    g0_s = g0_ms * 1e-3
+    achieved = g0_paths * BYTES_PER_STEP / g0_s / 1e9 if g0_ms > 0 else 0.0
+    survey_frac = (g0_steps * BYTES_PER_STEP / g0_s / 1e9 / HBM_PEAK_GBS) if g0_ms > 0 else 0.0
     grid_txt = "30x9" if wk == "c3" else "%dx%d" % (args.grid, args.grid)
     workload_key = "%s_%s_%d_%s" % (wk, grid_txt, sources, args.mode)
     pmc = load_pmc(workload_key)
-    bps = pmc.get("hbm_bytes_per_step")
+    bpp = pmc.get("hbm_bytes_per_path")
     steps_per_launch = g0_steps / args.steps
-    traffic = bps * steps_per_launch if bps is not None else None
-    # VALU issue: wave-instructions per packet-step (PMC SQ_INSTS_VALU) at the
+    paths_per_launch = g0_paths / args.steps
+    traffic = bpp * paths_per_launch if bpp is not None else None
+    # VALU issue: wave-instructions per path-step (PMC SQ_INSTS_VALU) at the
     # achieved rate vs 1024 SIMDs x one wave64 VALU instruction per 4 cycles
-    vps = pmc.get("valu_wave_insts_per_step")
-    g0_rate = g0_steps / (g0_ms * 1e-3) if g0_ms > 0 else 0.0
-    valu_frac = (g0_rate * vps / (N_SIMD * CLOCK_HZ / 4.0)) if vps else None
+    vpp = pmc.get("valu_wave_insts_per_path")
+    g0_rate = g0_steps / g0_s if g0_ms > 0 else 0.0
+    g0_prate = g0_paths / g0_s if g0_ms > 0 else 0.0
+    valu_frac = (g0_prate * vpp / (N_SIMD * CLOCK_HZ / 4.0)) if vpp else None
     per_step = {k: float(np.mean([r[k] for r in rows])) for k in rows[0]
                 if isinstance(rows[0][k], (int, float))}
     kernels = {
         "transport_gen0": {"ms_avg": g0_ms / args.steps, "packet_steps_per_launch": steps_per_launch,
+                           "path_steps_per_launch": paths_per_launch,
+                           "packet_steps_per_path": (g0_steps / g0_paths) if g0_paths else None,
+                           "packet_steps_per_s": g0_rate, "path_steps_per_s": g0_prate,
                            "bound": "issue/latency (packet state in VGPRs); reported against HBM",
                            "hbm_frac_algorithmic": achieved / HBM_PEAK_GBS,
-                           "hbm_frac_measured": (bps * g0_rate / 1e9 / HBM_PEAK_GBS) if bps else None,
+                           "hbm_frac_measured": (bpp * g0_prate / 1e9 / HBM_PEAK_GBS) if bpp else None,
                            "valu_issue_frac": valu_frac},
         "transport_all_generations": {"ms_avg": per_step.get("transport_all_ms")},
     }
@@ -349,12 +367,16 @@ def main():
             "traffic": traffic,
             "kernel": "c2d_bundle_kernel_%s (generation 0)" % args.mode,
             "per_unit_bytes": BYTES_PER_STEP,
+            "unit_of_work": "lane path-step (one pass through imctrk2d.f:228-379 shared by the copies "
+                            "on the path; c2d_last_path_steps)",
             "kernel_ms_avg": g0_ms / args.steps,
             "traffic_unit": "bytes per launch (PMC FETCH_SIZEx2 + WRITE_SIZE), from %s" %
                             (pmc.get("source") or "no PMC profile of this workload"),
-            "traffic_bytes_per_step": bps,
+            "traffic_bytes_per_path": bpp,
             "valu_issue_frac": valu_frac,
             "steps_per_launch_avg": steps_per_launch,
+            "paths_per_launch_avg": paths_per_launch,
+            "survey_formula_frac": survey_frac,
         },
         "kernels": kernels,
         "cpu_baseline": None,

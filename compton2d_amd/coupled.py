@@ -102,11 +102,13 @@ class CoupledRun:
         self.ecens_prev = tal[o[0]:o[0] + o[1]].reshape(nz, nr).copy()
         c = tal[self._cnt:self._cnt + abi.NCOUNTERS]
         g0_ms, all_ms, _ = eng.last_kernel_ms()
+        g0_paths, all_paths = eng.last_path_steps()
         self.last = dict(
             ncycle=ncycle, tables_s=t1 - t0, transport_s=t2 - t1, allreduce_s=t3 - t2, fp_s=t4 - t3,
             step_s=t4 - t0, vem_kernel_ms=eng.last_vem_ms(), transport_gen0_ms=g0_ms,
             transport_all_ms=all_ms, fp_kernel_ms=fp_ms, packet_steps=float(c[abi.CNT_STEPS]),
-            gen0_steps=float(eng.last_gen0_steps()), sources=float(c[abi.CNT_SOURCES]),
+            gen0_steps=float(eng.last_gen0_steps()), gen0_paths=float(g0_paths),
+            all_paths=float(all_paths), sources=float(c[abi.CNT_SOURCES]),
             census=float(c[abi.CNT_CENSUS]), escapes=float(c[abi.CNT_ESCAPES]),
             aborted=float(c[abi.CNT_ABORTED]), mean_Te=float(np.mean(st.get("Te_new", st["tea"]))),
             volume_packets=int(nsv.sum()))

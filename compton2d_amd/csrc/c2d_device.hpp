@@ -128,6 +128,13 @@ __device__ __forceinline__ void gor(int32_t* p, int32_t v) {
  * copy is a hot spot (2.5x on the EC light-curve workload). */
 #define C2D_NF_REPL 32
 
+/* internal counter slot (not part of the tally buffer's counters, zeroed
+ * before the counters are copied there): lane path-steps = passes of a lane
+ * through the geometry block.  The per-copy tracker counts one per
+ * packet-step; the bundle kernel one per shared step of all copies on the
+ * path.  The roofline's algorithmic bytes are priced on it. */
+#define C2D_CNT_PATHS_INT 10
+
 struct KParams {
   int32_t nz, nr, ncell, nphtotal, nph_lc, nmu;
   int32_t split1, split2, split3, spl3_trg, spec_switch;

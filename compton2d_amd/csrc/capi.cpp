@@ -160,6 +160,7 @@ struct c2d_ctx {
   float last_src_ms = 0.f;
   unsigned long long last_prof[C2D_TR_PROF_WORDS] = {};  /* transport section counters */
   int64_t last_g0_steps = 0;
+  int64_t last_g0_paths = 0, last_all_paths = 0;   /* lane path-steps (C2D_CNT_PATHS_INT) */
   int last_launches = 0;
   /* Fokker-Planck */
   bool fp_ready = false;
@@ -731,7 +732,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   HIPCHK(c, hipMemcpyAsync(c->dP, &P, sizeof(KParams), hipMemcpyHostToDevice, c->stream));
   int gen = 0, qin = 0, launches = 0;
   int64_t n2 = 0, n3 = 0;
-  unsigned long long nq[CTL_CNT + 1 - CTL_N2];
+  unsigned long long nq[CTL_CNT + C2D_CNT_PATHS_INT + 1 - CTL_N2];
   /* ---- generation 0: census + sampled sources ---- */
   {
     HIPCHK(c, hipEventRecord(c->ev_g0a, c->stream));
@@ -765,6 +766,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     HIPCHK(c, hipMemcpyAsync(nq, c->ctl + CTL_N2, sizeof nq, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->last_g0_steps = (int64_t)nq[CTL_CNT - CTL_N2];
+    c->last_g0_paths = (int64_t)nq[CTL_CNT + C2D_CNT_PATHS_INT - CTL_N2];
     gen = 1;
   }
   /* ---- generations >= 1: scatter sampling, then transport of the secondaries ---- */
@@ -890,6 +892,8 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   /* counters into the fused buffer (exact integers as f64) */
   double hc[C2D_NCOUNTERS];
   for (int i = 0; i < C2D_NCOUNTERS; i++) hc[i] = (double)ctl[CTL_CNT + i];
+  c->last_all_paths = (int64_t)ctl[CTL_CNT + C2D_CNT_PATHS_INT];
+  hc[C2D_CNT_PATHS_INT] = 0.0;              /* internal: not a tally counter */
   hc[C2D_CNT_GENS] = (double)gen;
   HIPCHK(c, hipMemcpyAsync(c->T + c->L.counters, hc, sizeof hc, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1170,6 +1174,13 @@ extern "C" int c2d_fp_tridag(c2d_ctx* c, const c2d_fp_in* in, double* x) {
 extern "C" int c2d_last_gen0_steps(c2d_ctx* c, int64_t* steps) {
   if (!c || !steps) return C2D_E_ARG;
   *steps = c->last_g0_steps;
+  return C2D_OK;
+}
+
+extern "C" int c2d_last_path_steps(c2d_ctx* c, int64_t* gen0_paths, int64_t* all_paths) {
+  if (!c) return C2D_E_ARG;
+  if (gen0_paths) *gen0_paths = c->last_g0_paths;
+  if (all_paths) *all_paths = c->last_all_paths;
   return C2D_OK;
 }
 

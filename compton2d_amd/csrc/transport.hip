@@ -111,6 +111,7 @@ constexpr int MAX_REJECT = 1 << 20;
 __shared__ uint32_t c2d_cnt_lds[C2D_NCOUNTERS];   /* the workgroup's event counters */
 struct LaneCnt {
   uint32_t steps;
+  uint32_t paths;     /* lane path-steps (C2D_CNT_PATHS_INT) */
 };
 #define LC_ADD(lc, which) atomicAdd(&c2d_cnt_lds[which], 1u)
 
@@ -1170,7 +1171,9 @@ __device__ __forceinline__ void init_counters(uint32_t* sh) {
 /* after the final __syncthreads of the kernel */
 __device__ __forceinline__ void flush_counters(const KParams& P, LaneCnt& lc, uint32_t lane) {
   const uint32_t st = wave_sum(lc.steps);
+  const uint32_t pa = wave_sum(lc.paths);
   if (lane == 0 && st) atomicAdd(&c2d_cnt_lds[C2D_CNT_STEPS], st);
+  if (lane == 0 && pa) atomicAdd(&c2d_cnt_lds[C2D_CNT_PATHS_INT], pa);
   __syncthreads();
   if (threadIdx.x < C2D_NCOUNTERS && c2d_cnt_lds[threadIdx.x])
     atomicAdd(&P.cnt[threadIdx.x], (unsigned long long)c2d_cnt_lds[threadIdx.x]);
@@ -1526,6 +1529,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
       if (v != 0.0) atomicAdd(&gdst[i], v);
     }
   }
+  lc.paths = lc.steps;                  /* per-copy tracking: one copy per path */
   flush_counters(P, lc, lane);
 }
 
@@ -1695,6 +1699,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
     return;
   }
   p.wmu = clampd(p.wmu, lim8);
+  lc.paths++;
   const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
   double sigsc = 1.0;
   if (b.alive) {

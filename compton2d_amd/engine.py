@@ -97,6 +97,8 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
                                       C.POINTER(C.c_double), C.c_int64]
     lib.c2d_last_gen0_steps.restype = C.c_int
     lib.c2d_last_gen0_steps.argtypes = [vp, C.POINTER(C.c_int64)]
+    lib.c2d_last_path_steps.restype = C.c_int
+    lib.c2d_last_path_steps.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     lib.c2d_last_kernel_ms.restype = C.c_int
     lib.c2d_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                        C.POINTER(C.c_int32)]
@@ -302,6 +304,13 @@ class Engine:
         n = C.c_int64()
         self._check(self.lib.c2d_last_gen0_steps(self.ctx, C.byref(n)))
         return n.value
+
+    def last_path_steps(self) -> tuple[int, int]:
+        """(generation-0, all launches) lane path-steps of the last step: a
+        probe bundle's shared step counts once for all its copies."""
+        g0, al = C.c_int64(), C.c_int64()
+        self._check(self.lib.c2d_last_path_steps(self.ctx, C.byref(g0), C.byref(al)))
+        return g0.value, al.value
 
     # -- Fokker-Planck -------------------------------------------------------
     def fp_set_config(self, const: abi.FpConstants) -> None:

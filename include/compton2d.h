@@ -437,6 +437,13 @@ int  c2d_volume_em(c2d_ctx* ctx, const c2d_vem_in* in, c2d_vem_out* out);
 int  c2d_last_vem_ms(c2d_ctx* ctx, double* ms);
 /* Packet-steps executed by that generation-0 launch (roofline numerator). */
 int  c2d_last_gen0_steps(c2d_ctx* ctx, int64_t* steps);
+/* Lane path-steps of the last step: passes of a GPU lane through the
+ * geometry block (imctrk2d.f:228-379), of the generation-0 launch and of all
+ * launches.  The per-copy tracker makes one per packet-step; a probe bundle
+ * one per shared step of all the copies on its path, so
+ * packet-steps / path-steps is the work sharing factor.  Either pointer may
+ * be NULL. */
+int  c2d_last_path_steps(c2d_ctx* ctx, int64_t* gen0_paths, int64_t* all_paths);
 
 /* ------------------------------------------------------------------------
  * Multi-GPU tally reduction over RCCL (xGMI), for hosts that drive one

@@ -51,6 +51,10 @@ def test_exact_kernel_bit_parity_with_oracle(name):
         tg, to = eng.tallies(), orc.split()
         np.testing.assert_array_equal(tg["counters"][list(COUNTERS)], to["counters"][list(COUNTERS)],
                                       err_msg="%s step %d counters" % (name, n))
+        # lane path-steps (roofline unit): a bundle's shared step counts once
+        g0p, allp = eng.last_path_steps()
+        assert 0 < g0p <= allp <= tg["counters"][abi.CNT_STEPS], (name, n, g0p, allp)
+        assert eng.last_gen0_steps() >= g0p
         for k in TALLY_KEYS:
             ref = np.asarray(to[k])
             scale = max(np.max(np.abs(ref)), 1e-300)

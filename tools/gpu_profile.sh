@@ -12,20 +12,22 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 B="$ROOT/bench.py --no-cpu-baseline $*"
+# every pass runs the bench's own configuration (the driver's default K/W)
+K=${STEPS:-5}; W=${WARMUP:-2}
 echo "== kernel trace $(date +%T)"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
-    python3 $B --steps 5 --warmup 2 > "$OUT/bench_kt.json" 2> "$OUT/kt.err"
+    python3 $B --steps $K --warmup $W > "$OUT/bench_kt.json" 2> "$OUT/kt.err"
 echo "== FETCH_SIZE $(date +%T)"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/fetch" -o run --output-format csv -- \
-    python3 $B --steps 1 --warmup 1 > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
+    python3 $B --steps $K --warmup $W > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
 echo "== WRITE_SIZE $(date +%T)"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/write" -o run --output-format csv -- \
-    python3 $B --steps 1 --warmup 1 > "$OUT/bench_write.json" 2> "$OUT/write.err"
+    python3 $B --steps $K --warmup $W > "$OUT/bench_write.json" 2> "$OUT/write.err"
 echo "== SQ $(date +%T)"
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
     SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM \
     --kernel-trace -d "$OUT/sq" -o run --output-format csv -- \
-    python3 $B --steps 1 --warmup 1 > "$OUT/bench_sq.json" 2> "$OUT/sq.err"
+    python3 $B --steps $K --warmup $W > "$OUT/bench_sq.json" 2> "$OUT/sq.err"
 echo "== done $(date +%T)"
 python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/summary.txt"
 cat "$OUT/summary.txt"

@@ -62,9 +62,14 @@ def main(root):
         g0 = gen0_ids(rows)
         dur = [(int(by[i]["End_Timestamp"]) - int(by[i]["Start_Timestamp"])) / 1e6 for i in g0]
         print("generation-0 transport dispatches: %d; ms: %s" % (len(dur), ", ".join("%.3f" % d for d in dur)))
-        if len(dur) >= 5:
-            print("mean of the last 5 (bench timed steps): %.3f ms" % mean(dur[-5:]))
-            res["gen0_ms_timed_mean"] = mean(dur[-5:])
+        k = 5
+        try:
+            k = int(json.load(open(os.path.join(root, "bench_kt.json")))["steps"])
+        except Exception:
+            pass
+        if len(dur) >= k:
+            print("mean of the last %d (bench timed steps): %.3f ms" % (k, mean(dur[-k:])))
+            res["gen0_ms_timed_mean"] = mean(dur[-k:])
         names = {}
         for r in rows:
             n = r["Kernel_Name"].split("(")[0]
@@ -84,19 +89,29 @@ def main(root):
         g0 = gen0_ids(rows)
         if not g0:
             continue
-        did = g0[-1]
-        c = counters(d, did)
-        r = [x for x in rows if x["Dispatch_Id"] == did][0]
-        ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        # the timed generation-0 dispatches of that pass (its bench JSON's K)
         bj = os.path.join(root, "bench_%s.json" % sub)
-        steps = None
+        steps = paths = None
+        k = 1
         if os.path.exists(bj):
             try:
-                steps = json.load(open(bj))["roofline"]["steps_per_launch_avg"]
+                b = json.load(open(bj))
+                k = int(b["steps"])
+                steps = b["roofline"]["steps_per_launch_avg"] * k
+                paths = b["roofline"].get("paths_per_launch_avg")
+                paths = paths * k if paths else None
             except Exception:
-                steps = None
-        print("[%s] dispatch %s: %.3f ms, packet-steps %s, counters %s" % (sub, did, ms, steps, c))
-        res[sub] = {"ms": ms, "steps": steps, "counters": c}
+                steps = paths = None
+        ids = g0[-k:]
+        by = {r["Dispatch_Id"]: r for r in rows}
+        ms = sum((int(by[i]["End_Timestamp"]) - int(by[i]["Start_Timestamp"])) / 1e6 for i in ids)
+        c = {}
+        for i in ids:
+            for kk, v in counters(d, i).items():
+                c[kk] = c.get(kk, 0.0) + v
+        print("[%s] %d timed dispatches %s: %.3f ms, packet-steps %s, path-steps %s, counters %s"
+              % (sub, len(ids), ",".join(ids), ms, steps, paths, c))
+        res[sub] = {"ms": ms, "steps": steps, "paths": paths, "launches": len(ids), "counters": c}
     if "fetch" in res and "write" in res and res["fetch"]["steps"] and res["write"]["steps"]:
         fk = res["fetch"]["counters"].get("FETCH_SIZE", 0.0)
         wk = res["write"]["counters"].get("WRITE_SIZE", 0.0)
@@ -104,6 +119,14 @@ def main(root):
         wb = wk * 1024.0 / res["write"]["steps"]
         res["hbm_bytes_per_step"] = fb + wb
         print("HBM bytes per packet-step: fetch(x2) %.2f + write %.2f = %.2f" % (fb, wb, fb + wb))
+        if res["fetch"]["paths"] and res["write"]["paths"]:
+            fpb = fk * 1024.0 * 2.0 / res["fetch"]["paths"]
+            wpb = wk * 1024.0 / res["write"]["paths"]
+            res["hbm_bytes_per_path"] = fpb + wpb
+            res["hbm_gbs_measured"] = (fk * 1024.0 * 2.0 / (res["fetch"]["ms"] * 1e-3) +
+                                       wk * 1024.0 / (res["write"]["ms"] * 1e-3)) / 1e9
+            print("HBM bytes per lane path-step: fetch(x2) %.2f + write %.2f = %.2f; measured %.0f GB/s"
+                  % (fpb, wpb, fpb + wpb, res["hbm_gbs_measured"]))
     # the FP kernel (c2d_fp_kernel<W>): last dispatch of each pass
     fp = {}
     for sub in ("fetch", "write", "sq"):
@@ -142,6 +165,12 @@ def main(root):
                 c.get("SQ_WAIT_ANY", 0) / w, c.get("SQ_WAIT_INST_ANY", 0) / w,
                 c.get("SQ_ACTIVE_INST_ANY", 0) / w, c.get("SQ_ACTIVE_INST_VALU", 0) / w))
             st = res["sq"]["steps"]
+            pa = res["sq"]["paths"]
+            if pa:
+                res["valu_wave_insts_per_path"] = c.get("SQ_INSTS_VALU", 0) / pa
+                print("per lane path-step: VALU insts %.1f  SALU %.1f  VMEM %.2f" % (
+                    64 * c.get("SQ_INSTS_VALU", 0) / pa, 64 * c.get("SQ_INSTS_SALU", 0) / pa,
+                    64 * c.get("SQ_INSTS_VMEM", 0) / pa))
             if st:
                 res["valu_wave_insts_per_step"] = c.get("SQ_INSTS_VALU", 0) / st
                 res["transport_valu_issue_frac"] = (c.get("SQ_INSTS_VALU", 0) * 4.0 /
@@ -158,6 +187,9 @@ def latest(res, workload_key, source):
     """The per-packet-step figures bench.py reads (profiles/pmc_latest.json)."""
     return {"workload_key": workload_key,
             "hbm_bytes_per_step": res.get("hbm_bytes_per_step"),
+            "hbm_bytes_per_path": res.get("hbm_bytes_per_path"),
+            "hbm_gbs_measured": res.get("hbm_gbs_measured"),
+            "valu_wave_insts_per_path": res.get("valu_wave_insts_per_path"),
             "valu_wave_insts_per_step": res.get("valu_wave_insts_per_step"),
             "transport_valu_issue_frac": res.get("transport_valu_issue_frac"),
             "fp_valu_issue_frac": res.get("fp_valu_issue_frac"),
