@@ -21,7 +21,11 @@
  *   census source    = key stored in the census record
  *   probe copy p     = (K_src, sub 1+p)                       (imctrk2d.f:125 split1 loop)
  *   probe bundle g0  = (K_src, sub C2D_SUB_BUNDLE | g0)       probes g0.. tracked together:
- *                      their collision decisions and absorption points;
+ *                      their collision decisions and the colliders' absorption points
+ *                      (DESIGN.md §2c);
+ *   bundle points g0 = (K_src, sub C2D_SUB_ABSPT | g0)        the survivors' absorption points,
+ *                      four 32-bit uniforms per Philox block (c2d_block4), a fresh
+ *                      block for every shared step;
  *                      a collider's record carries (K_src, sub 1+p, bundle ctr)
  *   recombined       = (K_src, sub C2D_SUB_RECOMB)            (imctrk2d.f:690-704)
  *   scatter copy ii  = derive(K_par, TAG_SCAT2, ii, ctr_par; sub_par)  (imctrk2d.f:611)
@@ -91,6 +95,7 @@ C2D_RHD double c2d_u01_bits(uint32_t a, uint32_t b) {
 
 #define C2D_SUB_RECOMB  0xFFFFFFu   /* 24-bit sub-stream ids: probes use 1 .. split1 */
 #define C2D_SUB_BUNDLE  0x800000u   /* | g0: the stream of the probe bundle starting at g0 */
+#define C2D_SUB_ABSPT   0xC00000u   /* | g0: that bundle's absorption-point stream          */
 
 /* Draw number n of stream (key, sub).  One Philox block gives two uniforms:
  * draws 2m and 2m+1 are the low and high halves of block m, so a tracker
@@ -109,6 +114,18 @@ C2D_RHD double c2d_draw_pair(uint64_t key, uint32_t sub, uint32_t n, double* nex
   c2d_philox(c, (uint32_t)key, (uint32_t)(key >> 32));
   *next = c2d_u01_bits(c[2], c[3]);
   return c2d_u01_bits(c[0], c[1]);
+}
+
+/* Block m of stream (key, sub) as four 32-bit words (absorption-point
+ * uniforms: c2d_u01_32 of each word). */
+C2D_RHD void c2d_block4(uint64_t key, uint32_t sub, uint32_t m, uint32_t w[4]) {
+  w[0] = m; w[1] = sub; w[2] = 0u; w[3] = C2D_DRAW_C3;
+  c2d_philox(w, (uint32_t)key, (uint32_t)(key >> 32));
+}
+
+/* Uniform in (0,1) from 32 random bits, never 0 or 1 (exact). */
+C2D_RHD double c2d_u01_32(uint32_t a) {
+  return ((double)a + 0.5) * 2.3283064365386962890625e-10;   /* 2^-32 */
 }
 
 C2D_RHD uint64_t c2d_derive_s(uint64_t key, uint32_t tag, uint32_t a, uint32_t b, uint32_t sub) {

@@ -1583,6 +1583,7 @@ struct Bundle {
   long long src;      /* source item                                             */
   uint32_t alive;     /* probes g0 + i still on the path (bit i)                 */
   uint32_t bctr;      /* draws consumed from the bundle stream                   */
+  uint32_t actr;      /* blocks consumed from the absorption-point stream        */
   int32_t g0;         /* first probe of this bundle (== split1: refly alone)     */
   int32_t nscat;      /* probes of the source that collided                      */
   int32_t flags;
@@ -1609,6 +1610,7 @@ __device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bun
   b.wtminp = 1.0e-10 * ew0;
   b.alive = G >= 32 ? 0xffffffffu : ((1u << G) - 1u);
   b.bctr = 0;
+  b.actr = 0;
   b.flags = 0;
   b.tsteps = 0;
   b.tau = 0.0;
@@ -1806,12 +1808,40 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
       double deleabs = b.ewp - ewnew;
       if (deleabs < 1.0e-50) deleabs = 1.0e-50;
       double sum_prdep = 0.0;
+#ifdef C2D_ABLATE_PROBE_ABS            /* profiling ablation only (tools/build_sweep.sh) */
+      if (two && n < 0) {
+#else
       if (two) {
-        for (int t = 0; t < n; t++) {
-          const double mr = UB(b);
-          const double sstar = -c2d_log_pos(1.0 - mr * deleabs / b.ewp) / sigabs;
-          const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
-          sum_prdep += deleabs * ((wmu * rpre + sstar) / denom) * C_LIGHT;
+#endif
+        /* the survivors' absorption points: four 32-bit uniforms per block of
+         * the bundle's point stream, a fresh block per shared step */
+        const double q = deleabs / b.ewp;
+        const uint32_t sub = C2D_SUB_ABSPT | (uint32_t)b.g0;
+#if C2D_TABLE_COMTOT
+        const double isig = 1.0 / sigabs;
+        const double A = wmu * rpre, B = rpre * rpre;
+#endif
+        for (int t = 0; t < n; t += 4) {
+          uint32_t w[4];
+          c2d_block4(p.key, sub, b.actr++, w);
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            if (t + j < n) {
+              const double x = c2d_u01_32(w[j]) * q;
+#if C2D_TABLE_COMTOT
+              /* -log(1-x): series below 1e-4 (truncation < x^4/5 relative) */
+              const double L = (x < 1.0e-4) ? x * (1.0 + x * (0.5 + x * (0.33333333333333333 + x * 0.25)))
+                                            : -c2d_log_pos(1.0 - x);
+              const double sstar = L * isig;
+              const double denom = __builtin_sqrt(B + sstar * (2.0 * A + sstar));
+              sum_prdep += deleabs * ((A + sstar) / denom) * C_LIGHT;
+#else
+              const double sstar = -c2d_log_pos(1.0 - x) / sigabs;
+              const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
+              sum_prdep += deleabs * ((wmu * rpre + sstar) / denom) * C_LIGHT;
+#endif
+            }
+          }
         }
       } else {
         sum_prdep = (double)n * (deleabs * wmu * C_LIGHT);
