@@ -43,10 +43,18 @@ struct SpecDev {             /* file_sp table (imcsurf2d_para.f:544-685) */
 };
 
 /* Census packet store, SoA (record of imctrk2d.f:558-572 + lineage key). */
+/* Census SoA.  Exact build: `phi` is the reference's azimuth.  Fast build
+ * (tabulated comtot) stores the azimuth encoded as the flight carries it:
+ * `phi` holds Eta = cos(phi) and bit C2D_CENS_ESW of `bins` the quadrant
+ * switch (phi > pi or phi < 1e-10), so a census packet costs no acos when it
+ * is written and no cos when it is read back; the host decodes and encodes
+ * with the same c2d_acos / c2d_cos (c2d_census_export / _import), so the
+ * records it sees are the ones the fast kernel wrote before this encoding. */
+#define C2D_CENS_ESW (1u << 24)
 struct CensusSoA {
   double* rpre; double* zpre; double* wmu; double* phi; double* ew; double* xnu;
   uint32_t* jk;      /* jph << 16 | kph (1-based)                  */
-  uint32_t* bins;    /* jgpsp | jgplc << 8 | jgpmu << 16            */
+  uint32_t* bins;    /* jgpsp | jgplc << 8 | jgpmu << 16 (| C2D_CENS_ESW) */
   uint64_t* key;
 };
 

@@ -970,6 +970,17 @@ extern "C" int c2d_events(c2d_ctx* c, double* buf, int64_t cap, int64_t* n) {
   return C2D_OK;
 }
 
+/* Fast contexts keep the census azimuth encoded (CensusSoA): phi column =
+ * cos(phi), C2D_CENS_ESW in bins = the quadrant switch.  The host sees the
+ * reference's phi: decoded with the kernel's own c2d_acos, encoded with its
+ * c2d_cos (the value the kernel's set_phi would compute). */
+static constexpr double C2D_PI_REF = 3.1415926536;   /* general.pa:24 */
+static inline bool cens_encoded(const c2d_ctx* c) { return c->cfg.comtot_mode == C2D_COMTOT_TABLE; }
+static inline double cens_phi_decode(double eta, uint32_t bins) {
+  const double ph = c2d_acos(eta);
+  return (bins & C2D_CENS_ESW) ? 2.0 * C2D_PI_REF - ph : ph;
+}
+
 extern "C" int c2d_census_count(c2d_ctx* c, int64_t* n) {
   if (!c || !n) return C2D_E_ARG;
   *n = c->n_census;
@@ -994,14 +1005,16 @@ extern "C" int c2d_census_export_range(c2d_ctx* c, int64_t first, int64_t stride
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const DevCensus& d = c->cens[c->cur_out];
   std::vector<double> col(m);
-  for (int f = 0; f < 6; f++) {
-    HIPCHK(c, col_down(col.data(), d.d[f], first, stride, m));
-    if (d6)
-      for (int64_t i = 0; i < m; i++) d6[6 * i + f] = col[i];
-  }
   std::vector<uint32_t> jk(m), bins(m);
   HIPCHK(c, col_down(jk.data(), d.jk, first, stride, m));
   HIPCHK(c, col_down(bins.data(), d.bins, first, stride, m));
+  const bool enc = cens_encoded(c);
+  for (int f = 0; f < 6; f++) {
+    HIPCHK(c, col_down(col.data(), d.d[f], first, stride, m));
+    if (d6)
+      for (int64_t i = 0; i < m; i++)
+        d6[6 * i + f] = (f == 3 && enc) ? cens_phi_decode(col[i], bins[i]) : col[i];
+  }
   if (i5)
     for (int64_t i = 0; i < m; i++) {
       i5[5 * i + 0] = (int32_t)(bins[i] & 0xff);
@@ -1023,14 +1036,16 @@ extern "C" int c2d_census_export(c2d_ctx* c, double* d6, int32_t* i5, uint64_t* 
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const DevCensus& d = c->cens[c->cur_out];
   std::vector<double> col(m);
-  for (int f = 0; f < 6; f++) {
-    HIPCHK(c, hipMemcpy(col.data(), d.d[f], m * sizeof(double), hipMemcpyDeviceToHost));
-    if (d6)
-      for (int64_t i = 0; i < m; i++) d6[6 * i + f] = col[i];
-  }
   std::vector<uint32_t> jk(m), bins(m);
   HIPCHK(c, hipMemcpy(jk.data(), d.jk, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIPCHK(c, hipMemcpy(bins.data(), d.bins, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  const bool enc = cens_encoded(c);
+  for (int f = 0; f < 6; f++) {
+    HIPCHK(c, hipMemcpy(col.data(), d.d[f], m * sizeof(double), hipMemcpyDeviceToHost));
+    if (d6)
+      for (int64_t i = 0; i < m; i++)
+        d6[6 * i + f] = (f == 3 && enc) ? cens_phi_decode(col[i], bins[i]) : col[i];
+  }
   if (i5)
     for (int64_t i = 0; i < m; i++) {
       i5[5 * i + 0] = (int32_t)(bins[i] & 0xff);
@@ -1051,8 +1066,12 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const DevCensus& d = c->cens[c->cur_out];
   std::vector<double> col(n);
+  const bool enc = cens_encoded(c);
   for (int f = 0; f < 6; f++) {
-    for (int64_t i = 0; i < n; i++) col[i] = d6[6 * i + f];
+    for (int64_t i = 0; i < n; i++) {
+      col[i] = d6[6 * i + f];
+      if (f == 3 && enc) col[i] = c2d_cos(col[i]);
+    }
     if (n) HIPCHK(c, hipMemcpy(d.d[f], col.data(), n * sizeof(double), hipMemcpyHostToDevice));
   }
   std::vector<uint32_t> jk(n), bins(n);
@@ -1062,6 +1081,10 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
         q[1] < 0 || q[1] > 255 || q[2] < 0 || q[2] > 255)
       return fail(c, C2D_E_ARG, "census record %lld out of range", (long long)i);
     bins[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16);
+    if (enc) {
+      const double ph = d6[6 * i + 3];
+      if (!(ph <= C2D_PI_REF && ph >= 1.0e-10)) bins[i] |= C2D_CENS_ESW;
+    }
     jk[i] = ((uint32_t)q[3] << 16) | (uint32_t)q[4];
   }
   if (n) {

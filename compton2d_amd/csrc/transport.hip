@@ -628,12 +628,24 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
     gst(P.cout.rpre + slot, p.rpre);
     gst(P.cout.zpre + slot, p.zpre);
     gst(P.cout.wmu + slot, p.wmu);
+#if C2D_TABLE_COMTOT
+    gst(P.cout.phi + slot, p.eta);                   /* encoded azimuth (CensusSoA) */
+#else
     gst(P.cout.phi + slot, p.phi);
+#endif
     gst(P.cout.ew + slot, p.ew);
     gst(P.cout.xnu + slot, p.xnu);
     gst(P.cout.jk + slot, ((uint32_t)p.jph << 16) | (uint32_t)p.kph);
-    gst(P.cout.bins + slot, (uint32_t)p.jgpsp | ((uint32_t)p.jgplc << 8) | ((uint32_t)p.jgpmu << 16));
+    gst(P.cout.bins + slot, (uint32_t)p.jgpsp | ((uint32_t)p.jgplc << 8) | ((uint32_t)p.jgpmu << 16)
+#if C2D_TABLE_COMTOT
+                                | (p.esw == -1 ? C2D_CENS_ESW : 0u)
+#endif
+    );
+#ifdef C2D_ABLATE_DERIVE               /* profiling ablation only */
+    gst(P.cout.key + slot, p.key ^ p.ctr ^ ((uint64_t)p.sub << 32));
+#else
     gst(P.cout.key + slot, c2d_derive_s(p.key, C2D_TAG_CENSUS, p.ctr, 0u, p.sub));
+#endif
   } else {
     gor(P.err, ERR_CENSUS);
   }
@@ -678,7 +690,11 @@ __device__ __forceinline__ void load_rec(Pkt& p, const ScatRec& r) {
 __device__ __forceinline__ void cache_energy(const KParams& P, const Geo* g, Pkt& p) {
   p.ie = grid_lookup(g->E_ph, C2D_N_VOL, g->eph_start, g->eph_k0, p.xnu);
 #if C2D_TABLE_COMTOT
+#ifdef C2D_ABLATE_TRIG                 /* profiling ablation only */
+  const double s = (p.xnu * 1e-3 - C2D_COMTAB_U0) * P.comtab_du_inv;
+#else
   const double s = (c2d_log(p.xnu) - C2D_COMTAB_U0) * P.comtab_du_inv;
+#endif
   if (s >= 1.0 && s < (double)(C2D_COMTAB_N - 3)) {
     p.tg = (int32_t)s;
     p.tt = s - (double)p.tg;
@@ -697,7 +713,11 @@ __device__ __forceinline__ void cache_energy(const KParams& P, const Geo* g, Pkt
 __device__ __forceinline__ void set_phi(Pkt& p, double phi) {
   p.phi = phi;
 #if C2D_TABLE_COMTOT
+#ifdef C2D_ABLATE_TRIG
+  p.eta = 1.0 - 0.3 * phi;
+#else
   p.eta = c2d_cos(phi);
+#endif
   p.esw = (phi <= PI_REF && phi >= 1.0e-10) ? 1 : -1;
 #endif
 }
@@ -904,7 +924,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   const bool leaves = (jnew == P.nz + 1 || jnew == 0 || knew == P.nr + 1 || knew == 0);
 #if C2D_TABLE_COMTOT
   p.eta = Eta;
-  if (p.mode != -1 && (ikind != 1 || leaves)) {   /* an event will read phi */
+  if (p.mode != -1 && (ikind == 3 || leaves)) {   /* an event will read phi (census: encoded) */
     p.phi = c2d_acos(Eta);
     if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
   }
@@ -1334,8 +1354,15 @@ __device__ __forceinline__ void load_source(const KParams& P0, Pkt& p, long long
     const int64_t i = item;
     p.rpre = gld(P.cin.rpre + i); p.zpre = gld(P.cin.zpre + i);
     p.wmu = clampd(gld(P.cin.wmu + i), 0.99999999);
-    p.phi = gld(P.cin.phi + i); p.ew = gld(P.cin.ew + i); p.xnu = gld(P.cin.xnu + i);
+    p.ew = gld(P.cin.ew + i); p.xnu = gld(P.cin.xnu + i);
     const uint32_t jk = gld(P.cin.jk + i), bn = gld(P.cin.bins + i);
+#if C2D_TABLE_COMTOT
+    p.eta = gld(P.cin.phi + i);                        /* encoded azimuth (CensusSoA) */
+    p.esw = (bn & C2D_CENS_ESW) ? -1 : 1;
+    p.phi = 0.0;
+#else
+    p.phi = gld(P.cin.phi + i);
+#endif
     p.jph = (int32_t)(jk >> 16); p.kph = (int32_t)(jk & 0xffffu);
     p.jgpsp = (int32_t)(bn & 0xffu); p.jgplc = (int32_t)((bn >> 8) & 0xffu);
     p.jgpmu = (int32_t)((bn >> 16) & 0xffu);
@@ -1345,6 +1372,7 @@ __device__ __forceinline__ void load_source(const KParams& P0, Pkt& p, long long
     p.kap = 0;
   } else {
     load_pk(p, P.pk, item - P.n_cens_items);
+    set_phi(p, p.phi);
   }
 }
 
@@ -1382,7 +1410,6 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
    * launch: it is re-read instead of being held in registers. */
   long long src_item = 0;
 #if C2D_TABLE_COMTOT
-  double s_eta = 1.0;     /* cos(phi) of the source, reused by every copy */
 #endif
   int32_t state = ST_IDLE, probe = 0, nscat = 0;
   ComCache cc = {-1, -1, 0.0, 0.0};
@@ -1444,6 +1471,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
       } else {
         /* a scatter secondary, tracked as imctrk2d(1) (imctrk2d.f:662-679) */
         load_pk(p, cold(P).pk, item);
+        set_phi(p, p.phi);
         rng_sync(p);
         p.mode = 1;
         p.wtmin = 1.0e-10 * p.ew;
@@ -1451,11 +1479,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
       }
       p.nflight = 0;
       cc.cell0 = -1; cc.cell1 = -1;
-      cache_energy(P, T.g, p);
-      set_phi(p, p.phi);
-#if C2D_TABLE_COMTOT
-      s_eta = p.eta;
-#endif
+      cache_energy(P, T.g, p);        /* azimuth: set by load_source / above */
     }
     if (exhausted && __ballot(state != ST_IDLE) == 0ull) break;
     TP_MARK(pf, TP_START);
@@ -1479,11 +1503,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
             const double s_ew = ew0 / P.split1;
             p.ctr = 0;
             p.nflight = 0;
-            /* same xnu and phi: the energy caches, ComCache and cos(phi) stay valid */
-#if C2D_TABLE_COMTOT
-            p.eta = s_eta;
-            p.esw = (p.phi <= PI_REF && p.phi >= 1.0e-10) ? 1 : -1;
-#endif
+            /* same xnu: the energy caches and ComCache stay valid (azimuth: load_source) */
             if (probe < P.split1) {
               p.ew = s_ew;
               p.wtmin = 1.0e-10 * ew0;
@@ -1625,8 +1645,7 @@ __device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bun
     p.ctr = 0;
     b.flags = BF_TRACK | (G > 0 ? BF_SPEC : 0);
   }
-  cache_energy(P, T.g, p);
-  set_phi(p, p.phi);
+  cache_energy(P, T.g, p);          /* azimuth: set by load_source */
 }
 
 /* probe g0 + i collides at dcol inside the shared step: its own partial
@@ -1885,8 +1904,12 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
   const bool leaves = bnd && (jnew == P.nz + 1 || jnew == 0 || knew == P.nr + 1 || knew == 0);
 #if C2D_TABLE_COMTOT
   p.eta = Eta;
-  if ((b.flags & BF_TRACK) && (!bnd || leaves)) {   /* an event will read phi */
+  if ((b.flags & BF_TRACK) && leaves) {   /* an escape event reads phi (census: encoded) */
+    #ifdef C2D_ABLATE_TRIG
+    p.phi = 1.5 - Eta;
+#else
     p.phi = c2d_acos(Eta);
+#endif
     if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
   }
 #else

@@ -65,3 +65,44 @@ def test_restart_from_census_file_matches_oracle(tmp_path, name):
     for e in (a, b):
         e.close()
     o.close()
+
+
+def test_fast_census_azimuth_encoding():
+    """Fast contexts keep the census azimuth encoded (c2d_device.hpp
+    CensusSoA: cos(phi) in the phi column, the quadrant switch in a bins
+    bit).  The exported phi is the decode of the raw device words with the
+    kernel's own acos, bit for bit, and an import re-encodes it as the
+    kernel's set_phi would (cos of the phi it is given)."""
+    import torch
+    gc = GoldenCase("c3_mrk421")
+    a = Engine(gc.grid(comtot_mode=abi.COMTOT_TABLE))
+    a.transport_step(gc.step_inputs(0))
+    d6, i5, keys = a.census()
+    n = len(keys)
+    assert n > 1000
+    raw = torch.zeros(n * abi.CENSUS_REC_WORDS, dtype=torch.int64, device="cuda:0")
+    a.census_pack(0, n, raw.data_ptr())
+    w = raw.view(n, abi.CENSUS_REC_WORDS).cpu().numpy().view(np.uint64)
+    eta = w[:, 3].view(np.float64)
+    bins = (w[:, 6] >> np.uint64(32)).astype(np.uint32)
+    esw = (bins & np.uint32(1 << 24)) != 0
+    assert np.all(np.abs(eta) <= 1.0) and esw.any() and (~esw).any()
+    acos = np.zeros_like(eta)
+    OL.load("det").c2o_unit_math(3, np.ascontiguousarray(eta).ctypes.data_as(abi.PD),
+                                 acos.ctypes.data_as(abi.PD), n)
+    phi = np.where(esw, 2.0 * 3.1415926536 - acos, acos)
+    np.testing.assert_array_equal(d6[:, 3].view(np.uint64), phi.view(np.uint64))
+    np.testing.assert_array_equal(i5[:, 0], (bins & np.uint32(0xff)).astype(np.int32))
+    # import: cos(phi) and the switch, as set_phi forms them
+    b = Engine(gc.grid(comtot_mode=abi.COMTOT_TABLE))
+    b.import_census(d6, i5, keys)
+    raw2 = torch.zeros_like(raw)
+    b.census_pack(0, n, raw2.data_ptr())
+    w2 = raw2.view(n, abi.CENSUS_REC_WORDS).cpu().numpy().view(np.uint64)
+    cosv = np.zeros_like(eta)
+    OL.load("det").c2o_unit_math(2, np.ascontiguousarray(d6[:, 3]).ctypes.data_as(abi.PD),
+                                 cosv.ctypes.data_as(abi.PD), n)
+    np.testing.assert_array_equal(w2[:, 3], cosv.view(np.uint64))
+    np.testing.assert_array_equal(w2[:, 6] >> np.uint64(32), w[:, 6] >> np.uint64(32))
+    a.close()
+    b.close()

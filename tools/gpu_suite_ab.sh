@@ -1,9 +1,9 @@
 #!/bin/bash
-# r02x: absorption-point stream (4 uniforms per Philox block) + series log1p
-# in the fast build: GPU suite, then the C3 bench A/B
+# r02x: GPU suite, then the C3 bench (tools/gpu_tr_ab.sh base)
+
 set -o pipefail
 cd "$(dirname "$0")/.."
-OUT=gpurun_out/r02x
+OUT=gpurun_out/${TAG:-r02x}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests \
     > $OUT/pytest.txt 2>&1
