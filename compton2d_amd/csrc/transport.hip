@@ -1852,8 +1852,13 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
               const double L = (x < 1.0e-4) ? x * (1.0 + x * (0.5 + x * (0.33333333333333333 + x * 0.25)))
                                             : -c2d_log_pos(1.0 - x);
               const double sstar = L * isig;
-              const double denom = __builtin_sqrt(B + sstar * (2.0 * A + sstar));
-              sum_prdep += deleabs * ((A + sstar) / denom) * C_LIGHT;
+              /* 1/sqrt(d) from v_rsq_f64 and two Newton steps (f64 accurate) */
+              const double d = B + sstar * (2.0 * A + sstar);
+              const double h = 0.5 * d;
+              double y = __builtin_amdgcn_rsq(d);
+              y = y * __builtin_fma(-h, y * y, 1.5);
+              y = y * __builtin_fma(-h, y * y, 1.5);
+              sum_prdep += deleabs * ((A + sstar) * y) * C_LIGHT;
 #else
               const double sstar = -c2d_log_pos(1.0 - x) / sigabs;
               const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
