@@ -1799,7 +1799,10 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
   const double ex = (xabs < 100.0) ? c2d_exp(-xabs) : 0.0;
   const bool two = xabs > 0.00001;      /* the absorption point is sampled */
   TP_MARK(pf, TP_GEOM);
-  /* ---- probes (mode -1) ---- */
+  /* ---- probes (mode -1): collisions and weights; their absorption-point
+   * deposits are deferred to the end of the step (below) ---- */
+  int nabs = 0;                 /* survivors that deposit over the whole step */
+  double dabs = 0.0, qabs = 0.0;
   if (b.alive) {
     int n = __popc(b.alive);
     lc.steps += (uint32_t)n;
@@ -1826,52 +1829,9 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
       const double ewnew = (xabs < 100.0) ? b.ewp * ex : 0.0;
       double deleabs = b.ewp - ewnew;
       if (deleabs < 1.0e-50) deleabs = 1.0e-50;
-      double sum_prdep = 0.0;
-#ifdef C2D_ABLATE_PROBE_ABS            /* profiling ablation only (tools/build_sweep.sh) */
-      if (two && n < 0) {
-#else
-      if (two) {
-#endif
-        /* the survivors' absorption points: four 32-bit uniforms per block of
-         * the bundle's point stream, a fresh block per shared step */
-        const double q = deleabs / b.ewp;
-        const uint32_t sub = C2D_SUB_ABSPT | (uint32_t)b.g0;
-#if C2D_TABLE_COMTOT
-        const double isig = 1.0 / sigabs;
-        const double A = wmu * rpre, B = rpre * rpre;
-#endif
-        for (int t = 0; t < n; t += 4) {
-          uint32_t w[4];
-          c2d_block4(p.key, sub, b.actr++, w);
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            if (t + j < n) {
-              const double x = c2d_u01_32(w[j]) * q;
-#if C2D_TABLE_COMTOT
-              /* -log(1-x): series below 1e-4 (truncation < x^4/5 relative) */
-              const double L = (x < 1.0e-4) ? x * (1.0 + x * (0.5 + x * (0.33333333333333333 + x * 0.25)))
-                                            : -c2d_log_pos(1.0 - x);
-              const double sstar = L * isig;
-              /* 1/sqrt(d) from v_rsq_f64 and two Newton steps (f64 accurate) */
-              const double d = B + sstar * (2.0 * A + sstar);
-              const double h = 0.5 * d;
-              double y = __builtin_amdgcn_rsq(d);
-              y = y * __builtin_fma(-h, y * y, 1.5);
-              y = y * __builtin_fma(-h, y * y, 1.5);
-              sum_prdep += deleabs * ((A + sstar) * y) * C_LIGHT;
-#else
-              const double sstar = -c2d_log_pos(1.0 - x) / sigabs;
-              const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
-              sum_prdep += deleabs * ((wmu * rpre + sstar) / denom) * C_LIGHT;
-#endif
-            }
-          }
-        }
-      } else {
-        sum_prdep = (double)n * (deleabs * wmu * C_LIGHT);
-      }
-      cell_add(P, T, TC_EDEP, cell, (double)n * deleabs);
-      cell_add(P, T, TC_PRDEP, cell, sum_prdep);
+      nabs = n;
+      dabs = deleabs;
+      qabs = deleabs / b.ewp;
       if (ewnew <= b.wtminp) {
         atomicAdd(&c2d_cnt_lds[C2D_CNT_KILLED], (uint32_t)n);
         b.alive = 0;
@@ -1890,61 +1850,115 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
     if (ewnew <= p.wtmin) b.flags = (b.flags & ~BF_TRACK) | BF_TKILL;
     else p.ew = ewnew;
   }
-  if (!b.alive && !(b.flags & BF_TRACK)) return;
-  /* ---- the shared move ---- */
-  double rnew, znew;
-  if (bnd) {
-    rnew = rbnd;
-    znew = Zbnd;
-  } else {
-    jnew = p.jph;
-    knew = p.kph;
-    const double f = trld * swmu;
-    rnew = __builtin_sqrt(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
-    znew = zpre + trld * wmu;
-  }
-  p.dcen = p.dcen - trld;
-  Eta = (trld + Eta * rpre) / rnew;          /* hazard H1: trld, not f (imctrk2d.f:472) */
-  Eta = clampd(Eta, lim9);
-  const bool leaves = bnd && (jnew == P.nz + 1 || jnew == 0 || knew == P.nr + 1 || knew == 0);
-#if C2D_TABLE_COMTOT
-  p.eta = Eta;
-  if ((b.flags & BF_TRACK) && leaves) {   /* an escape event reads phi (census: encoded) */
-    #ifdef C2D_ABLATE_TRIG
-    p.phi = 1.5 - Eta;
-#else
-    p.phi = c2d_acos(Eta);
-#endif
-    if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
-  }
-#else
-  p.phi = c2d_acos(Eta);
-  if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
-#endif
-  p.rpre = rnew;
-  p.zpre = znew;
-  if (bnd) {
-    if (leaves) {
-      b.alive = 0;                            /* probes leaving end (no tally) */
-      p.jph = jnew;
-      p.kph = knew;
-      if (b.flags & BF_TRACK) {
-        TP_COUNT(pf, TP_LEAK_W, TP_LEAK_L);
-        if (imcleak(P, T, p, lc) == 1) b.flags &= ~BF_TRACK;
-        else set_phi(p, p.phi);               /* axis pass-through set phi = 1e-6 */
-      }
-      return;
+  /* ---- the shared move and the recombined copy's event.  Census records
+   * and escape events are stored here, before the survivors' point loop:
+   * stores and the n_field atomic count in vmcnt with the loads, so the
+   * VALU-only loop below lets them drain before the next load is waited
+   * for. ---- */
+  if (b.alive || (b.flags & BF_TRACK)) {
+    double rnew, znew;
+    if (bnd) {
+      rnew = rbnd;
+      znew = Zbnd;
+    } else {
+      jnew = p.jph;
+      knew = p.kph;
+      const double f = trld * swmu;
+      rnew = __builtin_sqrt(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
+      znew = zpre + trld * wmu;
     }
-    p.kph = knew;
-    p.jph = jnew;
-    return;
+    p.dcen = p.dcen - trld;
+    double Etan = (trld + Eta * rpre) / rnew;   /* hazard H1: trld, not f (imctrk2d.f:472) */
+    Etan = clampd(Etan, lim9);
+    const bool leaves = bnd && (jnew == P.nz + 1 || jnew == 0 || knew == P.nr + 1 || knew == 0);
+#if C2D_TABLE_COMTOT
+    p.eta = Etan;
+    if ((b.flags & BF_TRACK) && leaves) {   /* an escape event reads phi (census: encoded) */
+#ifdef C2D_ABLATE_TRIG
+      p.phi = 1.5 - Etan;
+#else
+      p.phi = c2d_acos(Etan);
+#endif
+      if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
+    }
+#else
+    p.phi = c2d_acos(Etan);
+    if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
+#endif
+    p.rpre = rnew;
+    p.zpre = znew;
+    if (bnd) {
+      if (leaves) {
+        b.alive = 0;                            /* probes leaving end (no tally) */
+        p.jph = jnew;
+        p.kph = knew;
+        if (b.flags & BF_TRACK) {
+          TP_COUNT(pf, TP_LEAK_W, TP_LEAK_L);
+          if (imcleak(P, T, p, lc) == 1) b.flags &= ~BF_TRACK;
+          else set_phi(p, p.phi);               /* axis pass-through set phi = 1e-6 */
+        }
+      } else {
+        p.kph = knew;
+        p.jph = jnew;
+      }
+    } else {
+      /* census (imctrk2d.f:528-578): probes end, the recombined copy is written */
+      b.alive = 0;
+      if (b.flags & BF_TRACK) {
+        TP_COUNT(pf, TP_CENS_W, TP_CENS_L);
+        census_write(P, T, p, lc, cch);
+        b.flags &= ~BF_TRACK;
+      }
+    }
   }
-  /* census (imctrk2d.f:528-578): probes end, the recombined copy is written */
-  b.alive = 0;
-  if (b.flags & BF_TRACK) {
-    TP_COUNT(pf, TP_CENS_W, TP_CENS_L);
-    census_write(P, T, p, lc, cch);
-    b.flags &= ~BF_TRACK;
+  /* ---- the survivors' absorption points and deposits (imctrk2d.f:382-462),
+   * at the step's starting point ---- */
+  if (nabs > 0) {
+    double sum_prdep = 0.0;
+#ifdef C2D_ABLATE_PROBE_ABS            /* profiling ablation only (tools/build_sweep.sh) */
+    if (two && nabs < 0) {
+#else
+    if (two) {
+#endif
+      /* four 32-bit uniforms per block of the bundle's point stream, a fresh
+       * block per shared step */
+      const uint32_t sub = C2D_SUB_ABSPT | (uint32_t)b.g0;
+#if C2D_TABLE_COMTOT
+      const double isig = 1.0 / sigabs;
+      const double Aw = wmu * rpre, Bw = rpre * rpre;
+#endif
+      for (int t = 0; t < nabs; t += 4) {
+        uint32_t w[4];
+        c2d_block4(p.key, sub, b.actr++, w);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if (t + j < nabs) {
+            const double x = c2d_u01_32(w[j]) * qabs;
+#if C2D_TABLE_COMTOT
+            /* -log(1-x): series below 1e-4 (truncation < x^4/5 relative) */
+            const double L = (x < 1.0e-4) ? x * (1.0 + x * (0.5 + x * (0.33333333333333333 + x * 0.25)))
+                                          : -c2d_log_pos(1.0 - x);
+            const double sstar = L * isig;
+            /* 1/sqrt(d) from v_rsq_f64 and two Newton steps (f64 accurate) */
+            const double d = Bw + sstar * (2.0 * Aw + sstar);
+            const double h = 0.5 * d;
+            double y = __builtin_amdgcn_rsq(d);
+            y = y * __builtin_fma(-h, y * y, 1.5);
+            y = y * __builtin_fma(-h, y * y, 1.5);
+            sum_prdep += dabs * ((Aw + sstar) * y) * C_LIGHT;
+#else
+            const double sstar = -c2d_log_pos(1.0 - x) / sigabs;
+            const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
+            sum_prdep += dabs * ((wmu * rpre + sstar) / denom) * C_LIGHT;
+#endif
+          }
+        }
+      }
+    } else {
+      sum_prdep = (double)nabs * (dabs * wmu * C_LIGHT);
+    }
+    cell_add(P, T, TC_EDEP, cell, (double)nabs * dabs);
+    cell_add(P, T, TC_PRDEP, cell, sum_prdep);
   }
 }
 
