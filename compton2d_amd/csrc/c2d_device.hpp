@@ -174,6 +174,7 @@ struct KParams {
   /* census */
   CensusSoA cin, cout;
   int64_t n_cin, cap_cout;
+  uint32_t cens_chunk;       /* census slots per wave reservation (bundle kernel) */
   unsigned long long* n_cout;
   /* events */
   double* ev;

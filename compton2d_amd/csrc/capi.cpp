@@ -661,6 +661,15 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.cout = c->cens[out_buf].soa();
   P.n_cin = c->n_census;
   P.cap_cout = cfg.census_capacity;
+  {
+    /* census chunk per wave reservation: <= 1024 slots, and the chunk tails
+     * (at most one per wave) at most 1/8 of the capacity; >= 64 so one
+     * reservation always covers a wave's census lanes */
+    const int64_t waves = (int64_t)std::max(c->bundle_grid, 1) * (C2D_TR_BLOCK / 64);
+    int64_t ch = 1024;
+    while (ch > 64 && ch * waves * 8 > cfg.census_capacity) ch >>= 1;
+    P.cens_chunk = (uint32_t)ch;
+  }
   P.n_cout = c->ctl + CTL_NCOUT;
   P.ev = c->ev; P.cap_ev = cfg.event_capacity;
   P.n_ev_sh = c->ctl + CTL_EVSH;
@@ -806,6 +815,14 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   /* close the holes the bundle kernel's census chunks left (census stays dense) */
   int64_t cens_dense = -1;
   if (c->bundle && c->cens_holes) {
+    /* a census write beyond the capacity: fail before the compaction reads
+     * records from reserved slots past the end of the buffer */
+    int32_t herr0 = 0;
+    HIPCHK(c, hipMemcpyAsync(&herr0, c->derr, sizeof herr0, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (herr0 & ERR_CENSUS)
+      return fail(c, C2D_E_CENSUS_OVERFLOW, "census overflow (capacity %lld)",
+                  (long long)cfg.census_capacity);
     unsigned long long reserved = 0;
     HIPCHK(c, hipMemcpyAsync(&reserved, c->ctl + CTL_NCOUT, sizeof reserved, hipMemcpyDeviceToHost,
                              c->stream));

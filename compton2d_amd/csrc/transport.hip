@@ -76,7 +76,12 @@ constexpr double EMASSKEV = 5.11e2;
 constexpr double SIGTHOM = 6.6516e-25;
 constexpr int BLOCK = C2D_TR_BLOCK;   /* transport and bundle kernels */
 constexpr int SBLOCK = 256;       /* source / scatter kernels */
-constexpr long long CHUNK = 64;
+/* generation-0 items a wave takes per fetch (one returning atomic on a work
+ * shard counter: 64 -> 256 -> 1024 items, +6 %, +2 %) */
+#ifndef C2D_WORK_CHUNK
+#define C2D_WORK_CHUNK 1024
+#endif
+constexpr long long CHUNK = C2D_WORK_CHUNK;
 
 /* Fortran REAL literals promoted to double (src/imcvol2d_para.f:204,221,247,268,336) */
 #define F32(x) ((double)(float)(x))
@@ -568,12 +573,12 @@ C2D_COLD_FN int imcleak(const KParams& P0, const Tal& T, Pkt& p, LaneCnt& lc) {
 }
 
 /* Census slots of the bundle kernel come from wave-private chunks of
- * CENS_CHUNK slots, reserved with one atomic on the census counter (a single
+ * P.cens_chunk slots (host: up to 1024, and at most 1/8 of the capacity over
+ * all waves: 256 -> 1024 slots was +1 %), reserved with one atomic on the census counter (a single
  * address every wave appends to: per-write reservations were the kernel's
  * limiter).  A wave's last chunk leaves a hole [used, CENS_CHUNK), recorded
  * in P.cens_holes and closed after the step by moving records from the end
  * of the census (c2d_census_move), so the census stays dense. */
-constexpr uint32_t CENS_CHUNK = 256;
 /* per wave of the workgroup, in LDS (updated by the lanes that write) */
 __shared__ unsigned long long c2d_cch_base[16];
 __shared__ uint32_t c2d_cch_used[16];
@@ -590,6 +595,7 @@ __device__ __forceinline__ unsigned long long census_slot_chunk(const KParams& P
   const uint32_t rank = (uint32_t)__popcll(lt), k = (uint32_t)__popcll(mask);
   const unsigned long long base = c2d_cch_base[w];
   const uint32_t used = c2d_cch_used[w];
+  const uint32_t CENS_CHUNK = P.cens_chunk;
   const uint32_t rem = CENS_CHUNK - used;
   if (k <= rem) {
     if (lane == leader) c2d_cch_used[w] = used + k;
@@ -2002,6 +2008,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
   pf.t = clock64();
 #endif
   CensChunk cch = {0};
+  const uint32_t CENS_CHUNK = cold(P).cens_chunk;
   if (lane == 0) { c2d_cch_base[tid >> 6] = 0ull; c2d_cch_used[tid >> 6] = CENS_CHUNK; }
 
   for (;;) {
@@ -2119,7 +2126,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
 
 #if C2D_TABLE_COMTOT
 /* close the census holes: move n records src -> dst per workgroup (one move
- * each, n <= CENS_CHUNK); moves never overlap */
+ * each, n <= P.cens_chunk); moves never overlap */
 __global__ void __launch_bounds__(256) c2d_census_move(CensusSoA c, const long long* mv) {
   const long long src = mv[3 * blockIdx.x], dst = mv[3 * blockIdx.x + 1], n = mv[3 * blockIdx.x + 2];
   for (long long i = threadIdx.x; i < n; i += 256) {
