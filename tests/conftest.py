@@ -10,3 +10,15 @@ for p in (str(ROOT), str(ROOT / "tests")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
     config.addinivalue_line("markers", "slow: long CPU test")
+
+
+def pytest_collection_modifyitems(config, items):
+    # GPU runs: bring up torch's HIP runtime before any test opens a context
+    # through the C-ABI library (a test that needs torch device memory after
+    # the library initialised HIP in-process otherwise sees no device)
+    if any(it.get_closest_marker("gpu") for it in items) and config.getoption("-m") != "not gpu":
+        try:
+            import torch
+            torch.cuda.is_available()
+        except Exception:
+            pass

@@ -106,3 +106,22 @@ def test_fast_census_azimuth_encoding():
     np.testing.assert_array_equal(w2[:, 6] >> np.uint64(32), w[:, 6] >> np.uint64(32))
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("mode", [abi.COMTOT_EXACT, abi.COMTOT_TABLE])
+def test_census_overflow_is_reported(mode):
+    """A step whose census does not fit fails with C2D_E_CENSUS_OVERFLOW (the
+    reference's `stop 'too many photons'`, src/imctrk2d.f:573-577) instead of
+    writing past the buffer."""
+    from compton2d_amd.engine import C2DError
+    gc = GoldenCase("ssc_tau")
+    full = Engine(gc.grid(comtot_mode=mode))
+    full.transport_step(gc.step_inputs(0))
+    need = full.census_count()
+    full.close()
+    assert need > 200
+    small = Engine(gc.grid(comtot_mode=mode, census_capacity=need // 4))
+    with pytest.raises(C2DError) as e:
+        small.transport_step(gc.step_inputs(0))
+    assert e.value.code == -3, str(e.value)
+    small.close()
