@@ -82,6 +82,11 @@ constexpr int SBLOCK = 256;       /* source / scatter kernels */
 #define C2D_WORK_CHUNK 1024
 #endif
 constexpr long long CHUNK = C2D_WORK_CHUNK;
+/* fast build: -log(1-x) of the survivors' absorption points by its series
+ * below 1e-2 (0: always the log, -3 %) */
+#ifndef C2D_PT_SERIES
+#define C2D_PT_SERIES 1
+#endif
 
 /* Fortran REAL literals promoted to double (src/imcvol2d_para.f:204,221,247,268,336) */
 #define F32(x) ((double)(float)(x))
@@ -1941,9 +1946,17 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
           if (t + j < nabs) {
             const double x = c2d_u01_32(w[j]) * qabs;
 #if C2D_TABLE_COMTOT
-            /* -log(1-x): series below 1e-4 (truncation < x^4/5 relative) */
-            const double L = (x < 1.0e-4) ? x * (1.0 + x * (0.5 + x * (0.33333333333333333 + x * 0.25)))
-                                          : -c2d_log_pos(1.0 - x);
+#if C2D_PT_SERIES
+            /* -log(1-x): series below 1e-2 (8 terms, truncation < x^8/9 relative;
+             * 1e-4 with 4 terms -3 %, 0.05 with 12 terms or 2 atanh(x/(2-x))
+             * below 0.2: no better, r02ap-aq) */
+            const double L = (x < 1.0e-2)
+                ? x * (1.0 + x * (0.5 + x * (0.33333333333333333 + x * (0.25 + x * (0.2 + x * (
+                      0.16666666666666667 + x * (0.14285714285714286 + x * 0.125)))))))
+                : -c2d_log_pos(1.0 - x);
+#else
+            const double L = -c2d_log_pos(1.0 - x);
+#endif
             const double sstar = L * isig;
             /* 1/sqrt(d) from v_rsq_f64 and two Newton steps (f64 accurate) */
             const double d = Bw + sstar * (2.0 * Aw + sstar);
