@@ -102,7 +102,9 @@ struct Pkt {
   int32_t tg;         /* comtot table index (0: outside the table, exact sum)     */
   int32_t esw;        /* Eta_switch (quadrant of phi), constant between events    */
 #endif
-  int32_t jph, kph, jgpsp, jgplc, jgpmu, mode, kap;
+  int32_t jph, kph, mode;
+  uint32_t bins;      /* jgpsp | jgplc << 8 | jgpmu << 16 | kap << 24 (PktSoA layout): the
+                         spectral bins (imcleak2d.f) and the kappa phase (H3) in one register */
   int32_t ie;         /* E_ph bin of xnu (imctrk2d.f:382-384), cached per xnu     */
   double rnext;       /* draw ctr of `key` when ctr is odd (second half of a block) */
   uint64_t key;
@@ -110,6 +112,17 @@ struct Pkt {
   uint32_t ctr;
   uint32_t nflight;   /* safety cap: a history that stops progressing is aborted */
 };
+
+__device__ __forceinline__ int32_t JGPSP(const Pkt& p) { return (int32_t)(p.bins & 0xffu); }
+__device__ __forceinline__ int32_t JGPLC(const Pkt& p) { return (int32_t)((p.bins >> 8) & 0xffu); }
+__device__ __forceinline__ int32_t JGPMU(const Pkt& p) { return (int32_t)((p.bins >> 16) & 0xffu); }
+__device__ __forceinline__ int32_t KAP(const Pkt& p) { return (int32_t)(p.bins >> 24); }
+__device__ __forceinline__ uint32_t pack_bins(int32_t sp, int32_t lc, int32_t mu, int32_t kap) {
+  return (uint32_t)sp | ((uint32_t)lc << 8) | ((uint32_t)mu << 16) | ((uint32_t)kap << 24);
+}
+__device__ __forceinline__ void set_bins(Pkt& p, int32_t sp, int32_t lc, int32_t mu) {
+  p.bins = pack_bins(sp, lc, mu, KAP(p));
+}
 
 /* Safety caps (never reached by a valid history; they keep a malformed input
  * from hanging the GPU).  Hitting one counts C2D_CNT_ABORTED. */
@@ -501,9 +514,8 @@ __device__ __forceinline__ int compb2d(const KParams& P, const Geo* g, double* n
                           lim);
   double dphi = c2d_acos(cosdphi);
   double phis = p.phi + dphi;
-  p.jgpsp = bin_sp(g, P.nphtotal, xnus, 1.000001, 0.999999, 0);
-  p.jgplc = bin_lc(g, P.nph_lc, xnus);
-  p.jgpmu = bin_mu(g, P.nmu, wmus);
+  set_bins(p, bin_sp(g, P.nphtotal, xnus, 1.000001, 0.999999, 0), bin_lc(g, P.nph_lc, xnus),
+           bin_mu(g, P.nmu, wmus));
   p.ew = p.ew * xnus / p.xnu;
   p.xnu = xnus;
   p.wmu = wmus;
@@ -530,9 +542,10 @@ __device__ __forceinline__ void push_event(const KParams& P0, double tb, const P
 
 __device__ __forceinline__ void escape_tally(const KParams& P0, const Tal& T, const Pkt& p) {
   const KParams& P = cold(P0);
-  if (p.jgplc > 0) atomicAdd(&T_EDOUT(P, T)[(p.jgpmu - 1) * C2D_NPHLCMAX + (p.jgplc - 1)], p.ew / P.dt);
-  if (p.jgpsp > 0 && P.spec_switch == 0)
-    atomicAdd(&T_FOUT(P, T)[(p.jgpmu - 1) * C2D_NPHOMAX + (p.jgpsp - 1)], p.ew);
+  const int32_t jgpsp = JGPSP(p), jgplc = JGPLC(p), jgpmu = JGPMU(p);
+  if (jgplc > 0) atomicAdd(&T_EDOUT(P, T)[(jgpmu - 1) * C2D_NPHLCMAX + (jgplc - 1)], p.ew / P.dt);
+  if (jgpsp > 0 && P.spec_switch == 0)
+    atomicAdd(&T_FOUT(P, T)[(jgpmu - 1) * C2D_NPHOMAX + (jgpsp - 1)], p.ew);
 }
 
 /* returns idead: 1 = left the system, 0 = continue (axis pass-through) */
@@ -647,7 +660,7 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
     gst(P.cout.ew + slot, p.ew);
     gst(P.cout.xnu + slot, p.xnu);
     gst(P.cout.jk + slot, ((uint32_t)p.jph << 16) | (uint32_t)p.kph);
-    gst(P.cout.bins + slot, (uint32_t)p.jgpsp | ((uint32_t)p.jgplc << 8) | ((uint32_t)p.jgpmu << 16)
+    gst(P.cout.bins + slot, (p.bins & 0x00ffffffu)
 #if C2D_TABLE_COMTOT
                                 | (p.esw == -1 ? C2D_CENS_ESW : 0u)
 #endif
@@ -680,7 +693,7 @@ __device__ __forceinline__ ScatRec make_rec(const Pkt& p, uint64_t key, uint32_t
   r.jk = ((uint32_t)p.jph << 16) | (uint32_t)p.kph;
   r.ctr = ctr;
   r.key = key;
-  r.kap = (uint32_t)p.kap;
+  r.kap = (uint32_t)KAP(p);
   r.sub = p.sub;
   return r;
 }
@@ -690,7 +703,7 @@ __device__ __forceinline__ void load_rec(Pkt& p, const ScatRec& r) {
   p.dcen = r.dcen;
   p.jph = (int32_t)(r.jk >> 16);
   p.kph = (int32_t)(r.jk & 0xffffu);
-  p.kap = (int32_t)r.kap;
+  p.bins = (p.bins & 0x00ffffffu) | (r.kap << 24);
 }
 
 /* ------------------------------------------------------------------ */
@@ -785,7 +798,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   const double* tb_e = P.comtab + (int64_t)cell_e * C2D_COMTAB_N + (p.tg > 0 ? p.tg - 1 : 0);
   const double ey0 = gld(tb_e), ey1 = gld(tb_e + 1), ey2 = gld(tb_e + 2), ey3 = gld(tb_e + 3);
   const double ene = gld(P.n_e + cell_e);
-  const double ekap = gld((p.kap ? P.kappa_s : P.kappa_cv) + (int64_t)cell_e * C2D_N_VOL + (p.ie - 1));
+  const double ekap = gld((KAP(p) ? P.kappa_s : P.kappa_cv) + (int64_t)cell_e * C2D_N_VOL + (p.ie - 1));
 #endif
   /* mode 0 uses mb_ran = 1e-10 (imctrk2d.f:150) but never reads colmfp (dcol below) */
   double colmfp = 0.0;
@@ -895,7 +908,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
 #if C2D_TABLE_COMTOT && C2D_EARLY_LOADS
   double sigabs = 1.0e-40 + 1.0 * ekap;
 #else
-  const double* kap = p.kap ? P.kappa_s : P.kappa_cv;
+  const double* kap = KAP(p) ? P.kappa_s : P.kappa_cv;
   double sigabs = 1.0e-40 + 1.0 * gld(kap + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
 #endif
   if (sigabs < 1.0e-40) sigabs = 1.0e-40;
@@ -997,9 +1010,8 @@ __device__ __forceinline__ void planck(const KParams& P, const Geo* G, Pkt& p, d
     ap1 = ap1 + (ap3 * ap3) * (ap3 * ap3);
   }
   p.xnu = ap0 * ap3 * tpl;
-  p.jgpsp = bin_sp(G, P.nphtotal, p.xnu, F32(1.000001), F32(0.999999), 0);
-  p.jgplc = bin_lc(G, P.nph_lc, p.xnu);
-  p.jgpmu = bin_mu(G, P.nmu, p.wmu);
+  set_bins(p, bin_sp(G, P.nphtotal, p.xnu, F32(1.000001), F32(0.999999), 0), bin_lc(G, P.nph_lc, p.xnu),
+           bin_mu(G, P.nmu, p.wmu));
 }
 
 /* file_sample (src/imcsurf2d_para.f:694-788) */
@@ -1007,7 +1019,7 @@ __device__ __forceinline__ void file_sample(const KParams& P, const Geo* G, Pkt&
   if (spec < 0 || spec >= P.n_spectra) {
     gor(P.err, ERR_SPEC);
     p.xnu = 1.0;
-    p.jgpsp = 0; p.jgplc = 0; p.jgpmu = bin_mu(G, P.nmu, p.wmu);
+    set_bins(p, 0, 0, bin_mu(G, P.nmu, p.wmu));
     return;
   }
   const SpecDev sp = P.spectra[spec];
@@ -1019,9 +1031,8 @@ __device__ __forceinline__ void file_sample(const KParams& P, const Geo* G, Pkt&
   double x2 = U(p);
   double Ei = sp.E_file[i - 1], a1 = sp.a1[i - 1], Ii = sp.I_file[i - 1], Fi = sp.F_file[i - 1];
   p.xnu = Ei * c2d_pow(a1 * Ii * x2 / (Fi * Ei) + 1.0, 1.0 / a1);
-  p.jgpsp = bin_sp(G, P.nphtotal, p.xnu, 1.000001, 0.999999, 0);
-  p.jgplc = bin_lc(G, P.nph_lc, p.xnu);
-  p.jgpmu = bin_mu(G, P.nmu, p.wmu);
+  set_bins(p, bin_sp(G, P.nphtotal, p.xnu, 1.000001, 0.999999, 0), bin_lc(G, P.nph_lc, p.xnu),
+           bin_mu(G, P.nmu, p.wmu));
 }
 
 /* one volume packet of vol_calc (src/imcvol2d_para.f:157-392) */
@@ -1098,9 +1109,8 @@ __device__ __forceinline__ void vol_source(const KParams& P, const Geo* g, Pkt& 
     psi = U(p);
     p.rpre = __builtin_sqrt(rlow * rlow + psi * (g->r[kv] * g->r[kv] - rlow * rlow));
   }
-  p.jgpsp = bin_sp(g, P.nphtotal, p.xnu, F32(1.000001), F32(0.999999), P.nphtotal);
-  p.jgplc = bin_lc(g, P.nph_lc, p.xnu);
-  p.jgpmu = bin_mu(g, P.nmu, p.wmu);
+  set_bins(p, bin_sp(g, P.nphtotal, p.xnu, F32(1.000001), F32(0.999999), P.nphtotal),
+           bin_lc(g, P.nph_lc, p.xnu), bin_mu(g, P.nmu, p.wmu));
 }
 
 /* surface packets: z_surf_calc / r_surf_calc (src/imcsurf2d_para.f:254-528).
@@ -1214,8 +1224,7 @@ __device__ __forceinline__ void store_pk(const PktSoA& s, int64_t i, const Pkt& 
   s.rpre[i] = p.rpre; s.zpre[i] = p.zpre; s.wmu[i] = p.wmu; s.phi[i] = p.phi;
   s.ew[i] = p.ew; s.xnu[i] = p.xnu; s.dcen[i] = p.dcen;
   s.jk[i] = ((uint32_t)p.jph << 16) | (uint32_t)p.kph;
-  s.bins[i] = (uint32_t)p.jgpsp | ((uint32_t)p.jgplc << 8) | ((uint32_t)p.jgpmu << 16) |
-              ((uint32_t)p.kap << 24);
+  s.bins[i] = p.bins;
   s.ctr[i] = p.ctr;
   s.key[i] = p.key;
 }
@@ -1225,8 +1234,7 @@ __device__ __forceinline__ void load_pk(Pkt& p, const PktSoA& s, int64_t i) {
   p.ew = gld(s.ew + i); p.xnu = gld(s.xnu + i); p.dcen = gld(s.dcen + i);
   const uint32_t jk = gld(s.jk + i), bn = gld(s.bins + i);
   p.jph = (int32_t)(jk >> 16); p.kph = (int32_t)(jk & 0xffffu);
-  p.jgpsp = (int32_t)(bn & 0xffu); p.jgplc = (int32_t)((bn >> 8) & 0xffu);
-  p.jgpmu = (int32_t)((bn >> 16) & 0xffu); p.kap = (int32_t)(bn >> 24);
+  p.bins = bn;
   p.ctr = gld(s.ctr + i);
   p.key = gld(s.key + i);
   p.sub = 0;
@@ -1258,7 +1266,7 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_source_kernel)(const KPara
       const int cell = upper_index(P.vol_prefix, P.ncell, gidx);
       const int64_t nn = gidx - P.vol_prefix[cell];
       p.key = c2d_derive(P.step_key, C2D_TAG_VOL, (uint32_t)nn, (uint32_t)cell);
-      p.kap = 0;
+      p.bins = 0u;                       /* kap 0: census/volume phase */
       vol_source(P, g, p, cell / P.nr + 1, cell % P.nr + 1);
     } else {
       const int64_t gidx = (it - P.n_vol_items) * P.world + P.rank;
@@ -1269,7 +1277,7 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_source_kernel)(const KPara
       else { side = 2 + ((slot - 2 * P.nz) & 1); s1 = (slot - 2 * P.nz) / 2 + 1; }
       p.key = c2d_derive(P.step_key, C2D_TAG_SURF + (uint32_t)side, (uint32_t)nn,
                          (uint32_t)(s1 - 1));
-      p.kap = 1;
+      p.bins = 1u << 24;                 /* kap 1: surface phase */
       surf_source(P, g, p, side, s1, slot);
     }
     p.ctr = 0;   /* a source's own draws are done: its copies use sub-streams */
@@ -1375,12 +1383,10 @@ __device__ __forceinline__ void load_source(const KParams& P0, Pkt& p, long long
     p.phi = gld(P.cin.phi + i);
 #endif
     p.jph = (int32_t)(jk >> 16); p.kph = (int32_t)(jk & 0xffffu);
-    p.jgpsp = (int32_t)(bn & 0xffu); p.jgplc = (int32_t)((bn >> 8) & 0xffu);
-    p.jgpmu = (int32_t)((bn >> 16) & 0xffu);
+    p.bins = bn & 0x00ffffffu;                     /* kap = 0 (census phase, H3) */
     p.key = gld(P.cin.key + i);
     p.sub = 0;
     p.dcen = P.cdt;                                    /* imcfield2d.f:117 */
-    p.kap = 0;
   } else {
     load_pk(p, P.pk, item - P.n_cens_items);
     set_phi(p, p.phi);
@@ -1415,7 +1421,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
   const long long n_items = A.gen == 0 ? (long long)A.n_items : (long long)rfl64(*A.n_pk);
 
   Pkt p;
-  p.mode = 0; p.kap = 0; p.ctr = 0; p.key = 0; p.sub = 0; p.nflight = 0;
+  p.mode = 0; p.bins = 0u; p.ctr = 0; p.key = 0; p.sub = 0; p.nflight = 0;
   /* The split1 loop (imctrk2d.f:106-123) restarts every copy from the source
    * record, which stays in memory (census store / packet store) for the whole
    * launch: it is re-read instead of being held in registers. */
@@ -1702,7 +1708,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
   r.jk = ((uint32_t)p.jph << 16) | (uint32_t)p.kph;
   r.ctr = b.bctr;
   r.key = p.key;
-  r.kap = (uint32_t)p.kap;
+  r.kap = (uint32_t)KAP(p);
   r.sub = 1u + (uint32_t)(b.g0 + i);
   push_scat(P, A.q2_out, A.n2_out, r);
   b.nscat++;
@@ -1800,9 +1806,9 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
   const bool bnd = trldb < p.dcen;
   const double trld = bnd ? trldb : p.dcen;
 #if C2D_TABLE_COMTOT && C2D_EARLY_LOADS
-  double sigabs = 1.0e-40 + 1.0 * gld((p.kap ? P.kappa_s : P.kappa_cv) + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
+  double sigabs = 1.0e-40 + 1.0 * gld((KAP(p) ? P.kappa_s : P.kappa_cv) + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
 #else
-  const double* kap = p.kap ? P.kappa_s : P.kappa_cv;
+  const double* kap = KAP(p) ? P.kappa_s : P.kappa_cv;
   double sigabs = 1.0e-40 + 1.0 * gld(kap + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
 #endif
   if (sigabs < 1.0e-40) sigabs = 1.0e-40;
@@ -2005,7 +2011,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
   const long long n_items = (long long)A.n_items;
 
   Bundle b;
-  b.p.mode = 0; b.p.kap = 0; b.p.ctr = 0; b.p.key = 0; b.p.sub = 0; b.p.nflight = 0;
+  b.p.mode = 0; b.p.bins = 0u; b.p.ctr = 0; b.p.key = 0; b.p.sub = 0; b.p.nflight = 0;
   b.alive = 0; b.flags = 0; b.src = 0; b.g0 = 0; b.nscat = 0; b.bctr = 0; b.tsteps = 0;
   b.tau = 0.0; b.brnext = 0.0; b.ewp = 0.0; b.wtminp = 0.0;
   bool busy = false;
