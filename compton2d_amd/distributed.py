@@ -14,9 +14,14 @@ import os
 
 
 def env_rank():
+    """(rank, world, local device) from the torchrun environment.  Rehearsal
+    on a one-GPU box: C2D_ONE_GPU=1 puts every rank on device 0 (with
+    C2D_DIST_BACKEND=gloo, since RCCL refuses two ranks on one device)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if os.environ.get("C2D_ONE_GPU") == "1":
+        local = 0
     return rank, world, local
 
 
@@ -28,7 +33,8 @@ def init(backend: str | None = None):
         import torch.distributed as dist
         if not dist.is_initialized():
             if backend is None:
-                backend = "nccl" if torch.cuda.is_available() else "gloo"
+                backend = os.environ.get("C2D_DIST_BACKEND") or (
+                    "nccl" if torch.cuda.is_available() else "gloo")
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kw = {}
             if backend == "nccl":
@@ -65,7 +71,7 @@ def allreduce_max(value: float, device=None) -> float:
 def barrier(device=None) -> None:
     if is_dist():
         import torch.distributed as dist
-        if device is not None and device.type == "cuda":
+        if device is not None and device.type == "cuda" and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
