@@ -23,9 +23,10 @@
  *   probe bundle g0  = (K_src, sub C2D_SUB_BUNDLE | g0)       probes g0.. tracked together:
  *                      their collision decisions and the colliders' absorption points
  *                      (DESIGN.md §2c);
- *   bundle points g0 = (K_src, sub C2D_SUB_ABSPT | g0)        the survivors' absorption points,
- *                      four 32-bit uniforms per Philox block (c2d_block4), a fresh
- *                      block for every shared step;
+ *   bundle points g0 = (K_src, sub C2D_SUB_ABSPT | g0)        the survivors' absorption points:
+ *                      output n = SplitMix64's finaliser of K_src + gamma*(sub<<32 | n)
+ *                      (c2d_abspt), two 32-bit uniforms per output, fresh outputs
+ *                      for every shared step;
  *                      a collider's record carries (K_src, sub 1+p, bundle ctr)
  *   recombined       = (K_src, sub C2D_SUB_RECOMB)            (imctrk2d.f:690-704)
  *   scatter copy ii  = derive(K_par, TAG_SCAT2, ii, ctr_par; sub_par)  (imctrk2d.f:611)
@@ -126,6 +127,20 @@ C2D_RHD void c2d_block4(uint64_t key, uint32_t sub, uint32_t m, uint32_t w[4]) {
 /* Uniform in (0,1) from 32 random bits, never 0 or 1 (exact). */
 C2D_RHD double c2d_u01_32(uint32_t a) {
   return ((double)a + 0.5) * 2.3283064365386962890625e-10;   /* 2^-32 */
+}
+
+/* Absorption-point stream of a probe bundle: output n of (key, sub) is the
+ * SplitMix64 finaliser (Steele, Lea & Flood, OOPSLA 2014; passes BigCrush) of
+ * key + gamma * (sub << 32 | n) -- counter-based like the Philox streams, at a
+ * third of a Philox block's multiplies per 64 random bits.  The high and low
+ * halves are two 32-bit uniforms (c2d_u01_32). */
+C2D_RHD uint64_t c2d_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+C2D_RHD uint64_t c2d_abspt(uint64_t key, uint32_t sub, uint32_t n) {
+  return c2d_mix64(key + 0x9E3779B97F4A7C15ull * (((uint64_t)sub << 32) | (uint64_t)n));
 }
 
 C2D_RHD uint64_t c2d_derive_s(uint64_t key, uint32_t tag, uint32_t a, uint32_t b, uint32_t sub) {

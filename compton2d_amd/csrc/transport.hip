@@ -1620,7 +1620,7 @@ struct Bundle {
   long long src;      /* source item                                             */
   uint32_t alive;     /* probes g0 + i still on the path (bit i)                 */
   uint32_t bctr;      /* draws consumed from the bundle stream                   */
-  uint32_t actr;      /* blocks consumed from the absorption-point stream        */
+  uint32_t actr;      /* outputs consumed from the absorption-point stream       */
   int32_t g0;         /* first probe of this bundle (== split1: refly alone)     */
   int32_t nscat;      /* probes of the source that collided                      */
   int32_t flags;
@@ -1937,20 +1937,19 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
 #else
     if (two) {
 #endif
-      /* four 32-bit uniforms per block of the bundle's point stream, a fresh
-       * block per shared step */
+      /* two 32-bit uniforms per output of the bundle's point stream
+       * (c2d_abspt), fresh outputs per shared step */
       const uint32_t sub = C2D_SUB_ABSPT | (uint32_t)b.g0;
 #if C2D_TABLE_COMTOT
       const double isig = 1.0 / sigabs;
       const double Aw = wmu * rpre, Bw = rpre * rpre;
 #endif
-      for (int t = 0; t < nabs; t += 4) {
-        uint32_t w[4];
-        c2d_block4(p.key, sub, b.actr++, w);
+      for (int t = 0; t < nabs; t += 2) {
+        const uint64_t wo = c2d_abspt(p.key, sub, b.actr++);
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < 2; j++) {
           if (t + j < nabs) {
-            const double x = c2d_u01_32(w[j]) * qabs;
+            const double x = c2d_u01_32(j == 0 ? (uint32_t)(wo >> 32) : (uint32_t)wo) * qabs;
 #if C2D_TABLE_COMTOT
 #if C2D_PT_SERIES
             /* -log(1-x): series below 1e-2 (8 terms, truncation < x^8/9 relative;

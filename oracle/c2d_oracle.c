@@ -918,7 +918,7 @@ static int flight_loop(c2o_ctx* c, pkt_t* p, int s, rng_t* g, double wtmin) {
  *                             u -> tau of the n-1 others from the collision point
  *   per step, survivors       each one's absorption point (xabs > 1e-5), in probe
  *                             order, from the point stream (key, C2D_SUB_ABSPT | g0):
- *                             four 32-bit uniforms per block, a fresh block per step
+ *                             two 32-bit uniforms per output, fresh outputs per step
  * Per copy, the geometry, absorption, deposits, collision records and
  * counters are the per-copy tracker's (flight_loop with s = -1); only the
  * random numbers that decide the collisions are drawn per bundle instead of
@@ -928,7 +928,7 @@ static int probe_bundle(c2o_ctx* c, const pkt_t* src, double s_ew, double wtmin,
                         const rng_t* g) {
   const double lim8 = 9.9999999e-1, lim9 = 0.999999999;
   rng_t gb = rng_sub(g, C2D_SUB_BUNDLE | (uint32_t)g0);
-  uint32_t actr = 0;                                 /* point-stream blocks */
+  uint32_t actr = 0;                                 /* point-stream outputs */
   pkt_t p = *src;
   p.ew = s_ew;
   uint32_t alive = G >= 32 ? 0xffffffffu : ((1u << G) - 1u);
@@ -1052,16 +1052,16 @@ static int probe_bundle(c2o_ctx* c, const pkt_t* src, double s_ew, double wtmin,
     double deleabs = p.ew - ewnew;
     if (deleabs < 1.0e-50) deleabs = 1.0e-50;
     /* the survivors' absorption points: the bundle's point stream (source
-     * key, C2D_SUB_ABSPT | g0), four 32-bit uniforms per Philox block, a
-     * fresh block per shared step (c2d_rng.h) */
+     * key, C2D_SUB_ABSPT | g0), two 32-bit uniforms per output (high half
+     * first), fresh outputs per shared step (c2d_rng.h c2d_abspt) */
     const double q = deleabs / p.ew;
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    uint64_t wo = 0;
     int t = 0;
     for (uint32_t m = alive; m; m &= m - 1u, t++) {
       double wmustar = wmu;
       if (xabs > 0.00001) {
-        if ((t & 3) == 0) c2d_block4(gb.key, C2D_SUB_ABSPT | (uint32_t)g0, actr++, w);
-        const double mr = c2d_u01_32(w[t & 3]);
+        if ((t & 1) == 0) wo = c2d_abspt(gb.key, C2D_SUB_ABSPT | (uint32_t)g0, actr++);
+        const double mr = c2d_u01_32((t & 1) == 0 ? (uint32_t)(wo >> 32) : (uint32_t)wo);
         const double sstar = -LOG(1.0 - mr * q) / sigabs;
         const double denom = SQRT(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
         wmustar = (wmu * rpre + sstar) / denom;
