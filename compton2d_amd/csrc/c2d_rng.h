@@ -31,7 +31,7 @@
  *   recombined       = (K_src, sub C2D_SUB_RECOMB)            (imctrk2d.f:690-704)
  *   scatter copy ii  = derive(K_par, TAG_SCAT2, ii, ctr_par; sub_par)  (imctrk2d.f:611)
  *   split3 copy ii2  = derive(K_chd, TAG_SCAT3, ii2, ctr_chd)          (imctrk2d.f:633)
- *   census key       = derive(K_pkt, TAG_CENSUS, ctr_pkt, 0; sub_pkt)  (imctrk2d.f:571)
+ *   census key       = census_key(K_pkt, ctr_pkt, sub_pkt)             (imctrk2d.f:571)
  * Draw n of (key, sub) is half (n & 1) of Philox_key({n >> 1, sub, 0, C_DRAW});
  * derive(key, tag, a, b; sub) = Philox_key({a, b, tag | sub << 8, C_DERIVE}).
  */
@@ -141,6 +141,15 @@ C2D_RHD uint64_t c2d_mix64(uint64_t z) {
 }
 C2D_RHD uint64_t c2d_abspt(uint64_t key, uint32_t sub, uint32_t n) {
   return c2d_mix64(key + 0x9E3779B97F4A7C15ull * (((uint64_t)sub << 32) | (uint64_t)n));
+}
+
+/* Lineage key of a census packet for the next step (replaces the per-packet
+ * fibran reseed, imctrk2d.f:571): a SplitMix64 hash of the packet's key and
+ * its stream position (sub, ctr) -- one per census write, so a 4-multiply
+ * hash instead of a Philox block. */
+C2D_RHD uint64_t c2d_census_key(uint64_t key, uint32_t ctr, uint32_t sub) {
+  const uint64_t pos = ((uint64_t)sub << 32) | (uint64_t)ctr;
+  return c2d_mix64(key ^ c2d_mix64(pos + 0x9E3779B97F4A7C15ull * (uint64_t)C2D_TAG_CENSUS));
 }
 
 C2D_RHD uint64_t c2d_derive_s(uint64_t key, uint32_t tag, uint32_t a, uint32_t b, uint32_t sub) {

@@ -665,11 +665,7 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
                                 | (p.esw == -1 ? C2D_CENS_ESW : 0u)
 #endif
     );
-#ifdef C2D_ABLATE_DERIVE               /* profiling ablation only */
-    gst(P.cout.key + slot, p.key ^ p.ctr ^ ((uint64_t)p.sub << 32));
-#else
-    gst(P.cout.key + slot, c2d_derive_s(p.key, C2D_TAG_CENSUS, p.ctr, 0u, p.sub));
-#endif
+    gst(P.cout.key + slot, c2d_census_key(p.key, p.ctr, p.sub));
   } else {
     gor(P.err, ERR_CENSUS);
   }

@@ -685,7 +685,7 @@ static void census_write(c2o_ctx* c, pkt_t* p, rng_t* g) {
   q->i[0] = p->jgpsp; q->i[1] = p->jgplc; q->i[2] = p->jgpmu;
   q->i[3] = p->jph; q->i[4] = p->kph;
   if (g->mode == C2O_RNG_LINEAGE)
-    q->key = c2d_derive_s(g->key, C2D_TAG_CENSUS, g->ctr, 0u, g->sub);
+    q->key = c2d_census_key(g->key, g->ctr, g->sub);
   else
     q->key = (uint64_t)(int64_t)(int32_t)(U(g) * 1.0e5);
   TALLY(c, counters + C2D_CNT_CENSUS) += 1.0;
