@@ -1245,9 +1245,16 @@ __device__ __forceinline__ void load_pk(Pkt& p, const PktSoA& s, int64_t i) {
 __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_source_kernel)(const KParams* __restrict__ Pg) {
   const KParams& P = *Pg;
   __shared__ double geo_lds[GEO_DOUBLES];
+  /* the volume-source prefix over cells, for the per-packet cell search
+   * (9-10 dependent probes): in LDS when it fits */
+  constexpr int PREF_LDS = 1100;
+  __shared__ int64_t pref_lds[PREF_LDS];
+  const bool pref_in_lds = P.ncell + 1 <= PREF_LDS;
   {
     const double* gsrc = reinterpret_cast<const double*>(P.geo);
     for (int i = threadIdx.x; i < GEO_DOUBLES; i += SBLOCK) geo_lds[i] = gsrc[i];
+    if (pref_in_lds)
+      for (int i = threadIdx.x; i <= P.ncell; i += SBLOCK) pref_lds[i] = P.vol_prefix[i];
   }
   __syncthreads();
   const Geo* g = reinterpret_cast<const Geo*>(geo_lds);
@@ -1259,7 +1266,18 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_source_kernel)(const KPara
     p.sub = 0;
     if (it < P.n_vol_items) {
       const int64_t gidx = it * P.world + P.rank;
-      const int cell = upper_index(P.vol_prefix, P.ncell, gidx);
+      int cell;
+      if (pref_in_lds) {
+        int lo = 0, hi = P.ncell - 1;       /* upper_index on the LDS copy */
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (pref_lds[mid] <= gidx) lo = mid;
+          else hi = mid - 1;
+        }
+        cell = lo;
+      } else {
+        cell = upper_index(P.vol_prefix, P.ncell, gidx);
+      }
       const int64_t nn = gidx - P.vol_prefix[cell];
       p.key = c2d_derive(P.step_key, C2D_TAG_VOL, (uint32_t)nn, (uint32_t)cell);
       p.bins = 0u;                       /* kap 0: census/volume phase */
