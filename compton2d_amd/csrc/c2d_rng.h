@@ -4,15 +4,18 @@
  * Replaces the reference's lagged-Fibonacci zone streams (src/rand.f:9-316:
  * seed_zone, initialize_rand, fibran, RNFSTR/RNFARR) whose draws depend on
  * the depth-first order in which one worker tracks every packet of a zone.
- * Here every packet owns a Philox4x32-10 stream (key = 64-bit lineage key,
- * counter = draws consumed, two draws per Philox block), and children derive their keys from the
- * parent's key at the point of the split, so a packet history is the same
+ * Here every packet owns a counter-based stream (key = 64-bit lineage key,
+ * counter = draws consumed): draw n of stream (key, sub) is the SplitMix64
+ * output (Steele, Lea & Flood, OOPSLA 2014; passes BigCrush) for the state
+ * key + gamma * ((sub << 32 | n) + 1), one 64-bit output per draw.  Children derive
+ * their keys from the parent's key at the point of the split with
+ * Philox4x32-10 (Salmon et al., SC'11), so a packet history is the same
  * whatever lane, wave, generation or GPU tracks it.
  *
  * A stream is (key, sub): sub = 0 for a packet's own stream, and the split1
  * copies of a source (which only differ in their random numbers) use
  * sub-streams of the source key instead of derived keys, so starting a
- * copy costs no Philox call.
+ * copy costs no key derivation.
  *
  * Lineage rules (shared by the HIP kernels and the oracle's lineage mode):
  *   step key      S  = derive(seed, TAG_STEP, ncycle, 0)
@@ -24,15 +27,14 @@
  *                      their collision decisions and the colliders' absorption points
  *                      (DESIGN.md §2c);
  *   bundle points g0 = (K_src, sub C2D_SUB_ABSPT | g0)        the survivors' absorption points:
- *                      output n = SplitMix64's finaliser of K_src + gamma*(sub<<32 | n)
- *                      (c2d_abspt), two 32-bit uniforms per output, fresh outputs
- *                      for every shared step;
+ *                      two 32-bit uniforms per 64-bit output (c2d_abspt), fresh
+ *                      outputs for every shared step;
  *                      a collider's record carries (K_src, sub 1+p, bundle ctr)
  *   recombined       = (K_src, sub C2D_SUB_RECOMB)            (imctrk2d.f:690-704)
  *   scatter copy ii  = derive(K_par, TAG_SCAT2, ii, ctr_par; sub_par)  (imctrk2d.f:611)
  *   split3 copy ii2  = derive(K_chd, TAG_SCAT3, ii2, ctr_chd)          (imctrk2d.f:633)
  *   census key       = census_key(K_pkt, ctr_pkt, sub_pkt)             (imctrk2d.f:571)
- * Draw n of (key, sub) is half (n & 1) of Philox_key({n >> 1, sub, 0, C_DRAW});
+ * Draw n of (key, sub) = u53(mix64(key + gamma * ((sub << 32 | n) + 1)));
  * derive(key, tag, a, b; sub) = Philox_key({a, b, tag | sub << 8, C_DERIVE}).
  */
 #ifndef C2D_RNG_H
@@ -98,55 +100,42 @@ C2D_RHD double c2d_u01_bits(uint32_t a, uint32_t b) {
 #define C2D_SUB_BUNDLE  0x800000u   /* | g0: the stream of the probe bundle starting at g0 */
 #define C2D_SUB_ABSPT   0xC00000u   /* | g0: that bundle's absorption-point stream          */
 
-/* Draw number n of stream (key, sub).  One Philox block gives two uniforms:
- * draws 2m and 2m+1 are the low and high halves of block m, so a tracker
- * that keeps the high half (c2d_draw_pair) pays one block per two draws. */
-C2D_RHD double c2d_draw_s(uint64_t key, uint32_t sub, uint32_t n) {
-  uint32_t c[4] = {n >> 1, sub, 0u, C2D_DRAW_C3};
-  c2d_philox(c, (uint32_t)key, (uint32_t)(key >> 32));
-  return (n & 1u) ? c2d_u01_bits(c[2], c[3]) : c2d_u01_bits(c[0], c[1]);
-}
-
-C2D_RHD double c2d_draw(uint64_t key, uint32_t n) { return c2d_draw_s(key, 0u, n); }
-
-/* Both draws of block m = n >> 1 (n even): returns draw n, *next = draw n+1. */
-C2D_RHD double c2d_draw_pair(uint64_t key, uint32_t sub, uint32_t n, double* next) {
-  uint32_t c[4] = {n >> 1, sub, 0u, C2D_DRAW_C3};
-  c2d_philox(c, (uint32_t)key, (uint32_t)(key >> 32));
-  *next = c2d_u01_bits(c[2], c[3]);
-  return c2d_u01_bits(c[0], c[1]);
-}
-
-/* Block m of stream (key, sub) as four 32-bit words (absorption-point
- * uniforms: c2d_u01_32 of each word). */
-C2D_RHD void c2d_block4(uint64_t key, uint32_t sub, uint32_t m, uint32_t w[4]) {
-  w[0] = m; w[1] = sub; w[2] = 0u; w[3] = C2D_DRAW_C3;
-  c2d_philox(w, (uint32_t)key, (uint32_t)(key >> 32));
-}
-
 /* Uniform in (0,1) from 32 random bits, never 0 or 1 (exact). */
 C2D_RHD double c2d_u01_32(uint32_t a) {
   return ((double)a + 0.5) * 2.3283064365386962890625e-10;   /* 2^-32 */
 }
 
-/* Absorption-point stream of a probe bundle: output n of (key, sub) is the
- * SplitMix64 finaliser (Steele, Lea & Flood, OOPSLA 2014; passes BigCrush) of
- * key + gamma * (sub << 32 | n) -- counter-based like the Philox streams, at a
- * third of a Philox block's multiplies per 64 random bits.  The high and low
- * halves are two 32-bit uniforms (c2d_u01_32). */
+/* SplitMix64's output function. */
 C2D_RHD uint64_t c2d_mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
+
+/* 64-bit output n of stream (key, sub): output (sub << 32 | n) of the
+ * SplitMix64 sequence seeded with the key (state key + (i + 1) * gamma), so
+ * the streams of one key are disjoint 2^32-long segments of it. */
+C2D_RHD uint64_t c2d_stream64(uint64_t key, uint32_t sub, uint32_t n) {
+  return c2d_mix64(key + 0x9E3779B97F4A7C15ull * ((((uint64_t)sub << 32) | (uint64_t)n) + 1ull));
+}
+
+/* Draw number n of stream (key, sub): 53 random bits, in (0,1). */
+C2D_RHD double c2d_draw_s(uint64_t key, uint32_t sub, uint32_t n) {
+  const uint64_t x = c2d_stream64(key, sub, n);
+  return c2d_u01_bits((uint32_t)(x >> 32), (uint32_t)x);
+}
+
+C2D_RHD double c2d_draw(uint64_t key, uint32_t n) { return c2d_draw_s(key, 0u, n); }
+
+/* Absorption-point stream of a probe bundle: output n as two 32-bit uniforms
+ * (c2d_u01_32 of the high and the low half). */
 C2D_RHD uint64_t c2d_abspt(uint64_t key, uint32_t sub, uint32_t n) {
-  return c2d_mix64(key + 0x9E3779B97F4A7C15ull * (((uint64_t)sub << 32) | (uint64_t)n));
+  return c2d_stream64(key, sub, n);
 }
 
 /* Lineage key of a census packet for the next step (replaces the per-packet
  * fibran reseed, imctrk2d.f:571): a SplitMix64 hash of the packet's key and
- * its stream position (sub, ctr) -- one per census write, so a 4-multiply
- * hash instead of a Philox block. */
+ * its stream position (sub, ctr), one per census write. */
 C2D_RHD uint64_t c2d_census_key(uint64_t key, uint32_t ctr, uint32_t sub) {
   const uint64_t pos = ((uint64_t)sub << 32) | (uint64_t)ctr;
   return c2d_mix64(key ^ c2d_mix64(pos + 0x9E3779B97F4A7C15ull * (uint64_t)C2D_TAG_CENSUS));

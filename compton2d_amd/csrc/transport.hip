@@ -106,7 +106,6 @@ struct Pkt {
   uint32_t bins;      /* jgpsp | jgplc << 8 | jgpmu << 16 | kap << 24 (PktSoA layout): the
                          spectral bins (imcleak2d.f) and the kappa phase (H3) in one register */
   int32_t ie;         /* E_ph bin of xnu (imctrk2d.f:382-384), cached per xnu     */
-  double rnext;       /* draw ctr of `key` when ctr is odd (second half of a block) */
   uint64_t key;
   uint32_t sub;       /* lineage sub-stream: split1 copies of a source (c2d_rng.h) */
   uint32_t ctr;
@@ -196,17 +195,10 @@ __device__ __forceinline__ const KParams& cold(const KParams& P) {
 #endif
 }
 
-/* Next draw of the packet's stream.  Every key change sets ctr = 0, except a
- * packet loaded from a record mid-stream, which calls rng_sync first. */
+/* Next draw of the packet's stream (every key change sets ctr = 0; a packet
+ * loaded from a record resumes at the record's ctr). */
 __device__ __forceinline__ double U(Pkt& p) {
-  double v;
-  if (p.ctr & 1u) v = p.rnext;
-  else v = c2d_draw_pair(p.key, p.sub, p.ctr, &p.rnext);
-  p.ctr++;
-  return v;
-}
-__device__ __forceinline__ void rng_sync(Pkt& p) {
-  if (p.ctr & 1u) p.rnext = c2d_draw_s(p.key, p.sub, p.ctr);
+  return c2d_draw_s(p.key, p.sub, p.ctr++);
 }
 
 __device__ __forceinline__ double clampd(double v, double lim) {
@@ -1503,7 +1495,6 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
         /* a scatter secondary, tracked as imctrk2d(1) (imctrk2d.f:662-679) */
         load_pk(p, cold(P).pk, item);
         set_phi(p, p.phi);
-        rng_sync(p);
         p.mode = 1;
         p.wtmin = 1.0e-10 * p.ew;
         state = ST_TRACK;
@@ -1630,7 +1621,6 @@ struct Bundle {
   Pkt p;              /* shared path; p.ew, p.wtmin, p.ctr: the recombined copy's */
   double ewp, wtminp; /* the probes' common weight and kill threshold               */
   double tau;         /* optical depth (per probe) to the next collision among them */
-  double brnext;      /* second half of the bundle stream's last Philox block       */
   long long src;      /* source item                                             */
   uint32_t alive;     /* probes g0 + i still on the path (bit i)                 */
   uint32_t bctr;      /* draws consumed from the bundle stream                   */
@@ -1643,11 +1633,7 @@ struct Bundle {
 
 /* next draw of the bundle stream (source key, C2D_SUB_BUNDLE | g0) */
 __device__ __forceinline__ double UB(Bundle& b) {
-  double v;
-  if (b.bctr & 1u) v = b.brnext;
-  else v = c2d_draw_pair(b.p.key, C2D_SUB_BUNDLE | (uint32_t)b.g0, b.bctr, &b.brnext);
-  b.bctr++;
-  return v;
+  return c2d_draw_s(b.p.key, C2D_SUB_BUNDLE | (uint32_t)b.g0, b.bctr++);
 }
 
 /* start (or restart) the bundle at probe g0 of source b.src */
@@ -2026,7 +2012,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
   Bundle b;
   b.p.mode = 0; b.p.bins = 0u; b.p.ctr = 0; b.p.key = 0; b.p.sub = 0; b.p.nflight = 0;
   b.alive = 0; b.flags = 0; b.src = 0; b.g0 = 0; b.nscat = 0; b.bctr = 0; b.tsteps = 0;
-  b.tau = 0.0; b.brnext = 0.0; b.ewp = 0.0; b.wtminp = 0.0;
+  b.tau = 0.0; b.ewp = 0.0; b.wtminp = 0.0;
   bool busy = false;
   ComCache cc = {-1, -1, 0.0, 0.0};
   LaneCnt lc = {0u};

@@ -59,7 +59,7 @@ def rel_l2(a, b):
 def oracle_run(args):
     """(F(E), edout, escapes) of one oracle run: ('fib', seed) with the
     reference's lagged-Fibonacci zone streams, or ('lineage', seed, rank, world)
-    with the engine's Philox lineage streams on a shard of the sources."""
+    with the engine's counter-based lineage streams on a shard of the sources."""
     import oracle_lib as OL
     kind, seed = args[0], args[1]
     rank, world = (args[2], args[3]) if kind == "lineage" else (0, 1)

@@ -9,7 +9,7 @@ the same stochastic process as the reference's per-copy tracking
 (src/imctrk2d.f:106-123, a fresh colmfp per copy and packet-step), with other
 random numbers.  The statistical reference is the oracle's lineage mode with
 C2O_PROBE_BUNDLES=0: the reference's per-copy loop (flight_loop with s = -1, a
-fresh colmfp per copy and packet-step) on the same Philox family, streams
+fresh colmfp per copy and packet-step) on the same lineage stream family, streams
 (source key, 1 + probe).
 
 Workload: the golden 'ssc_tau' step (2x2 zones, n_e = 4e6, ~4 collisions per

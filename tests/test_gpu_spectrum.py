@@ -5,7 +5,7 @@ F(E) = fout / dE) <= 1 %.
 
 "Reference CPU path on identical seeds" = the C oracle (oracle/c2d_oracle.c:
 the reference's algorithm, glibc libm, pinned bit-exactly to the Fortran
-reference in tests/test_oracle_golden.py) drawing the same per-packet Philox
+reference in tests/test_oracle_golden.py) drawing the same per-packet counter-based
 streams as the GPU.  The only differences left are the fast kernel's tabulated
 comtot (< 1e-7 relative) and FMA-free vs libm rounding, which flip a handful of
 collision/census decisions: the measured deviation is orders of magnitude
@@ -65,7 +65,7 @@ def test_fast_kernel_spectrum_within_1pct_of_reference_cpu_path(kappa_lag):
 
 
 def test_fast_kernel_spectrum_vs_reference_stream_fixture():
-    """The production kernel (tabulated comtot, Philox lineage streams) on the
+    """The production kernel (tabulated comtot, counter-based lineage streams) on the
     north-star spectrum workload (tests/spectrum_case.py, 1e7 packets: ~9.5e6
     escapes) against the reference algorithm WITH the reference's own
     lagged-Fibonacci streams (tests/golden/spectrum_fib.npz: 3 seeds x 1.9e6

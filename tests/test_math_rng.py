@@ -65,7 +65,7 @@ def test_branch_free_log_bitwise_equals_log():
     np.testing.assert_array_equal(y5.view(np.uint64), y0.view(np.uint64))
 
 
-def test_philox_known_answers():
+def test_rng_known_answers():
     lib = OL.load("det")
     # Random123 kat_vectors, philox4x32-10: (ctr, key) -> out
     kats = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
@@ -87,22 +87,34 @@ def test_philox_known_answers():
             assert d == (w[1] << 32) | w[0]
         for n in (0, 1, 2, 17, 1 << 20, (1 << 20) + 1):
             u = lib.c2o_unit_philox_draw(key, n)
-            # draws 2m, 2m+1 = low / high half of Philox block m
-            w = philox_py((n >> 1, 0, 0, 0x5EEDD1CE), (key & 0xffffffff, key >> 32))
-            hi, lo = (w[2], w[3]) if n & 1 else (w[0], w[1])
-            x = (((hi << 32) | lo) >> 11)
+            # draw n = 53 bits of SplitMix64 output n of the sequence seeded with key
+            x = splitmix_py(key, n) >> 11
             assert u == (x + 0.5) * 2.0 ** -53
             assert 0.0 < u < 1.0
         # sub-streams (split1 copies) and sub-stream derivations
         for sub in (1, 7, 0xFFFFFF):
             for n in (0, 1, 5):
                 u = lib.c2o_unit_philox_draw_s(key, sub, n)
-                w = philox_py((n >> 1, sub, 0, 0x5EEDD1CE), (key & 0xffffffff, key >> 32))
-                hi, lo = (w[2], w[3]) if n & 1 else (w[0], w[1])
-                assert u == ((((hi << 32) | lo) >> 11) + 0.5) * 2.0 ** -53
+                assert u == ((splitmix_py(key, (sub << 32) | n) >> 11) + 0.5) * 2.0 ** -53
             d = lib.c2o_unit_derive_s(key, 11, 5, 9, sub)
             w = philox_py((5, 9, 11 | (sub << 8), 0x9E3779B9), (key & 0xffffffff, key >> 32))
             assert d == (w[1] << 32) | w[0]
+
+
+def splitmix_py(seed, i):
+    """Output i (0-based) of SplitMix64 seeded with `seed` (Steele, Lea &
+    Flood 2014; java.util.SplittableRandom): state seed + (i+1)*gamma, mixed."""
+    m = (1 << 64) - 1
+    z = (seed + (i + 1) * 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def test_splitmix_known_answers():
+    # the published SplitMix64 sequence for seed 0 (reference splitmix64.c)
+    assert [splitmix_py(0, i) for i in range(3)] == [0xE220A8397B1DCDAF, 0x6E789E6AA1B965F4,
+                                                     0x06C45D188009454F]
 
 
 def philox_py(ctr, key):
