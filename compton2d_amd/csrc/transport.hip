@@ -1739,6 +1739,9 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
   p.wmu = clampd(p.wmu, lim8);
   lc.paths++;
   const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
+  /* the step's absorption coefficient: issued before the comtot lookup and
+   * the geometry, used after them */
+  const double kap_cell = gld((KAP(p) ? P.kappa_s : P.kappa_cv) + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
   double sigsc = 1.0;
   if (b.alive) {
 #if C2D_TABLE_COMTOT
@@ -1805,12 +1808,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
   /* every copy that does not collide: boundary if trldb < dcen, else census */
   const bool bnd = trldb < p.dcen;
   const double trld = bnd ? trldb : p.dcen;
-#if C2D_TABLE_COMTOT && C2D_EARLY_LOADS
-  double sigabs = 1.0e-40 + 1.0 * gld((KAP(p) ? P.kappa_s : P.kappa_cv) + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
-#else
-  const double* kap = KAP(p) ? P.kappa_s : P.kappa_cv;
-  double sigabs = 1.0e-40 + 1.0 * gld(kap + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
-#endif
+  double sigabs = 1.0e-40 + 1.0 * kap_cell;
   if (sigabs < 1.0e-40) sigabs = 1.0e-40;
   const double xabs = sigabs * trld;
   const double ex = (xabs < 100.0) ? c2d_exp(-xabs) : 0.0;
