@@ -702,11 +702,7 @@ __device__ __forceinline__ void load_rec(Pkt& p, const ScatRec& r) {
 __device__ __forceinline__ void cache_energy(const KParams& P, const Geo* g, Pkt& p) {
   p.ie = grid_lookup(g->E_ph, C2D_N_VOL, g->eph_start, g->eph_k0, p.xnu);
 #if C2D_TABLE_COMTOT
-#ifdef C2D_ABLATE_TRIG                 /* profiling ablation only */
-  const double s = (p.xnu * 1e-3 - C2D_COMTAB_U0) * P.comtab_du_inv;
-#else
   const double s = (c2d_log(p.xnu) - C2D_COMTAB_U0) * P.comtab_du_inv;
-#endif
   if (s >= 1.0 && s < (double)(C2D_COMTAB_N - 3)) {
     p.tg = (int32_t)s;
     p.tt = s - (double)p.tg;
@@ -725,11 +721,7 @@ __device__ __forceinline__ void cache_energy(const KParams& P, const Geo* g, Pkt
 __device__ __forceinline__ void set_phi(Pkt& p, double phi) {
   p.phi = phi;
 #if C2D_TABLE_COMTOT
-#ifdef C2D_ABLATE_TRIG
-  p.eta = 1.0 - 0.3 * phi;
-#else
   p.eta = c2d_cos(phi);
-#endif
   p.esw = (phi <= PI_REF && phi >= 1.0e-10) ? 1 : -1;
 #endif
 }
@@ -1889,11 +1881,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
 #if C2D_TABLE_COMTOT
     p.eta = Etan;
     if ((b.flags & BF_TRACK) && leaves) {   /* an escape event reads phi (census: encoded) */
-#ifdef C2D_ABLATE_TRIG
-      p.phi = 1.5 - Etan;
-#else
       p.phi = c2d_acos(Etan);
-#endif
       if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
     }
 #else
