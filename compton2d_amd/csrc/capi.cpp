@@ -818,18 +818,17 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     /* a census write beyond the capacity: fail before the compaction reads
      * records from reserved slots past the end of the buffer */
     int32_t herr0 = 0;
-    HIPCHK(c, hipMemcpyAsync(&herr0, c->derr, sizeof herr0, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (herr0 & ERR_CENSUS)
-      return fail(c, C2D_E_CENSUS_OVERFLOW, "census overflow (capacity %lld)",
-                  (long long)cfg.census_capacity);
     unsigned long long reserved = 0;
+    HIPCHK(c, hipMemcpyAsync(&herr0, c->derr, sizeof herr0, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&reserved, c->ctl + CTL_NCOUT, sizeof reserved, hipMemcpyDeviceToHost,
                              c->stream));
     HIPCHK(c, hipMemcpyAsync(c->h_holes.data(), c->cens_holes,
                              sizeof(unsigned long long) * c->h_holes.size(), hipMemcpyDeviceToHost,
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (herr0 & ERR_CENSUS)
+      return fail(c, C2D_E_CENSUS_OVERFLOW, "census overflow (capacity %lld)",
+                  (long long)cfg.census_capacity);
     std::vector<std::pair<int64_t, int64_t>> holes;
     int64_t nh = 0;
     for (size_t w = 0; w + 1 < c->h_holes.size(); w += 2) {
