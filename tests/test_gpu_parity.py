@@ -82,6 +82,10 @@ def test_fast_kernel_close_to_oracle(name):
         for k in ("edep", "ecens", "npcen", "erlko", "erlku", "fout", "edout"):
             a, b = np.sum(tg[k]), np.sum(to[k])
             assert abs(a - b) <= 1e-3 * max(abs(b), 1e-300), (name, n, k, a, b)
+        # radiation-pressure deposits (signed: compared against their magnitude);
+        # the fast build's point loop uses a series for -log(1-x) and v_rsq_f64
+        a, b = np.asarray(tg["prdep"]), np.asarray(to["prdep"])
+        assert np.sum(np.abs(a - b)) <= 1e-3 * max(np.sum(np.abs(b)), 1e-300), (name, n, "prdep")
 
 
 @pytest.mark.parametrize("fn,lo,hi", [(0, 1e-300, 1e300), (1, -700.0, 700.0), (2, -7.0, 14.0),
@@ -108,7 +112,8 @@ def test_device_branch_free_log_equals_host():
     np.testing.assert_array_equal(yd.view(np.uint64), y.view(np.uint64))
 
 
-def test_device_philox_equals_host():
+def test_device_draws_equal_host():
+    """Lineage draws (c2d_rng.h c2d_draw): device = host bit for bit."""
     keys = np.array([0, 1, 0x5EEDC2D, 2 ** 53 - 1], np.float64)
     x = np.repeat(keys, 1000)
     yd = device_math(7, x)
