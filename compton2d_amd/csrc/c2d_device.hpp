@@ -134,7 +134,9 @@ __device__ __forceinline__ void gor(int32_t* p, int32_t v) {
  * generation.  f64 atomics execute at the memory side and serialise per
  * address; packets that census together share (cell, energy bin), so a single
  * copy is a hot spot (2.5x on the EC light-curve workload). */
+#ifndef C2D_NF_REPL
 #define C2D_NF_REPL 32
+#endif
 
 /* internal counter slot (not part of the tally buffer's counters, zeroed
  * before the counters are copied there): lane path-steps = passes of a lane
