@@ -173,6 +173,7 @@ struct KParams {
   const double* comtab;         /* [ncell][C2D_COMTAB_N] cosig on the u grid, f64 (as the
                                    reference evaluates comtot; 16 KB per cell)               */
   double comtab_du_inv;
+  double egg_min;            /* E_field(1)^2 / E_field(2): n_field threshold (imctrk2d.f:547-556) */
   /* census */
   CensusSoA cin, cout;
   int64_t n_cin, cap_cout;

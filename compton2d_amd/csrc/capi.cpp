@@ -160,6 +160,7 @@ struct c2d_ctx {
   float last_src_ms = 0.f;
   unsigned long long last_prof[C2D_TR_PROF_WORDS] = {};  /* transport section counters */
   int64_t last_g0_steps = 0;
+  double egg_min = 0.0;          /* E_field(1)^2 / E_field(2) (census n_field threshold) */
   int64_t last_g0_paths = 0, last_all_paths = 0;   /* lane path-steps (C2D_CNT_PATHS_INT) */
   int last_launches = 0;
   /* Fokker-Planck */
@@ -286,6 +287,7 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   for (int k = 0; k < c->nr; k++) g.r[k + 1] = cfg->r[k];
   for (int i = 0; i < C2D_N_VOL; i++) g.E_ph[i + 1] = cfg->E_ph[i];
   for (int i = 0; i < C2D_NPHFIELD; i++) g.E_field[i + 1] = cfg->E_field[i];
+  c->egg_min = (g.E_field[1] * g.E_field[1]) / g.E_field[2];   /* imctrk2d.f Egg_min */
   build_lookup(g.E_ph, C2D_N_VOL, g.eph_start, &g.eph_k0);
   build_lookup(g.E_field, C2D_NPHFIELD, g.efl_start, &g.efl_k0);
   for (int i = 0; i <= cfg->nphtotal; i++) g.hu[i + 1] = cfg->hu[i];
@@ -656,6 +658,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.spectra = c->spectra; P.n_spectra = c->n_spectra; P.nslot = c->nslot;
   P.comtab = c->comtab;
   P.comtab_du_inv = (double)(C2D_COMTAB_N - 1) / (C2D_COMTAB_U1 - C2D_COMTAB_U0);
+  P.egg_min = c->egg_min;
   const int in_buf = c->cur_out, out_buf = 1 - c->cur_out;
   P.cin = c->cens[in_buf].soa();
   P.cout = c->cens[out_buf].soa();

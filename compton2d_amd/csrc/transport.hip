@@ -630,15 +630,15 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
   int cell = (p.jph - 1) * P.nr + (p.kph - 1);
   cell_add(P, T, TC_NPCEN, cell, 1.0);
   cell_add(P, T, TC_ECENS, cell, p.ew);
-  int i = grid_lookup(g->E_field, C2D_NPHFIELD, g->efl_start, g->efl_k0, p.xnu);
-  double Egg_min = (g->E_field[1] * g->E_field[1]) / g->E_field[2];
 #ifdef C2D_ABLATE_NFIELD                /* profiling ablation only (tools/build_sweep.sh) */
-  if (p.xnu < 0.0)
+  if (p.xnu < 0.0) {
 #else
-  if (p.xnu > Egg_min)
+  if (p.xnu > P.egg_min) {              /* Egg_min = E_field(1)^2/E_field(2), host-computed */
 #endif
+    const int i = grid_lookup(g->E_field, C2D_NPHFIELD, g->efl_start, g->efl_k0, p.xnu);
     gadd(&P.nf_rep[(int64_t)(blockIdx.x % C2D_NF_REPL) * P.ncell * C2D_NPHFIELD +
                    (int64_t)cell * C2D_NPHFIELD + (i - 1)], 6.25e8 * p.ew / p.xnu);
+  }
   unsigned long long slot = cch ? census_slot_chunk(P, *cch) : wave_reserve(P.n_cout);
   if (slot < (unsigned long long)P.cap_cout) {
     gst(P.cout.rpre + slot, p.rpre);
