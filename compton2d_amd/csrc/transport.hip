@@ -944,7 +944,10 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
       p.kph = knew;
       if (p.mode == -1) return FL_END;
       TP_COUNT(pf, TP_LEAK_W, TP_LEAK_L);
-      if (imcleak(P, T, p, lc) == 1) return FL_END;
+      if (imcleak(P, T, p, lc) == 1) {
+        if (p.mode == 1) LC_ADD(lc, C2D_CNT_ESC_SCAT);
+        return FL_END;
+      }
       set_phi(p, p.phi);                        /* axis pass-through set phi = 1e-6 */
       return FL_CONT;
     }

@@ -180,6 +180,7 @@ typedef struct c2d_tally_layout {
 #define C2D_CNT_EVENTS     7   /* event-file records written                      */
 #define C2D_CNT_GENS       8   /* scatter generations launched                    */
 #define C2D_CNT_ABORTED    9   /* packets stopped by a safety cap (must stay 0)   */
+#define C2D_CNT_ESC_SCAT  11   /* escapes of scattered packets (imctrk2d(1) copies) */
 #define C2D_NCOUNTERS      16
 
 static inline void c2d_tally_layout_for(int32_t nz, int32_t nr, int32_t nmu,

@@ -885,7 +885,10 @@ static int flight_loop(c2o_ctx* c, pkt_t* p, int s, rng_t* g, double wtmin) {
         p->jph = jnew;
         p->kph = knew;
         if (s == -1) return 0;
-        if (imcleak(c, p) == 1) return 0;
+        if (imcleak(c, p) == 1) {
+          if (s == 1) TALLY(c, counters + C2D_CNT_ESC_SCAT) += 1.0;
+          return 0;
+        }
         continue;
       }
       p->kph = knew;

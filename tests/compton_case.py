@@ -1,0 +1,91 @@
+"""The Compton spectrum workload (SURVEY.md §8(d) parity metric on the
+scattered component) — TEST INFRASTRUCTURE.
+
+The north-star spectrum workload (tests/spectrum_case.py: the inputm.dat
+medium of C3 on 2x2 zones, one MC step with ncycle = 1 and dt = 30 x the C2
+step) with the electron density scaled by N_E_FACTOR = 5e4 (n_e = 4e6 cm^-3,
+the `ssc_tau` golden case's density): the Thomson depth of the blob rises to
+~0.02, so a source makes ~0.14 collisions (split1 = 10 probes), every
+collision hands split2 = 10 secondaries a Klein-Nishina sample of the
+power-law electrons (gmin 1e2 .. gmax 1e5, p = 2.3, src/compb_2d.f:1-318),
+and gains above split1*split2*spl3_trg = 1000 trigger split3 resampling
+(src/imctrk2d.f:580-684).  Above COMPTON_E_MIN = 1e-3 keV more than 87 % of
+F(E) is carried by scattered packets (measured with n_e -> 0: tests/
+golden/make_compton.py prints the unscattered share per bin), so the bins and
+light-curve bands above it pin the scattered component:
+LC bands 1..4 = (1e-3,1), (1,1e2), (1e2,1e5), (1e5,1e9) keV.
+
+The band energies are heavy-tailed (a gain of up to ~gamma^2 = 1e10 per
+scattering off the p = 2.3 tail): a run of 2e4 sources has a relative
+seed-to-seed scatter of 6 %, 30 %, 40 % and 68 % in bands 1..4, so the
+reference-stream side of a 1 % comparison needs ~1e8 sources
+(tests/golden/compton_fib.npz); the identical-seed comparison (same lineage
+streams on both sides) does not: it is per history.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import spectrum_case as S
+from compton2d_amd import abi, synth
+
+N_E_FACTOR = 5.0e4
+COMPTON_E_MIN = 1.0e-3                # keV: lower edge of the first Compton bin/band
+COMPTON_BANDS = (1, 2, 3, 4)          # lcb_01.dat columns carried by scattered packets
+LINEAGE_SEED = 0x5EEDC2D
+IDENT_SOURCES = 1_000_000             # identical-seed fixture (oracle lineage, det math)
+IDENT_SHARDS = 8
+FIB_SOURCES = 100_000                 # per reference-stream (fib) run
+FIB_CHECK_SOURCES = 20_000            # the run the CPU test recomputes bit for bit
+FIB_SEED0 = 10007
+
+
+def fib_seed(k: int) -> int:
+    """rseed of the k-th reference-stream run (distinct lagged-Fibonacci streams)."""
+    return FIB_SEED0 + 7919 * k
+
+
+def workload(mode=abi.COMTOT_EXACT, seed=LINEAGE_SEED, rank=0, world=1, n=IDENT_SOURCES, device=0,
+             queue_capacity=None):
+    grid, si = S.workload(mode=mode, seed=seed, rank=rank, world=world, n=n, device=device)
+    si.n_e = si.n_e * N_E_FACTOR
+    # collisions: ~0.15 per source, split3 records a fraction of that
+    per = int(np.ceil(n / world))
+    grid.queue_capacity = queue_capacity or max(1 << 20, per // 2)
+    grid.census_capacity = max(grid.census_capacity, per // 2 + 4096)
+    grid.event_capacity = max(grid.event_capacity, 8 * per + 4096)
+    return grid, si
+
+
+def compton_bins() -> np.ndarray:
+    """Indices of the spb.dat bins whose lower edge is >= COMPTON_E_MIN."""
+    hu = synth.photon_grid()
+    return np.nonzero(hu[:-1] >= COMPTON_E_MIN * (1 - 1e-12))[0]
+
+
+def oracle_run(args):
+    """One oracle run of the Compton workload: ('fib', seed, n) with the
+    reference's lagged-Fibonacci streams (glibc: bit-exact to the Fortran),
+    or ('lineage', seed, n, rank, world, flavor) with the engine's lineage
+    streams on a shard of the sources.  Returns the full tally vector."""
+    import oracle_lib as OL
+    kind, seed, n = args[0], args[1], args[2]
+    if kind == "fib":
+        grid, si = workload(seed=seed, n=n)
+        o = OL.Oracle(grid, OL.RNG_FIB, "ref", rseed=seed)
+    else:
+        rank, world, flavor = args[3], args[4], args[5]
+        grid, si = workload(seed=seed, rank=rank, world=world, n=n)
+        o = OL.Oracle(grid, OL.RNG_LINEAGE, flavor)
+    rc = o.step(si)
+    t = o.tallies()
+    o.close()
+    if rc != 0:
+        raise RuntimeError("oracle run %r failed: %d" % (args, rc))
+    return t
+
+
+def summary(tallies, nz=2, nr=2, nmu=1):
+    """(F(E), edout, counters) of a tally vector."""
+    t = abi.split_tallies(np.asarray(tallies), nz, nr, nmu)
+    return S.f_of_e(t["fout"]), np.asarray(t["edout"]).ravel()[:5].copy(), np.asarray(t["counters"])

@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 TALLY_KEYS = ("edep", "prdep", "ecens", "npcen", "n_field", "E_IC", "nelectron", "fout", "edout",
               "erlki", "erlko", "erlku", "erlkl", "Ed_in")
 COUNTERS = (abi.CNT_STEPS, abi.CNT_ESCAPES, abi.CNT_CENSUS, abi.CNT_COLLIDE, abi.CNT_KILLED,
-            abi.CNT_SOURCES, abi.CNT_COMPB, abi.CNT_EVENTS)
+            abi.CNT_SOURCES, abi.CNT_COMPB, abi.CNT_EVENTS, abi.CNT_ESC_SCAT)
 
 
 def sort_rows(a):
@@ -86,6 +86,22 @@ def test_fast_kernel_close_to_oracle(name):
         # the fast build's point loop uses a series for -log(1-x) and v_rsq_f64
         a, b = np.asarray(tg["prdep"]), np.asarray(to["prdep"])
         assert np.sum(np.abs(a - b)) <= 1e-3 * max(np.sum(np.abs(b)), 1e-300), (name, n, "prdep")
+        # every other tally the FP solve and the host driver read: the photon
+        # field, the Compton tallies and the boundary leaks, as totals and
+        # per cell (relative L2 over the cells; n_field per cell over its 400 bins)
+        for k in ("n_field", "E_IC", "nelectron", "erlki", "erlkl", "Ed_in", "erlko", "erlku"):
+            a, b = np.sum(tg[k]), np.sum(to[k])
+            assert abs(a - b) <= 1e-3 * max(abs(b), 1e-300) + (1e-300 if b == 0 else 0), (name, n, k, a, b)
+        for k in ("edep", "ecens", "npcen", "n_field", "E_IC", "nelectron"):
+            a, b = np.asarray(tg[k], float).ravel(), np.asarray(to[k], float).ravel()
+            nb = np.linalg.norm(b)
+            assert np.linalg.norm(a - b) <= 1e-3 * nb + (0.0 if nb > 0 else 1e-300), (name, n, k)
+        nfg, nfo = np.asarray(tg["n_field"]), np.asarray(to["n_field"])
+        for j in range(nfo.shape[0]):
+            for kk in range(nfo.shape[1]):
+                nb = np.linalg.norm(nfo[j, kk])
+                assert np.linalg.norm(nfg[j, kk] - nfo[j, kk]) <= 1e-3 * nb + (0.0 if nb > 0 else 1e-300), \
+                    (name, n, "n_field cell", j, kk)
 
 
 @pytest.mark.parametrize("fn,lo,hi", [(0, 1e-300, 1e300), (1, -700.0, 700.0), (2, -7.0, 14.0),
