@@ -49,9 +49,10 @@ def workload(mode=abi.COMTOT_EXACT, seed=LINEAGE_SEED, rank=0, world=1, n=IDENT_
              queue_capacity=None):
     grid, si = S.workload(mode=mode, seed=seed, rank=rank, world=world, n=n, device=device)
     si.n_e = si.n_e * N_E_FACTOR
-    # collisions: ~0.15 per source, split3 records a fraction of that
+    # collisions: ~0.15 per source; a generation can hold ~1.3 third-split records
+    # per collision (split2 = 10 copies, gains above 1000 are common)
     per = int(np.ceil(n / world))
-    grid.queue_capacity = queue_capacity or max(1 << 20, per // 2)
+    grid.queue_capacity = queue_capacity or max(1 << 20, 4 * per)
     grid.census_capacity = max(grid.census_capacity, per // 2 + 4096)
     grid.event_capacity = max(grid.event_capacity, 8 * per + 4096)
     return grid, si

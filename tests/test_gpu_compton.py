@@ -80,12 +80,15 @@ def test_fast_kernel_compton_identical_seeds():
     print("\nCompton, fast kernel vs the CPU reference path on identical seeds (%d collisions, "
           "%d scattered escapes): %s" % (co[abi.CNT_COLLIDE], co[abi.CNT_ESC_SCAT],
                                          {k: "%.2e" % v for k, v in report.items()}))
-    assert report["F_compton"] <= 1e-2 and report["F_all"] <= 1e-2
+    # the north-star bound is 1 %; per-history agreement leaves ~1e-6 (r03b:
+    # F_compton 6.6e-7, bands <= 4.8e-6, n_field 1.1e-6, npcen 1.9e-4), so the
+    # test holds the kernel to 1e-3
+    assert report["F_compton"] <= 1e-3 and report["F_all"] <= 1e-3
     for i in CC.COMPTON_BANDS:
-        assert report["band%d" % i] <= 1e-2, (i, report["band%d" % i])
+        assert report["band%d" % i] <= 1e-3, (i, report["band%d" % i])
     for k in ("edep", "ecens", "npcen", "prdep", "n_field", "n_field_cell_max", "E_IC", "nelectron",
               "erlko", "erlku"):
-        assert report[k] <= 1e-2, (k, report[k])
+        assert report[k] <= 1e-3, (k, report[k])
 
 
 def test_exact_kernel_compton_counters_bitwise():
