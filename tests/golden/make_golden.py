@@ -49,6 +49,16 @@ CASES = {
     # so the driver hands each 200 of weight erinu/200 (c2d_refdrv NFORCEU)
     "bb_upper": dict(case=dict(nz=2, nr=2, n_e=2.0e6, nst=1000, tbbu=[2.0e-3, 5.0e-2]),
                      nsteps=2, nforceu=200),
+    # BASELINE C1: ONE zone, the inputm.dat medium, the EC
+    # seed spectrum disk/blackbody_20110929.in on the lower ring (tbbl = -1,
+    # the NaN-free file, H9); every flight ends at a system edge or census
+    # (src/imctrk2d.f:276-360 with nz = nr = 1).  The EC window is kept open
+    # (t0 = 0, t1 = 1e30) so the surface source runs every step.
+    "c1_ec1x1": dict(case=dict(nz=1, nr=1, n_e=80.0, nst=20000, tbbl=-1.0), nsteps=3),
+    # BASELINE C2: the 32x32 (r,z) grid of the inputm.dat medium, FP off: the
+    # 1024-cell indexing, the cell tallies beyond the LDS-privatised size and
+    # the n_field of 1024 cells
+    "c2_32x32": dict(case=dict(nz=32, nr=32, n_e=80.0, nst=200000), nsteps=2),
 }
 
 # C3: the Mrk 421 SSC deck src_20121026/input.dat:1-130 +

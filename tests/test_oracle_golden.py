@@ -80,3 +80,9 @@ def test_golden_cases_exercise_every_branch():
     c3 = GoldenCase("c3_mrk421")                       # the C3 deck, FP on
     assert (c3.nz, c3.nr) == (30, 9) and c3.meta["pair_switch"] == 1 and c3.meta["T_const"] == 0
     assert c3.meta["fp_steps"] == [1, 2]
+    c1 = GoldenCase("c1_ec1x1")                        # BASELINE C1: one zone, EC lower ring
+    assert (c1.nz, c1.nr) == (1, 1) and c1.a["in1_nsurfl"].sum() > 0 and c1.meta["step1"]["nfile"] >= 2
+    assert len(c1.out(2, "events")) > 1000 and c1.out(2, "census_d").shape[0] > 1000
+    c2 = GoldenCase("c2_32x32")                        # BASELINE C2: 32x32, every cell visited
+    assert (c2.nz, c2.nr) == (32, 32)
+    assert (c2.out(0, "edep") > 0).all() and (c2.out(1, "n_field").sum(axis=-1) > 0).sum() >= 1020
