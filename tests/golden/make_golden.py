@@ -56,8 +56,8 @@ CASES = {
     # (t0 = 0, t1 = 1e30) so the surface source runs every step.
     "c1_ec1x1": dict(case=dict(nz=1, nr=1, n_e=80.0, nst=20000, tbbl=-1.0), nsteps=3),
     # BASELINE C2: the 32x32 (r,z) grid of the inputm.dat medium, FP off: the
-    # 1024-cell indexing, the cell tallies beyond the LDS-privatised size and
-    # the n_field of 1024 cells
+    # 1024-cell indexing, LDS-privatised tallies of 1024 cells (32 KB) and the
+    # n_field of 1024 cells; nst = 2e5 so every cell is visited
     "c2_32x32": dict(case=dict(nz=32, nr=32, n_e=80.0, nst=200000), nsteps=2),
 }
 
