@@ -29,10 +29,12 @@ dominant kernel (generation-0 transport launch) at 160 algorithmic bytes
 pass through the geometry block that a probe bundle shares among its copies,
 and carries its measured HBM bytes and VALU-issue fraction from the committed
 PMC profile of the same command; `kernels` reports the FP and table kernels beside it;
-`cpu_baseline` times the C oracle (a port of the reference's algorithm) on
-the host's CPU share, on a strided sample of the GPU's own final census plus
-the same fraction of the step's volume sources, and the FP_calc of sampled
-zones, extrapolated to one whole coupled step.
+`cpu_baseline` times the reference's algorithm (the C oracle in its
+reference mode: per-copy probes, lagged-Fibonacci streams with the
+per-census-packet reseed, bit-exact to the Fortran) on the host's CPU share,
+on a strided sample of the GPU's own final census plus the same fraction of
+the step's volume sources, and the FP_calc of sampled zones, extrapolated to
+one whole coupled step.
 """
 from __future__ import annotations
 
@@ -53,8 +55,15 @@ BYTES_PER_STEP = 160.0          # 80 B packet record in + out
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s
 N_SIMD = 1024                   # 256 CUs x 4 SIMDs
 CLOCK_HZ = 2.4e9                # MI355X peak engine clock
-CENSUS_BYTES = 2 * 64           # in + out census SoA record (c2d_device.hpp CensusSoA)
-DEFAULT_SOURCES = {"c3": 100_000_000, "c2": 10_000_000, "c4": 125_000_000}
+CENSUS_BYTES = 64 * (1 + 1 / 16)  # in-place census SoA record + the append slack (capi.cpp cens_phys)
+DEFAULT_SOURCES = {"c3": 100_000_000, "c2": 10_000_000, "c4": 125_000_000, "c5": 20_000_000}
+# untimed census spin-up (steps before the warm-up): a C3 source stays in the
+# census ~16 steps (tools/c3_bench.py: the census saturates at 15.8 records
+# per source of a step after ~40 steps, profiles/r03a), so the timed steps
+# see the steady-state census of a long run instead of its growth
+SPINUP = {"c3": 40, "c4": 0, "c2": 0, "c5": 0}
+# census records per source of a step the capacity is sized for
+CENSUS_PER_SOURCE = {"c3": 20.0, "c4": 40.0, "c2": 40.0, "c5": 8.0}
 
 
 def cpu_share() -> tuple[int, int]:
@@ -69,19 +78,28 @@ def cpu_share() -> tuple[int, int]:
 
 
 def _cpu_transport(args):
-    """One host core: the C oracle (glibc, exact comtot, lineage RNG) on its
-    shard of the sampled step (census records + volume sources)."""
+    """One host core = one reference worker: the C oracle in its reference
+    mode (glibc libm, exact comtot, per-copy split1 probes, the reference's
+    lagged-Fibonacci streams with the per-census-packet reseed of
+    src/imcfield2d.f:115-116) on its share of the sampled step: every
+    world-th census record and the volume zones j*nr+k = rank (mod world),
+    as the reference's master hands zone jobs to its workers."""
+    import dataclasses
     rank, world, grid_kw, si, cens = args
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib as OL
     from compton2d_amd import abi
     g = abi.GridConfig(**grid_kw)
-    g.rank, g.world, g.comtot_mode = rank, world, abi.COMTOT_EXACT
-    o = OL.Oracle(g, OL.RNG_LINEAGE, "ref")
+    g.rank, g.world, g.comtot_mode = 0, 1, abi.COMTOT_EXACT
+    o = OL.Oracle(g, OL.RNG_FIB, "ref", rseed=9857 + 7919 * rank)
     d6, i5, keys = cens
-    o.import_census(d6[rank::world], i5[rank::world], keys[rank::world])
+    # census seeds: the reference stores int(fibran()*1e5) (imctrk2d.f:571, hazard H5)
+    o.import_census(d6[rank::world], i5[rank::world], (keys[rank::world] % 100000).astype(np.uint64))
+    nsv = np.asarray(si.nsv).copy()
+    cells = np.arange(nsv.size).reshape(nsv.shape)
+    nsv[cells % world != rank] = 0
     t0 = time.perf_counter()
-    rc = o.step(si)
+    rc = o.step(dataclasses.replace(si, nsv=nsv))
     dt = time.perf_counter() - t0
     L = abi.tally_layout(g.nz, g.nr, int(np.asarray(g.mu).size))
     steps = float(o.tallies()[L["counters"][0] + abi.CNT_STEPS])
@@ -100,10 +118,10 @@ def _cpu_fp(args):
 
 
 def cpu_baseline(eng, run, target_s: float = 12.0) -> dict:
-    """The reference algorithm on the host (oracle, `kind: port`) over a
-    bounded sample of the next coupled step of this run: a strided sample of
-    the GPU's census and the same fraction of the step's volume sources,
-    plus FP_calc of sampled zones."""
+    """The reference algorithm on the host (the C oracle in its reference
+    mode, `kind: port`) over a bounded sample of the next coupled step of
+    this run: a strided sample of the GPU's census and the same fraction of
+    the step's volume sources, plus FP_calc of sampled zones."""
     import multiprocessing as mp
     from dataclasses import asdict
     sys.path.insert(0, str(ROOT / "tests"))
@@ -148,14 +166,20 @@ def cpu_baseline(eng, run, target_s: float = 12.0) -> dict:
     step_s = tr_s * stride + fp_s_zone * ncell / cores
     cpu_steps = tr_steps * stride                # the whole step's packet-steps on the CPU
     return {"value": cpu_steps / step_s, "unit": "packet-steps/s", "cores": cores, "kind": "port",
+            "algorithm": "reference (per-copy split1 probes, lagged-Fibonacci streams reseeded per "
+                         "census packet, exact comtot, glibc libm)",
             "sample": ("the C3 step after this run's last timed step: every %d-th census record "
-                       "the GPU left (%d of %d) + 1/%d of the step's volume sources, lineage-sharded "
-                       "over %d processes (host nproc %d, CPU share %d); C oracle = port of the "
-                       "reference algorithm (exact 199-term comtot, glibc libm, lineage RNG): %.0f "
+                       "the GPU left (%d of %d) + 1/%d of the step's volume sources, over %d "
+                       "processes = reference workers (census records strided, volume zones "
+                       "j*nr+k mod %d; host nproc %d, CPU share %d); C oracle in its reference mode "
+                       "= the reference's algorithm as the Fortran runs it (per-copy split1 probes, "
+                       "no bundles; rand_switch=1 lagged-Fibonacci zone streams and the 10000-number "
+                       "reseed per census packet, src/imcfield2d.f:115-116; exact 199-term comtot; "
+                       "glibc libm; bit-exact to the Fortran in tests/test_oracle_golden.py): %.0f "
                        "packet-steps in %.2f s; FP_calc of %d zones at %.2f s/zone; whole coupled "
                        "step extrapolated = %.2f s x %d + %.2f s/zone x %d zones / %d cores = %.1f s "
                        "for %.3g packet-steps (pool wall %.1f s)"
-                       % (stride, len(cens[2]), n_cens, stride, cores, nproc, cores, tr_steps,
+                       % (stride, len(cens[2]), n_cens, stride, cores, cores, nproc, cores, tr_steps,
                           tr_s, nfp, fp_s_zone, tr_s, stride, fp_s_zone, ncell, cores, step_s,
                           cpu_steps, wall))}
 
@@ -175,12 +199,159 @@ def load_pmc(workload_key: str):
         return {}
 
 
-def build_c2(args, rank, world, local, total_steps, sources, grid_n, ccap, ecap):
-    from compton2d_amd import abi, synth
-    mode = abi.COMTOT_TABLE if args.mode == "fast" else abi.COMTOT_EXACT
-    return synth.c2_workload(nz=grid_n, nr=grid_n, sources=sources * world, comtot_mode=mode,
-                             rank=rank, world=world, device=local, census_capacity=ccap,
-                             event_capacity=ecap)
+def census_capacity(sources: int, per_source: float, free: float, side: float) -> int:
+    """Census records the run may hold: per_source x sources, within 85 % of
+    the free HBM beside the event and packet buffers (in-place census at 64 B
+    per record + its append slack, capi.cpp cens_phys)."""
+    return int(min(per_source * sources + (1 << 20), max(1 << 20, (0.85 * free - side) / CENSUS_BYTES)))
+
+
+def tally_exchange(eng, T, rank, world, dev):
+    """The per-step tally all-reduce of an N-rank run (xec_add / cens_add_up):
+    by default RCCL inside the C-ABI (c2d_comm_init + c2d_allreduce_tallies on
+    the library's stream, the Fortran host's path); `C2D_TALLY_EXCHANGE=torch`
+    or a gloo process group (the one-GPU rehearsal) use torch.distributed."""
+    from compton2d_amd import abi, distributed
+    if world == 1:
+        return None, "none (1 rank)"
+    import torch.distributed as dist
+    if dist.get_backend() == "nccl" and os.environ.get("C2D_TALLY_EXCHANGE", "cabi") == "cabi":
+        obj = [eng.comm_unique_id() if rank == 0 else bytes(abi.COMM_ID_BYTES)]
+        dist.broadcast_object_list(obj, src=0, device=dev)
+        eng.comm_init(obj[0], rank, world)
+        return eng.allreduce_tallies, "RCCL all-reduce inside the C-ABI (c2d_allreduce_tallies)"
+    return (lambda: distributed.allreduce_tallies(T)), \
+        "torch.distributed all-reduce (%s)" % dist.get_backend()
+
+
+def transport_row(eng, T, cnt0):
+    """Per-step counters and kernel times of a transport-only step (after the
+    tally exchange: the counters are global)."""
+    from compton2d_amd import abi
+    c = T[cnt0:cnt0 + abi.NCOUNTERS].cpu().numpy()
+    g0, al, _ = eng.last_kernel_ms()
+    g0p, allp = eng.last_path_steps()
+    return dict(packet_steps=float(c[abi.CNT_STEPS]), sources=float(c[abi.CNT_SOURCES]),
+                census=float(c[abi.CNT_CENSUS]), escapes=float(c[abi.CNT_ESCAPES]),
+                aborted=float(c[abi.CNT_ABORTED]), transport_gen0_ms=g0, transport_all_ms=al,
+                gen0_steps=float(eng.last_gen0_steps()), gen0_paths=float(g0p),
+                all_paths=float(allp), census_records=float(eng.census_count()))
+
+
+def build_c3(args, rank, world, local, dev, sources, ccap, ecap, mode):
+    import torch
+    from compton2d_amd import synth
+    from compton2d_amd.coupled import CoupledRun
+    from compton2d_amd.engine import Engine
+    wl = synth.c3_workload(sources=sources * world, comtot_mode=mode, rank=rank, world=world,
+                           device=local, census_capacity=ccap, event_capacity=ecap)
+    eng = Engine(wl.grid)
+    T = torch.zeros(eng.layout.total, dtype=torch.float64, device=dev)
+    eng.use_tally_tensor(T)
+    ex, ex_desc = tally_exchange(eng, T, rank, world, dev)
+    run = CoupledRun(eng, wl, device_resident=not args.host_tables, allreduce=ex)
+
+    def one_step():
+        r = dict(run.step())
+        r["census_records"] = float(eng.census_count())
+        return r
+    return eng, run, one_step, wl, wl.description, ex_desc
+
+
+def build_c2(args, rank, world, local, dev, sources, ccap, ecap, mode):
+    """C2 (32x32, 1e7/step, FP off) and C4 (C2's medium at 1.25e8 per GPU)."""
+    import torch
+    from compton2d_amd import synth
+    from compton2d_amd.engine import Engine
+    wl = synth.c2_workload(nz=args.grid, nr=args.grid, sources=sources * world, comtot_mode=mode,
+                           rank=rank, world=world, device=local, census_capacity=ccap,
+                           event_capacity=ecap)
+    eng = Engine(wl.grid)
+    T = torch.zeros(eng.layout.total, dtype=torch.float64, device=dev)
+    eng.use_tally_tensor(T)
+    ex, ex_desc = tally_exchange(eng, T, rank, world, dev)
+    eng.set_step(wl.step0)
+    state = {"n": 0}
+    cnt0 = eng.layout.counters
+
+    def one_step():
+        ncycle, t = wl.clock(state["n"])
+        eng.set_clock(ncycle, t, wl.dt)
+        eng.run_step()
+        if ex is not None:
+            ex()
+        state["n"] += 1
+        return transport_row(eng, T, cnt0)
+    desc = wl.description
+    if args.workload == "c4":
+        desc = ("C4: C2's medium (%dx%d, inputm.dat, FP off) at %d volume packets/step per GPU, "
+                "lineage-sharded over %d rank(s) (%d per step in all; BASELINE configs[3] is 1e9 "
+                "on 8 GPUs), tallies all-reduced every step" % (args.grid, args.grid, sources, world,
+                                                              sources * world))
+    return eng, None, one_step, wl, desc, ex_desc
+
+
+def build_c5(args, rank, world, local, dev, sources, ccap, ecap, mode):
+    """C5 (BASELINE configs[4]): the external-Compton BLR light-curve run of
+    tools/c5_bench.py as a bench workload.  Every step: host budgets (file_sp
+    + the lower-ring EC budget, imcsurf2d_para.f:544-685, imcgen2d.f:111-120,
+    174-183), census + volume + surface transport on the GPU, the tally
+    exchange, and the observer-frame light curves of the step's escapes
+    binned on the device (postprocessing/plcm.c:382-456, ext25_lc.input)."""
+    import torch
+    from compton2d_amd import surface, synth
+    from compton2d_amd.engine import Engine
+    sys.path.insert(0, str(ROOT / "tools"))
+    import c5_bench as C5
+    nz = nr = args.grid_c5
+    nst = sources * world
+    g_bulk, zmax, rmax, rmin = 25.0, 1.0e17, 1.0e17, 0.0
+    wl = synth.c2_workload(nz=nz, nr=nr, sources=nst, comtot_mode=mode, rank=rank, world=world,
+                           device=local, census_capacity=ccap, event_capacity=ecap)
+    z, r, vol, zs = synth.zone_geometry(nz, nr, zmax, rmin, rmax)
+    wl.grid.z, wl.grid.r = z, r
+    dt = min(r[-1] / nr, z[-1] / nz) / (np.sqrt(1.0 - 1.0 / g_bulk ** 2) * synth.C_LIGHT)
+    med = np.load(synth.DATA, allow_pickle=False)
+    fas = med["emiss_per_vol_per_s"] * vol * dt
+    nsv = (0.5 * nst * fas / fas.sum()).astype(np.int64)            # imcgen2d.f:446
+    ewsv = np.where(nsv > 0, fas / np.maximum(nsv, 1), 0.0)
+    tab, int_file = surface.file_sp(surface.seed_spectrum("blackbody_G25_4spectra"),
+                                    surface.EcConstants(g_bulk=g_bulk))
+    eng = Engine(wl.grid)
+    T = torch.zeros(eng.layout.total, dtype=torch.float64, device=dev)
+    eng.use_tally_tensor(T)
+    ex, ex_desc = tally_exchange(eng, T, rank, world, dev)
+    eng.obs_begin(C5.ext25_binning())
+    cnt0 = eng.layout.counters
+    state = {"n": 0}
+
+    def one_step():
+        n = state["n"]
+        ncycle, t = n, max(n - 1, 0) * dt
+        w = surface.time_window(ncycle, t, dt, C5.T1)
+        ec_on = w < len(C5.T0) and (t + 0.5 * dt) >= C5.T0[w]
+        tbbl = np.full(nr, -1.0) if w == 0 else np.zeros(nr)
+        nsurfl, ewsurfl = surface.lower_surface_budget(r, rmin, nst, dt, tbbl, ec_on, int_file)
+        si = wl.step0
+        si.ncycle, si.time, si.dt = ncycle, t, dt
+        si.zsurf, si.Eloss_tot, si.Eloss_th = zs, fas, fas * float(med["Eloss_th_frac"])
+        si.nsv, si.ewsv = nsv.astype(np.int32), ewsv
+        si.nsurfl, si.ewsurfl, si.tbbl = nsurfl, ewsurfl, tbbl
+        si.spectra = [tab]
+        surface.apply_bias(nst, si)
+        eng.transport_step(si)
+        if ex is not None:
+            ex()
+        eng.obs_accumulate(None)
+        state["n"] += 1
+        row = transport_row(eng, T, cnt0)
+        row["surface_sources"] = float(nsurfl.sum())
+        return row
+    desc = ("C5: EC/BLR light curve, %dx%d grid, z_max=r_max=1e17 cm, Gamma 25, "
+            "disk/blackbody_G25_4spectra.in on all %d lower rings (EC window t < 4e5 s), nst=%d per "
+            "GPU (nst surface + nst/2 volume packets), %d rank(s), ext25_lc light curves binned on "
+            "the device every step" % (nz, nr, nr, sources, world))
+    return eng, None, one_step, wl, desc, ex_desc
 
 
 def main():
@@ -188,9 +359,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("c3", "c2", "c4"), default="c3")
-    ap.add_argument("--sources", type=int, default=None, help="volume packets/step/GPU")
+    ap.add_argument("--workload", choices=("c3", "c2", "c4", "c5"), default=None,
+                    help="default: c3 on one GPU, c4 (BASELINE configs[3]) on N > 1")
+    ap.add_argument("--sources", type=int, default=None, help="volume packets/step/GPU (c5: nst/GPU)")
+    ap.add_argument("--spinup", type=int, default=None,
+                    help="untimed steps before the warm-up that bring the census to its steady "
+                         "state (default: c3 %d, c4 %d, else 0)" % (SPINUP["c3"], SPINUP["c4"]))
     ap.add_argument("--grid", type=int, default=32, help="c2/c4 grid (NxN)")
+    ap.add_argument("--grid-c5", type=int, default=16, help="c5 grid (NxN)")
     ap.add_argument("--mode", choices=("fast", "exact"), default="fast")
     ap.add_argument("--host-tables", action="store_true",
                     help="c3: move tables/electrons through host arrays every step")
@@ -199,9 +375,7 @@ def main():
     args = ap.parse_args()
 
     import torch
-    from compton2d_amd import abi, distributed, synth
-    from compton2d_amd.coupled import CoupledRun
-    from compton2d_amd.engine import Engine
+    from compton2d_amd import abi, distributed
 
     rank, world, local = distributed.init()
     if world != args.gpus and world > 1:
@@ -211,54 +385,26 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    wk = args.workload
+    wk = args.workload or ("c3" if world == 1 else "c4")
+    args.workload = wk
     sources = args.sources or DEFAULT_SOURCES[wk]
-    total_steps = args.warmup + args.steps
-    # census SoA in + out: as many records as the run can create, within ~70 %
-    # of the free HBM (288 GB per MI355X); events and the packet store beside it
+    spinup = SPINUP.get(wk, 0) if args.spinup is None else args.spinup
+    total_steps = spinup + args.warmup + args.steps
     free, _ = torch.cuda.mem_get_info(dev)
-    ecap = int(2 * sources) + (1 << 20)
-    side = ecap * 56 + sources * 80 + (4 << 30)
-    ccap = int(min((total_steps + 1) * sources * 1.1 + (1 << 20),
-                   max(1 << 20, (0.85 * free - side) / CENSUS_BYTES)))
     mode = abi.COMTOT_TABLE if args.mode == "fast" else abi.COMTOT_EXACT
-    T = None
-    if wk == "c3":
-        wl = synth.c3_workload(sources=sources * world, comtot_mode=mode, rank=rank, world=world,
-                               device=local, census_capacity=ccap, event_capacity=ecap)
-        eng = Engine(wl.grid)
-        T = torch.zeros(eng.layout.total, dtype=torch.float64, device=dev)
-        eng.use_tally_tensor(T)
-        run = CoupledRun(eng, wl, device_resident=not args.host_tables,
-                         allreduce=(lambda: distributed.allreduce_tallies(T)) if world > 1 else None)
-        one_step = run.step
-        desc = wl.description
-    else:
-        grid_n = args.grid
-        wl = build_c2(args, rank, world, local, total_steps, sources, grid_n, ccap, ecap)
-        eng = Engine(wl.grid)
-        T = torch.zeros(eng.layout.total, dtype=torch.float64, device=dev)
-        eng.use_tally_tensor(T)
-        eng.set_step(wl.step0)
-        state = {"n": 0}
-        cnt0 = eng.layout.counters
+    per_gpu_items = sources * (1.5 if wk == "c5" else 1.0)
+    ecap = int(2 * per_gpu_items) + (1 << 20)
+    side = ecap * 56 + per_gpu_items * 80 + (4 << 30)
+    ccap = census_capacity(int(per_gpu_items), min(CENSUS_PER_SOURCE[wk], total_steps + 1), free, side)
+    build = {"c3": build_c3, "c2": build_c2, "c4": build_c2, "c5": build_c5}[wk]
+    eng, run, one_step, wl, desc, ex_desc = build(args, rank, world, local, dev, sources, ccap, ecap,
+                                                  mode)
 
-        def one_step():
-            ncycle, t = wl.clock(state["n"])
-            eng.set_clock(ncycle, t, wl.dt)
-            eng.run_step()
-            distributed.allreduce_tallies(T)
-            state["n"] += 1
-            c = T[cnt0:cnt0 + abi.NCOUNTERS].cpu().numpy()
-            g0, al, _ = eng.last_kernel_ms()
-            return dict(packet_steps=float(c[abi.CNT_STEPS]), sources=float(c[abi.CNT_SOURCES]),
-                        census=float(c[abi.CNT_CENSUS]), escapes=float(c[abi.CNT_ESCAPES]),
-                        aborted=float(c[abi.CNT_ABORTED]), transport_gen0_ms=g0,
-                        transport_all_ms=al, gen0_steps=float(eng.last_gen0_steps()),
-                        gen0_paths=float(eng.last_path_steps()[0]),
-                        all_paths=float(eng.last_path_steps()[1]))
-        desc = wl.description.replace("C2:", "C4 (C2 medium, per GPU):") if wk == "c4" else wl.description
-
+    t_spin = time.perf_counter()
+    for _ in range(spinup):
+        one_step()
+    t_spin = time.perf_counter() - t_spin
+    census_start = eng.census_count()
     for _ in range(args.warmup):
         one_step()
     distributed.barrier(dev)
@@ -273,12 +419,12 @@ def main():
     elapsed = distributed.allreduce_max(elapsed, dev)
     # packet-steps of all ranks: the counters were all-reduced with the tallies
     steps_global = sum(r["packet_steps"] for r in rows)
-    if world > 1 and wk == "c3":
-        pass   # CoupledRun reads the counters after its all-reduce hook: already global
+    census_timed_start = rows[0]["census_records"] if rows else census_start
     if rank != 0:
         eng.close()
         return
     g0_ms = sum(r["transport_gen0_ms"] for r in rows)
+    # this rank's own generation-0 work (its kernel time is this rank's)
     g0_steps = sum(r["gen0_steps"] for r in rows)
     g0_paths = sum(r["gen0_paths"] for r in rows)
     value = steps_global / elapsed
@@ -291,7 +437,8 @@ def main():
     g0_s = g0_ms * 1e-3
     achieved = g0_paths * BYTES_PER_STEP / g0_s / 1e9 if g0_ms > 0 else 0.0
     survey_frac = (g0_steps * BYTES_PER_STEP / g0_s / 1e9 / HBM_PEAK_GBS) if g0_ms > 0 else 0.0
-    grid_txt = "30x9" if wk == "c3" else "%dx%d" % (args.grid, args.grid)
+    grid_txt = {"c3": "30x9", "c5": "%dx%d" % (args.grid_c5, args.grid_c5)}.get(
+        wk, "%dx%d" % (args.grid, args.grid))
     workload_key = "%s_%s_%d_%s" % (wk, grid_txt, sources, args.mode)
     pmc = load_pmc(workload_key)
     bpp = pmc.get("hbm_bytes_per_path")
@@ -326,6 +473,7 @@ def main():
                          "valu_issue_frac": pmc.get("fp_valu_issue_frac"),
                          "wait_frac": pmc.get("fp_wait_frac")}
         kernels["volume_em"] = {"ms_avg": per_step.get("vem_kernel_ms", 0.0), "zones": ncell}
+    rounds, moved, phys = eng.last_compaction()
     out = {
         "metric": METRIC,
         "value": value,
@@ -338,11 +486,14 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": ("synthetic: the reference's P_nontherm electrons of the inputm.dat medium in every "
-                 "zone, tables recomputed on the device every step from the evolving electrons; "
-                 "volume packets sampled on device" if wk == "c3" else
-                 "synthetic: reference volume_em/P_nontherm tables of the inputm.dat medium tiled "
-                 "over the grid; volume packets sampled on device"),
+        "data": {"c3": "synthetic: the reference's P_nontherm electrons of the inputm.dat medium in "
+                       "every zone, tables recomputed on the device every step from the evolving "
+                       "electrons; volume packets sampled on device",
+                 "c5": "synthetic: reference volume_em/P_nontherm tables of the inputm.dat medium "
+                       "tiled over the grid, the reference's blackbody_G25_4spectra.in seed file on "
+                       "the lower rings; volume and surface packets sampled on device"}.get(
+            wk, "synthetic: reference volume_em/P_nontherm tables of the inputm.dat medium tiled "
+                "over the grid; volume packets sampled on device"),
         "config": {
             "workload": desc,
             "grid": grid_txt,
@@ -353,8 +504,15 @@ def main():
             "arithmetic": "f64 throughout (comtot table stored in f64)",
             "tables": ("device-resident (C2D_DEV_EMISSION | C2D_DEV_ELECTRONS)"
                        if wk == "c3" and not args.host_tables else "host arrays"),
-            "parallelism": "lineage-sharded sources, %d rank(s), RCCL all-reduce of tallies" % world,
-            "census_capacity_per_gpu": ccap,
+            "parallelism": "lineage-sharded sources, %d rank(s), no data-path collective" % world,
+            "tally_exchange": ex_desc,
+            "census": {"spinup_steps": spinup, "spinup_s": t_spin,
+                       "records_after_spinup": census_start,
+                       "records_at_timed_start": census_timed_start,
+                       "records_at_end": eng.census_count(),
+                       "capacity_per_gpu": ccap, "physical_slots": phys,
+                       "bytes_per_record": 64, "layout": "in-place SoA (c2d_device.hpp C2D_CENS_DEAD)",
+                       "last_compaction_rounds": rounds, "last_compaction_moved": moved},
             "packet_steps_timed": steps_global,
             "per_step": per_step,
         },

@@ -51,6 +51,15 @@ struct SpecDev {             /* file_sp table (imcsurf2d_para.f:544-685) */
  * with the same c2d_acos / c2d_cos (c2d_census_export / _import), so the
  * records it sees are the ones the fast kernel wrote before this encoding. */
 #define C2D_CENS_ESW (1u << 24)
+/* In-place census (one SoA per context, read and written by the same step):
+ * the census packets of the previous step are the step's first items
+ * [0, n_cin); the recombined copy of census item i writes its next-step
+ * record back into slot i, every other census write appends at or after
+ * n_cin.  A census item that ends without a census write, and the unused
+ * tail of a wave's append chunk, are marked dead (bins = C2D_CENS_DEAD); the
+ * host closes the dead slots below the live count after the step
+ * (capi.cpp census_compact), so the census stays dense at 64 B per record. */
+#define C2D_CENS_DEAD (1u << 31)
 struct CensusSoA {
   double* rpre; double* zpre; double* wmu; double* phi; double* ew; double* xnu;
   uint32_t* jk;      /* jph << 16 | kph (1-based)                  */
@@ -144,6 +153,9 @@ __device__ __forceinline__ void gor(int32_t* p, int32_t v) {
  * packet-step; the bundle kernel one per shared step of all copies on the
  * path.  The roofline's algorithmic bytes are priced on it. */
 #define C2D_CNT_PATHS_INT 10
+/* internal counter slot: census slots marked dead by the bundle kernel
+ * (census items that did not return to the census + unused chunk tails) */
+#define C2D_CNT_DEAD_INT 12
 
 struct KParams {
   int32_t nz, nr, ncell, nphtotal, nph_lc, nmu;
@@ -174,7 +186,8 @@ struct KParams {
                                    reference evaluates comtot; 16 KB per cell)               */
   double comtab_du_inv;
   double egg_min;            /* E_field(1)^2 / E_field(2): n_field threshold (imctrk2d.f:547-556) */
-  /* census */
+  /* census: cin and cout are the same in-place SoA (C2D_CENS_DEAD); cap_cout is
+   * its physical size (census_capacity + the slack the append chunks need) */
   CensusSoA cin, cout;
   int64_t n_cin, cap_cout;
   uint32_t cens_chunk;       /* census slots per wave reservation (bundle kernel) */
@@ -200,7 +213,6 @@ struct KParams {
   int32_t* err;
   int32_t lds_cells;        /* 1: cell tallies privatised in LDS */
   unsigned long long* prof;  /* [C2D_TR_PROF_WORDS] section counters (-DC2D_TR_PROF builds) */
-  unsigned long long* cens_holes; /* bundle kernel: per wave (start, length) of its census hole */
 };
 
 /* Per-launch arguments (passed by value; KParams stays constant over a step). */

@@ -38,7 +38,6 @@ extern "C" int c2d_launch_bundle_fast(const KParams* P, const GenArgs* A, int gr
                                       hipStream_t s);
 extern "C" int c2d_bundle_occupancy_exact(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_bundle_occupancy_fast(int* blocks_per_cu, size_t lds);
-extern "C" int c2d_launch_census_move(CensusSoA c, const long long* moves, int n, hipStream_t s);
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t s);
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
                                       double* tab, int ncell, hipStream_t s);
@@ -113,9 +112,16 @@ struct c2d_ctx {
   /* generation 0 as probe bundles (c2d_bundle_kernel): its LDS and grid */
   int bundle = 1, bundle_grid = 0;
   size_t bundle_lds = 0;
-  unsigned long long* cens_holes = nullptr;   /* [bundle waves][2]: census chunk tails */
-  long long* cens_moves = nullptr;            /* [2 * bundle waves][3]: src, dst, n     */
-  std::vector<unsigned long long> h_holes;
+  /* in-place census (c2d_device.hpp C2D_CENS_DEAD): one SoA of cens_phys
+   * records = census_capacity + the slack the bundle kernel's append chunks
+   * need; the compaction's work lists (cscan_cap slots each) */
+  int64_t cens_phys = 0;
+  uint32_t cens_chunk = 64;
+  int64_t* cscan = nullptr;      /* [2][cscan_cap]: dead slots below W, live slots at/above W */
+  unsigned long long* cscan_n = nullptr;   /* [2] list lengths */
+  int64_t cscan_cap = 0;
+  int last_compact_rounds = 0;
+  int64_t last_compact_moved = 0;
   c2d_tally_layout L;
   /* device buffers */
   Geo* geo = nullptr;
@@ -129,9 +135,8 @@ struct c2d_ctx {
   int n_spectra = 0;
   double* comtab = nullptr;
   double* comS = nullptr;
-  DevCensus cens[2];
-  int cur_out = 0;           /* census buffer written by the last step */
-  int64_t n_census = 0;      /* packets in cens[cur_out] */
+  DevCensus cens;            /* the in-place census */
+  int64_t n_census = 0;      /* live records: cens[0, n_census) */
   double* ev = nullptr;
   int64_t n_ev = 0;
   int64_t ev_cnt[C2D_EV_SHARDS] = {};   /* events in each shard of the buffer (last step) */
@@ -324,13 +329,6 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
     int rc = c2d_launch_comtab_sigma(c->gnt, c->comS, c->stream);
     if (rc) return fail(c, C2D_E_HIP, "comtab_sigma launch: %d", rc);
   }
-  const int64_t ccap = std::max<int64_t>(cfg->census_capacity, 1);
-  for (int b = 0; b < 2; b++) {
-    for (int f = 0; f < 6; f++) HIPCHK(c, dalloc(&c->cens[b].d[f], ccap));
-    HIPCHK(c, dalloc(&c->cens[b].jk, ccap));
-    HIPCHK(c, dalloc(&c->cens[b].bins, ccap));
-    HIPCHK(c, dalloc(&c->cens[b].key, ccap));
-  }
   HIPCHK(c, dalloc(&c->ev, (size_t)std::max<int64_t>(cfg->event_capacity, 1) * C2D_EVENT_WORDS));
   const int64_t qcap = std::max<int64_t>(cfg->queue_capacity, 1);
   for (int b = 0; b < 2; b++) {
@@ -365,10 +363,29 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
     if (orc) return fail(c, C2D_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)orc));
     c->bundle_lds = c->lds_bytes;
     c->bundle_grid = c->n_cu * std::max(1, b0);
-    const size_t waves = (size_t)c->bundle_grid * (C2D_TR_BLOCK / 64);
-    HIPCHK(c, dalloc(&c->cens_holes, 2 * waves));
-    HIPCHK(c, dalloc(&c->cens_moves, 6 * waves + 6));
-    c->h_holes.assign(2 * waves, 0ull);
+  }
+  {
+    /* the in-place census.  Append chunks per wave reservation: <= 1024
+     * slots, >= 64 (one reservation covers a wave's census lanes), and their
+     * tails (at most one per wave) at most 1/8 of the capacity.  The
+     * physical size adds room for every wave's chunk tail and 1/16 of the
+     * capacity for appends that land before the dead slots are closed, so a
+     * census whose compacted size fits the capacity never overflows. */
+    const int64_t ccap = std::max<int64_t>(cfg->census_capacity, 1);
+    const int64_t waves = (int64_t)c->bundle_grid * (C2D_TR_BLOCK / 64);
+    int64_t ch = 1024;
+    while (ch > 64 && ch * waves * 8 > ccap) ch >>= 1;
+    c->cens_chunk = (uint32_t)ch;
+    c->cens_phys = ccap + waves * ch + ccap / 16 + 64;
+    for (int f = 0; f < 6; f++) HIPCHK(c, dalloc(&c->cens.d[f], (size_t)c->cens_phys));
+    HIPCHK(c, dalloc(&c->cens.jk, (size_t)c->cens_phys));
+    HIPCHK(c, dalloc(&c->cens.bins, (size_t)c->cens_phys));
+    HIPCHK(c, dalloc(&c->cens.key, (size_t)c->cens_phys));
+    c->cscan_cap = std::min<int64_t>(int64_t(1) << 27, std::max<int64_t>(int64_t(1) << 16, ccap / 16));
+    /* test knob: a short work list forces many compaction rounds */
+    if (const char* e = getenv("C2D_COMPACT_LIST")) c->cscan_cap = std::max<long long>(1, atoll(e));
+    HIPCHK(c, dalloc(&c->cscan, 2 * (size_t)c->cscan_cap));
+    HIPCHK(c, dalloc(&c->cscan_n, 2));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return C2D_OK;
@@ -384,16 +401,14 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
                   c->Pnt, c->n_e, c->vfrac, c->ewsv, c->surf_ew, c->surf_tbb, c->tbbl,
                   c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comS,
                   c->ev, c->q2[0], c->q2[1], c->q3[0], c->q3[1], c->T_own, c->nf_rep, c->ctl, c->derr, c->dP,
-                  c->cens_holes, c->cens_moves};
+                  c->cscan, c->cscan_n};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  for (int b = 0; b < 2; b++) {
-    for (int f = 0; f < 6; f++)
-      if (c->cens[b].d[f]) (void)hipFree(c->cens[b].d[f]);
-    if (c->cens[b].jk) (void)hipFree(c->cens[b].jk);
-    if (c->cens[b].bins) (void)hipFree(c->cens[b].bins);
-    if (c->cens[b].key) (void)hipFree(c->cens[b].key);
-  }
+  for (int f = 0; f < 6; f++)
+    if (c->cens.d[f]) (void)hipFree(c->cens.d[f]);
+  if (c->cens.jk) (void)hipFree(c->cens.jk);
+  if (c->cens.bins) (void)hipFree(c->cens.bins);
+  if (c->cens.key) (void)hipFree(c->cens.key);
   for (double* p : c->spec_bufs) (void)hipFree(p);
   void* optrs[] = {c->obs_edges, c->obs_hist, c->obs_ev};
   for (void* p : optrs)
@@ -636,6 +651,82 @@ __global__ void __launch_bounds__(256) c2d_nf_reduce(const double* __restrict__ 
   }
 }
 
+/* In-place census compaction: W live records of the R slots [0, R); every
+ * dead slot below W takes a live record from [W, R).  c2d_census_scan lists
+ * both (wave-aggregated appends, at most cap each), c2d_census_fill moves
+ * the pairs; rounds repeat while dead slots below W remain. */
+__global__ void __launch_bounds__(256) c2d_census_scan(const uint32_t* __restrict__ bins, int64_t R,
+                                                       int64_t W, int64_t cap, int64_t* __restrict__ holes,
+                                                       int64_t* __restrict__ srcs,
+                                                       unsigned long long* __restrict__ n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const uint32_t lane = __lane_id();
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < R; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    bool hole = false, src = false;
+    if (i < R) {
+      const bool dead = (bins[i] & C2D_CENS_DEAD) != 0u;
+      hole = dead && i < W;
+      src = !dead && i >= W;
+    }
+    for (int l = 0; l < 2; l++) {
+      const bool mine = l == 0 ? hole : src;
+      const unsigned long long m = __ballot(mine);
+      if (m == 0ull) continue;
+      const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);
+      unsigned long long b = 0;
+      if (lane == leader) b = atomicAdd(n + l, (unsigned long long)__popcll(m));
+      b = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(b >> 32), leader) << 32) |
+          __builtin_amdgcn_readlane((uint32_t)b, leader);
+      const unsigned long long r = b + __popcll(m & ((1ull << lane) - 1ull));
+      if (mine && (int64_t)r < cap) (l == 0 ? holes : srcs)[r] = i;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) c2d_census_fill(CensusSoA c, const int64_t* __restrict__ holes,
+                                                       const int64_t* __restrict__ srcs, int64_t m) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < m;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t d = holes[t], s = srcs[t];
+    c.rpre[d] = c.rpre[s]; c.zpre[d] = c.zpre[s]; c.wmu[d] = c.wmu[s]; c.phi[d] = c.phi[s];
+    c.ew[d] = c.ew[s]; c.xnu[d] = c.xnu[s]; c.jk[d] = c.jk[s]; c.bins[d] = c.bins[s];
+    c.key[d] = c.key[s];
+    c.bins[s] = C2D_CENS_DEAD;          /* moved: the next round must not list it again */
+  }
+}
+
+static int census_compact(c2d_ctx* c, int64_t R, int64_t W) {
+  c->last_compact_rounds = 0;
+  c->last_compact_moved = 0;
+  if (W >= R) return C2D_OK;               /* no dead slot */
+  const CensusSoA cs = c->cens.soa();
+  int64_t* holes = c->cscan;
+  int64_t* srcs = c->cscan + c->cscan_cap;
+  for (int round = 0;; round++) {
+    HIPCHK(c, hipMemsetAsync(c->cscan_n, 0, 2 * sizeof(unsigned long long), c->stream));
+    const int grid = (int)std::min<int64_t>((R + 255) / 256, (int64_t)c->n_cu * 16);
+    hipLaunchKernelGGL(c2d_census_scan, dim3(grid), dim3(256), 0, c->stream, c->cens.bins, R, W,
+                       c->cscan_cap, holes, srcs, c->cscan_n);
+    HIPCHK(c, hipGetLastError());
+    unsigned long long nn[2];
+    HIPCHK(c, hipMemcpyAsync(nn, c->cscan_n, sizeof nn, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nn[0] != nn[1])
+      return fail(c, C2D_E_STATE, "census compaction: %llu dead slots below %lld, %llu live above",
+                  nn[0], (long long)W, nn[1]);
+    if (nn[0] == 0) break;
+    const int64_t m = std::min<int64_t>((int64_t)nn[0], c->cscan_cap);
+    const int fg = (int)std::min<int64_t>((m + 255) / 256, (int64_t)c->n_cu * 16);
+    hipLaunchKernelGGL(c2d_census_fill, dim3(fg), dim3(256), 0, c->stream, cs, holes, srcs, m);
+    HIPCHK(c, hipGetLastError());
+    c->last_compact_rounds = round + 1;
+    c->last_compact_moved += m;
+    if ((int64_t)nn[0] <= c->cscan_cap) break;
+  }
+  return C2D_OK;
+}
+
 extern "C" int c2d_run_step(c2d_ctx* c) {
   if (!c) return C2D_E_ARG;
   if (!c->have_step) return fail(c, C2D_E_STATE, "c2d_set_step must precede c2d_run_step");
@@ -659,20 +750,13 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.comtab = c->comtab;
   P.comtab_du_inv = (double)(C2D_COMTAB_N - 1) / (C2D_COMTAB_U1 - C2D_COMTAB_U0);
   P.egg_min = c->egg_min;
-  const int in_buf = c->cur_out, out_buf = 1 - c->cur_out;
-  P.cin = c->cens[in_buf].soa();
-  P.cout = c->cens[out_buf].soa();
+  /* in-place census: last step's records are this step's first items;
+   * appends start after them */
+  P.cin = c->cens.soa();
+  P.cout = c->cens.soa();
   P.n_cin = c->n_census;
-  P.cap_cout = cfg.census_capacity;
-  {
-    /* census chunk per wave reservation: <= 1024 slots, and the chunk tails
-     * (at most one per wave) at most 1/8 of the capacity; >= 64 so one
-     * reservation always covers a wave's census lanes */
-    const int64_t waves = (int64_t)std::max(c->bundle_grid, 1) * (C2D_TR_BLOCK / 64);
-    int64_t ch = 1024;
-    while (ch > 64 && ch * waves * 8 > cfg.census_capacity) ch >>= 1;
-    P.cens_chunk = (uint32_t)ch;
-  }
+  P.cap_cout = c->cens_phys;
+  P.cens_chunk = c->cens_chunk;
   P.n_cout = c->ctl + CTL_NCOUT;
   P.ev = c->ev; P.cap_ev = cfg.event_capacity;
   P.n_ev_sh = c->ctl + CTL_EVSH;
@@ -690,7 +774,6 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.err = c->derr;
   P.lds_cells = c->lds_cells;
   P.prof = c->ctl + CTL_PROF;
-  P.cens_holes = c->cens_holes;
   P.n_vol_global = c->n_vol_global;
   P.n_surf_global = c->n_surf_global;
   /* this rank's share of the global source index space (lineage-sharded) */
@@ -725,9 +808,11 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   HIPCHK(c, hipMemsetAsync(c->nf_rep, 0, sizeof(double) * C2D_NF_REPL * c->ncell * C2D_NPHFIELD,
                            c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl, 0, sizeof(unsigned long long) * CTL_WORDS, c->stream));
-  if (c->cens_holes)
-    HIPCHK(c, hipMemsetAsync(c->cens_holes, 0, sizeof(unsigned long long) * c->h_holes.size(),
-                             c->stream));
+  {
+    const unsigned long long ncin = (unsigned long long)c->n_census;   /* appends start here */
+    HIPCHK(c, hipMemcpyAsync(c->ctl + CTL_NCOUT, &ncin, sizeof ncin, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   HIPCHK(c, hipMemsetAsync(c->derr, 0, sizeof(int32_t), c->stream));
 
   const bool fast = cfg.comtot_mode == C2D_COMTOT_TABLE;
@@ -762,16 +847,12 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     A.work_counter = c->ctl + CTL_WORK;
     A.work_sh = c->ctl + CTL_WSH;
     HIPCHK(c, hipEventRecord(c->ev_g0t, c->stream));
-    if (A.n_items > 0 && c->bundle) {
+    if (A.n_items > 0) {
       auto launch_b = fast ? c2d_launch_bundle_fast : c2d_launch_bundle_exact;
       const int grid = (int)std::max<int64_t>(
           1, std::min<int64_t>(c->bundle_grid, (A.n_items + C2D_TR_BLOCK - 1) / C2D_TR_BLOCK));
       int rc = launch_b(c->dP, &A, grid, c->bundle_lds, c->stream);
       if (rc) return fail(c, C2D_E_HIP, "bundle launch (gen 0): %s", hipGetErrorString((hipError_t)rc));
-      launches++;
-    } else if (A.n_items > 0) {
-      int rc = launch_tr(c->dP, &A, tr_grid(A.n_items), c->lds_bytes, c->stream);
-      if (rc) return fail(c, C2D_E_HIP, "transport launch (gen 0): %s", hipGetErrorString((hipError_t)rc));
       launches++;
     }
     HIPCHK(c, hipEventRecord(c->ev_g0b, c->stream));
@@ -815,71 +896,32 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     gen++;
   }
-  /* close the holes the bundle kernel's census chunks left (census stays dense) */
-  int64_t cens_dense = -1;
-  if (c->bundle && c->cens_holes) {
-    /* a census write beyond the capacity: fail before the compaction reads
-     * records from reserved slots past the end of the buffer */
+  /* close the in-place census's dead slots (C2D_CENS_DEAD): census items that
+   * did not return to the census and the unused tails of the append chunks */
+  int64_t cens_live = 0;
+  {
+    unsigned long long cw[2];
     int32_t herr0 = 0;
-    unsigned long long reserved = 0;
+    HIPCHK(c, hipMemcpyAsync(cw, c->ctl + CTL_NCOUT, sizeof cw[0], hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(cw + 1, c->ctl + CTL_CNT + C2D_CNT_DEAD_INT, sizeof cw[1],
+                             hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&herr0, c->derr, sizeof herr0, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&reserved, c->ctl + CTL_NCOUT, sizeof reserved, hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_holes.data(), c->cens_holes,
-                             sizeof(unsigned long long) * c->h_holes.size(), hipMemcpyDeviceToHost,
-                             c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    /* a record slot beyond the physical census: the census is incomplete */
     if (herr0 & ERR_CENSUS)
-      return fail(c, C2D_E_CENSUS_OVERFLOW, "census overflow (capacity %lld)",
-                  (long long)cfg.census_capacity);
-    std::vector<std::pair<int64_t, int64_t>> holes;
-    int64_t nh = 0;
-    for (size_t w = 0; w + 1 < c->h_holes.size(); w += 2) {
-      const int64_t a0 = (int64_t)c->h_holes[w], n = (int64_t)c->h_holes[w + 1];
-      if (n <= 0) continue;
-      holes.emplace_back(a0, n);
-      nh += n;
-    }
-    const int64_t R = (int64_t)reserved, W = R - nh;
-    cens_dense = W;
-    if (nh > 0 && W < cfg.census_capacity) {
-      std::sort(holes.begin(), holes.end());
-      /* destinations: hole slots below W; sources: non-hole slots in [W, R) */
-      std::vector<long long> mv;
-      size_t hi = 0;                       /* next hole (source side scan) */
-      int64_t src = W;
-      auto next_src = [&](int64_t& s, int64_t& run) {
-        /* advance s past holes; run = valid records from s before the next hole */
-        for (;;) {
-          while (hi < holes.size() && holes[hi].first + holes[hi].second <= s) hi++;
-          if (hi < holes.size() && holes[hi].first <= s) { s = holes[hi].first + holes[hi].second; continue; }
-          run = (hi < holes.size() ? holes[hi].first : R) - s;
-          return;
-        }
-      };
-      for (const auto& h : holes) {
-        if (h.first >= W) break;
-        int64_t dst = h.first, left = std::min<int64_t>(h.second, W - h.first);
-        while (left > 0) {
-          int64_t run = 0;
-          next_src(src, run);
-          const int64_t n = std::min(left, run);
-          if (n <= 0) return fail(c, C2D_E_STATE, "census compaction: inconsistent holes");
-          mv.push_back(src); mv.push_back(dst); mv.push_back(n);
-          src += n; dst += n; left -= n;
-        }
-      }
-      const int nmv = (int)(mv.size() / 3);
-      if ((size_t)nmv * 3 > 3 * c->h_holes.size() + 6)
-        return fail(c, C2D_E_STATE, "census compaction: %d moves", nmv);
-      if (nmv > 0) {
-        HIPCHK(c, hipMemcpyAsync(c->cens_moves, mv.data(), sizeof(long long) * mv.size(),
-                                 hipMemcpyHostToDevice, c->stream));
-        const int rc = c2d_launch_census_move(P.cout, c->cens_moves, nmv, c->stream);
-        if (rc) return fail(c, C2D_E_HIP, "census move: %s", hipGetErrorString((hipError_t)rc));
-        launches++;
-      }
-    }
+      return fail(c, C2D_E_CENSUS_OVERFLOW, "census overflow: more than %lld records before "
+                  "compaction (capacity %lld)", (long long)c->cens_phys, (long long)cfg.census_capacity);
+    /* reservations past the physical end are chunk tails (never written) */
+    const int64_t R = std::min<int64_t>((int64_t)cw[0], c->cens_phys);
+    const int64_t D = (int64_t)cw[1];
+    cens_live = R - D;
+    if (cens_live < 0 || D > R)
+      return fail(c, C2D_E_STATE, "census compaction: %lld dead of %lld slots", (long long)D, (long long)R);
+    if (cens_live > cfg.census_capacity)
+      return fail(c, C2D_E_CENSUS_OVERFLOW, "too many photons: census %lld > capacity %lld",
+                  (long long)cens_live, (long long)cfg.census_capacity);
+    int rc = census_compact(c, R, cens_live);
+    if (rc) return rc;
   }
   {
     const int64_t n = (int64_t)c->ncell * C2D_NPHFIELD;
@@ -912,11 +954,11 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   double hc[C2D_NCOUNTERS];
   for (int i = 0; i < C2D_NCOUNTERS; i++) hc[i] = (double)ctl[CTL_CNT + i];
   c->last_all_paths = (int64_t)ctl[CTL_CNT + C2D_CNT_PATHS_INT];
-  hc[C2D_CNT_PATHS_INT] = 0.0;              /* internal: not a tally counter */
+  hc[C2D_CNT_PATHS_INT] = 0.0;              /* internal: not tally counters */
+  hc[C2D_CNT_DEAD_INT] = 0.0;
   hc[C2D_CNT_GENS] = (double)gen;
   HIPCHK(c, hipMemcpyAsync(c->T + c->L.counters, hc, sizeof hc, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const int64_t ncout = cens_dense >= 0 ? cens_dense : (int64_t)ctl[CTL_NCOUT];
   c->n_ev = 0;
   unsigned long long ev_reserved = 0;
   for (int sh = 0; sh < C2D_EV_SHARDS; sh++) {
@@ -925,11 +967,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     c->ev_cnt[sh] = std::min<int64_t>((int64_t)m, c->ev_cap_sh);
     c->n_ev += c->ev_cnt[sh];
   }
-  c->cur_out = out_buf;
-  c->n_census = std::min<int64_t>(ncout, cfg.census_capacity);
-  if (herr & ERR_CENSUS)
-    return fail(c, C2D_E_CENSUS_OVERFLOW, "too many photons: census %lld > capacity %lld",
-                (long long)ncout, (long long)cfg.census_capacity);
+  c->n_census = cens_live;
   if (herr & ERR_EVENT) {
     unsigned long long fill = 0;
     for (int sh = 0; sh < C2D_EV_SHARDS; sh++)
@@ -1022,7 +1060,7 @@ extern "C" int c2d_census_export_range(c2d_ctx* c, int64_t first, int64_t stride
   const int64_t m = std::min(cap, avail);
   if (m <= 0) return C2D_OK;
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  const DevCensus& d = c->cens[c->cur_out];
+  const DevCensus& d = c->cens;
   std::vector<double> col(m);
   std::vector<uint32_t> jk(m), bins(m);
   HIPCHK(c, col_down(jk.data(), d.jk, first, stride, m));
@@ -1053,7 +1091,7 @@ extern "C" int c2d_census_export(c2d_ctx* c, double* d6, int32_t* i5, uint64_t* 
   const int64_t m = std::min(cap, c->n_census);
   if (m <= 0) return C2D_OK;
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  const DevCensus& d = c->cens[c->cur_out];
+  const DevCensus& d = c->cens;
   std::vector<double> col(m);
   std::vector<uint32_t> jk(m), bins(m);
   HIPCHK(c, hipMemcpy(jk.data(), d.jk, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -1083,7 +1121,7 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
   if (n > c->cfg.census_capacity)
     return fail(c, C2D_E_CENSUS_OVERFLOW, "census import %lld > capacity", (long long)n);
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  const DevCensus& d = c->cens[c->cur_out];
+  const DevCensus& d = c->cens;
   std::vector<double> col(n);
   const bool enc = cens_encoded(c);
   for (int f = 0; f < 6; f++) {
@@ -1160,7 +1198,7 @@ extern "C" int c2d_census_pack(c2d_ctx* c, int64_t first, int64_t n, uint64_t* d
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 8);
   hipLaunchKernelGGL(c2d_census_pack_kernel, dim3(grid), dim3(256), 0, c->stream,
-                     c->cens[c->cur_out].soa(), first, n, d_rec);
+                     c->cens.soa(), first, n, d_rec);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return C2D_OK;
@@ -1175,7 +1213,7 @@ extern "C" int c2d_census_append(c2d_ctx* c, const uint64_t* d_rec, int64_t n) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 8);
   hipLaunchKernelGGL(c2d_census_unpack_kernel, dim3(grid), dim3(256), 0, c->stream,
-                     c->cens[c->cur_out].soa(), c->n_census, n, d_rec);
+                     c->cens.soa(), c->n_census, n, d_rec);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->n_census += n;
@@ -1223,6 +1261,14 @@ extern "C" int c2d_last_path_steps(c2d_ctx* c, int64_t* gen0_paths, int64_t* all
   if (!c) return C2D_E_ARG;
   if (gen0_paths) *gen0_paths = c->last_g0_paths;
   if (all_paths) *all_paths = c->last_all_paths;
+  return C2D_OK;
+}
+
+extern "C" int c2d_last_compaction(c2d_ctx* c, int32_t* rounds, int64_t* moved, int64_t* physical) {
+  if (!c) return C2D_E_ARG;
+  if (rounds) *rounds = c->last_compact_rounds;
+  if (moved) *moved = c->last_compact_moved;
+  if (physical) *physical = c->cens_phys;
   return C2D_OK;
 }
 

@@ -91,7 +91,6 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 /* Fortran REAL literals promoted to double (src/imcvol2d_para.f:204,221,247,268,336) */
 #define F32(x) ((double)(float)(x))
 
-enum : int32_t { ST_IDLE = 0, ST_PROBE = 1, ST_TRACK = 2 };
 enum : int32_t { FL_CONT = 0, FL_END = 1, FL_COLLIDE = 2 };
 
 struct Pkt {
@@ -582,13 +581,13 @@ C2D_COLD_FN int imcleak(const KParams& P0, const Tal& T, Pkt& p, LaneCnt& lc) {
   return 1;
 }
 
-/* Census slots of the bundle kernel come from wave-private chunks of
+/* Census appends of the bundle kernel come from wave-private chunks of
  * P.cens_chunk slots (host: up to 1024, and at most 1/8 of the capacity over
- * all waves: 256 -> 1024 slots was +1 %), reserved with one atomic on the census counter (a single
- * address every wave appends to: per-write reservations were the kernel's
- * limiter).  A wave's last chunk leaves a hole [used, CENS_CHUNK), recorded
- * in P.cens_holes and closed after the step by moving records from the end
- * of the census (c2d_census_move), so the census stays dense. */
+ * all waves: 256 -> 1024 slots was +1 %), reserved with one atomic on the
+ * census counter (a single address every wave appends to: per-write
+ * reservations were the kernel's limiter).  A wave's last chunk leaves a tail
+ * [used, CENS_CHUNK) that the kernel marks dead at its end; the host's
+ * compaction closes it with the other dead slots (C2D_CENS_DEAD). */
 /* per wave of the workgroup, in LDS (updated by the lanes that write) */
 __shared__ unsigned long long c2d_cch_base[16];
 __shared__ uint32_t c2d_cch_used[16];
@@ -622,9 +621,11 @@ __device__ __forceinline__ unsigned long long census_slot_chunk(const KParams& P
   return rank < rem ? base + used + rank : nb + (rank - rem);
 }
 
-/* census write (src/imctrk2d.f:528-578) */
+/* census write (src/imctrk2d.f:528-578).  inplace >= 0: the packet's source
+ * is census record `inplace`, which it replaces (in-place census); else the
+ * record is appended. */
 C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, LaneCnt& lc,
-                              CensChunk* cch = nullptr) {
+                              CensChunk* cch = nullptr, long long inplace = -1) {
   const KParams& P = cold(P0);
   const Geo* g = T.g;
   int cell = (p.jph - 1) * P.nr + (p.kph - 1);
@@ -639,7 +640,9 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
     gadd(&P.nf_rep[(int64_t)(blockIdx.x % C2D_NF_REPL) * P.ncell * C2D_NPHFIELD +
                    (int64_t)cell * C2D_NPHFIELD + (i - 1)], 6.25e8 * p.ew / p.xnu);
   }
-  unsigned long long slot = cch ? census_slot_chunk(P, *cch) : wave_reserve(P.n_cout);
+  unsigned long long slot;
+  if (inplace >= 0) slot = (unsigned long long)inplace;
+  else slot = cch ? census_slot_chunk(P, *cch) : wave_reserve(P.n_cout);
   if (slot < (unsigned long long)P.cap_cout) {
     gst(P.cout.rpre + slot, p.rpre);
     gst(P.cout.zpre + slot, p.zpre);
@@ -1395,8 +1398,11 @@ __device__ __forceinline__ void load_source(const KParams& P0, Pkt& p, long long
 }
 
 /* ------------------------------------------------------------------ */
-/* the transport kernel                                                */
+/* the transport kernel: scatter secondaries of generations >= 1         */
 /* ------------------------------------------------------------------ */
+/* Every secondary is an imctrk2d(1) track (imctrk2d.f:662-679) from the
+ * packet store; generation 0 (census + sources, the split1 probes and the
+ * recombined copy) runs as probe bundles (c2d_bundle_kernel below). */
 __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kernel)(const KParams* __restrict__ Pg,
                                                                       const GenArgs A) {
   const KParams& P = *Pg;
@@ -1419,17 +1425,11 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
   }
   init_counters(c2d_cnt_lds);
   __syncthreads();
-  const long long n_items = A.gen == 0 ? (long long)A.n_items : (long long)rfl64(*A.n_pk);
+  const long long n_items = (long long)rfl64(*A.n_pk);
 
   Pkt p;
-  p.mode = 0; p.bins = 0u; p.ctr = 0; p.key = 0; p.sub = 0; p.nflight = 0;
-  /* The split1 loop (imctrk2d.f:106-123) restarts every copy from the source
-   * record, which stays in memory (census store / packet store) for the whole
-   * launch: it is re-read instead of being held in registers. */
-  long long src_item = 0;
-#if C2D_TABLE_COMTOT
-#endif
-  int32_t state = ST_IDLE, probe = 0, nscat = 0;
+  p.mode = 1; p.bins = 0u; p.ctr = 0; p.key = 0; p.sub = 0; p.nflight = 0;
+  bool busy = false;
   ComCache cc = {-1, -1, 0.0, 0.0};
   LaneCnt lc = {0u};
   long long chunk_base = 0, chunk_end = 0;
@@ -1445,7 +1445,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
     bool got = false;
     long long item = -1;
     if (!exhausted) {
-      unsigned long long needm = __ballot(state == ST_IDLE);
+      unsigned long long needm = __ballot(!busy);
       while (needm != 0ull) {
         if (chunk_base >= chunk_end) {
           unsigned long long nb = 0;
@@ -1464,7 +1464,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
           got = true;
         }
         chunk_base += (nneed < avail ? nneed : avail);
-        needm = __ballot(state == ST_IDLE && !got);
+        needm = __ballot(!busy && !got);
       }
     }
     TP_MARK(pf, TP_REFILL);
@@ -1473,72 +1473,26 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
 #endif
     if (got) {
       TP_COUNT(pf, TP_GOT_W, TP_GOT_L);
-      if (A.gen == 0) {
-        /* imctrk2d(-1) entry (imctrk2d.f:91,106-123): first probe copy */
-        LC_ADD(lc, C2D_CNT_SOURCES);
-        src_item = item;
-        load_source(P, p, item);
-        p.wtmin = 1.0e-10 * p.ew;
-        p.ew = p.ew / P.split1;
-        p.mode = -1;
-        p.sub = 1u;
-        p.ctr = 0;
-        probe = 0;
-        nscat = 0;
-        state = ST_PROBE;
-      } else {
-        /* a scatter secondary, tracked as imctrk2d(1) (imctrk2d.f:662-679) */
-        load_pk(p, cold(P).pk, item);
-        set_phi(p, p.phi);
-        p.mode = 1;
-        p.wtmin = 1.0e-10 * p.ew;
-        state = ST_TRACK;
-      }
+      load_pk(p, cold(P).pk, item);
+      set_phi(p, p.phi);
+      p.mode = 1;
+      p.wtmin = 1.0e-10 * p.ew;
       p.nflight = 0;
       cc.cell0 = -1; cc.cell1 = -1;
-      cache_energy(P, T.g, p);        /* azimuth: set by load_source / above */
+      cache_energy(P, T.g, p);
+      busy = true;
     }
-    if (exhausted && __ballot(state != ST_IDLE) == 0ull) break;
+    if (exhausted && __ballot(busy) == 0ull) break;
     TP_MARK(pf, TP_START);
-    if (state != ST_IDLE) {
+    if (busy) {
 #ifdef C2D_TR_PROF
       pf.acc[TP_LANES] += __popcll(__ballot(1));
 #endif
       const int out = flight(P, T, p, cc, lc, pf);
       TP_MARK(pf, TP_EVENT);
       if (out != FL_CONT) {
-        if (out == FL_COLLIDE) {
-          push_scat(P, A.q2_out, A.n2_out, make_rec(p, p.key, p.ctr));
-          if (state == ST_PROBE) nscat++;
-        }
-        if (state == ST_PROBE) {
-          probe++;
-          if (probe < P.split1 || P.split1 - nscat > 0) {
-            TP_COUNT(pf, TP_RST_W, TP_RST_L);
-            load_source(P, p, src_item);
-            const double ew0 = p.ew;
-            const double s_ew = ew0 / P.split1;
-            p.ctr = 0;
-            p.nflight = 0;
-            /* same xnu: the energy caches and ComCache stay valid (azimuth: load_source) */
-            if (probe < P.split1) {
-              p.ew = s_ew;
-              p.wtmin = 1.0e-10 * ew0;
-              p.sub = 1u + (uint32_t)probe;
-            } else {
-              /* recombined unscattered copies, imctrk2d(0) (imctrk2d.f:690-704) */
-              p.ew = (double)(P.split1 - nscat) * s_ew;
-              p.wtmin = 1.0e-10 * p.ew;
-              p.mode = 0;
-              p.sub = C2D_SUB_RECOMB;
-              state = ST_TRACK;
-            }
-          } else {
-            state = ST_IDLE;
-          }
-        } else {
-          state = ST_IDLE;
-        }
+        if (out == FL_COLLIDE) push_scat(P, A.q2_out, A.n2_out, make_rec(p, p.key, p.ctr));
+        busy = false;
       }
     }
     TP_MARK(pf, TP_POST);
@@ -1610,7 +1564,8 @@ enum : int32_t {
   BF_SPEC = 2,      /* ... with a weight that assumes no more collisions */
   BF_RERUN = 4,     /* a collision cancelled it: refly alone afterwards  */
   BF_TKILL = 8,     /* it ended KILLED / ABORTED: counted at the bundle end */
-  BF_TABORT = 16
+  BF_TABORT = 16,
+  BF_CWROTE = 32    /* it wrote its census record in place (census source)  */
 };
 struct Bundle {
   Pkt p;              /* shared path; p.ew, p.wtmin, p.ctr: the recombined copy's */
@@ -1912,8 +1867,10 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
       b.alive = 0;
       if (b.flags & BF_TRACK) {
         TP_COUNT(pf, TP_CENS_W, TP_CENS_L);
-        census_write(P, T, p, lc, cch);
-        b.flags &= ~BF_TRACK;
+        /* a census source's one census record replaces its own (C2D_CENS_DEAD):
+         * the recombined copy flies last, after every read of the record */
+        census_write(P, T, p, lc, cch, b.src < P.n_cens_items ? b.src : -1);
+        b.flags = (b.flags & ~BF_TRACK) | BF_CWROTE;
       }
     }
   }
@@ -2093,6 +2050,11 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
           bundle_begin(P, T, b);
         } else {
           busy = false;
+          if (b.src < P.n_cens_items && !(b.flags & BF_CWROTE)) {
+            /* the census record of a packet that left, died or collided is free */
+            gst(cold(P).cout.bins + b.src, C2D_CENS_DEAD);
+            LC_ADD(lc, C2D_CNT_DEAD_INT);
+          }
         }
       }
     }
@@ -2105,11 +2067,17 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
       if (pf.acc[i]) atomicAdd(&P.prof[i], (unsigned long long)pf.acc[i]);
 #endif
 
-  /* the unused tail of this wave's last census chunk */
-  if (lane == 0 && c2d_cch_used[tid >> 6] < CENS_CHUNK) {
-    const size_t w = (size_t)blockIdx.x * (BLOCK / 64) + (size_t)(tid >> 6);
-    P.cens_holes[2 * w] = c2d_cch_base[tid >> 6] + c2d_cch_used[tid >> 6];
-    P.cens_holes[2 * w + 1] = CENS_CHUNK - c2d_cch_used[tid >> 6];
+  /* the unused tail of this wave's last census chunk: dead slots (those past
+   * the physical end of the census were never reserved for a record) */
+  {
+    const unsigned long long t0 = c2d_cch_base[tid >> 6] + c2d_cch_used[tid >> 6];
+    unsigned long long t1 = c2d_cch_base[tid >> 6] + CENS_CHUNK;
+    const unsigned long long cap = (unsigned long long)cold(P).cap_cout;
+    if (t1 > cap) t1 = cap;
+    if (c2d_cch_used[tid >> 6] < CENS_CHUNK && t0 < t1) {
+      for (unsigned long long i = t0 + lane; i < t1; i += 64) gst(cold(P).cout.bins + i, C2D_CENS_DEAD);
+      if (lane == 0) atomicAdd(&c2d_cnt_lds[C2D_CNT_DEAD_INT], (uint32_t)(t1 - t0));
+    }
   }
 
   /* ---- flush: LDS tallies and counters ---- */
@@ -2130,21 +2098,6 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
   }
   flush_counters(P, lc, lane);
 }
-
-#if C2D_TABLE_COMTOT
-/* close the census holes: move n records src -> dst per workgroup (one move
- * each, n <= P.cens_chunk); moves never overlap */
-__global__ void __launch_bounds__(256) c2d_census_move(CensusSoA c, const long long* mv) {
-  const long long src = mv[3 * blockIdx.x], dst = mv[3 * blockIdx.x + 1], n = mv[3 * blockIdx.x + 2];
-  for (long long i = threadIdx.x; i < n; i += 256) {
-    c.rpre[dst + i] = c.rpre[src + i]; c.zpre[dst + i] = c.zpre[src + i];
-    c.wmu[dst + i] = c.wmu[src + i]; c.phi[dst + i] = c.phi[src + i];
-    c.ew[dst + i] = c.ew[src + i]; c.xnu[dst + i] = c.xnu[src + i];
-    c.jk[dst + i] = c.jk[src + i]; c.bins[dst + i] = c.bins[src + i];
-    c.key[dst + i] = c.key[src + i];
-  }
-}
-#endif
 
 #if C2D_TABLE_COMTOT
 /* Per-step comtot table: tab[cell][g] = sum_i sigma_E(i, x_g) f_nt(cell,i) dg_i
@@ -2254,11 +2207,6 @@ extern "C" int C2D_SFX(c2d_transport_occupancy)(int* blocks_per_cu, size_t lds_b
 }
 
 #if C2D_TABLE_COMTOT
-extern "C" int c2d_launch_census_move(c2d::CensusSoA c, const long long* moves, int n, hipStream_t stream) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(c2d::c2d_census_move, dim3(n), dim3(256), 0, stream, c, moves);
-  return (int)hipGetLastError();
-}
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t stream) {
   hipLaunchKernelGGL(c2d::c2d_comtab_sigma, dim3(C2D_COMTAB_N), dim3(256), 0, stream, gnt, S);
   return (int)hipGetLastError();

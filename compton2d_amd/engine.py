@@ -99,6 +99,9 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_last_gen0_steps.argtypes = [vp, C.POINTER(C.c_int64)]
     lib.c2d_last_path_steps.restype = C.c_int
     lib.c2d_last_path_steps.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    lib.c2d_last_compaction.restype = C.c_int
+    lib.c2d_last_compaction.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
+                                        C.POINTER(C.c_int64)]
     lib.c2d_last_kernel_ms.restype = C.c_int
     lib.c2d_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                        C.POINTER(C.c_int32)]
@@ -311,6 +314,13 @@ class Engine:
         g0, al = C.c_int64(), C.c_int64()
         self._check(self.lib.c2d_last_path_steps(self.ctx, C.byref(g0), C.byref(al)))
         return g0.value, al.value
+
+    def last_compaction(self) -> tuple[int, int, int]:
+        """(rounds, records moved, physical slots) of the last step's in-place
+        census compaction (c2d_last_compaction)."""
+        r, m, ph = C.c_int32(), C.c_int64(), C.c_int64()
+        self._check(self.lib.c2d_last_compaction(self.ctx, C.byref(r), C.byref(m), C.byref(ph)))
+        return r.value, m.value, ph.value
 
     # -- Fokker-Planck -------------------------------------------------------
     def fp_set_config(self, const: abi.FpConstants) -> None:

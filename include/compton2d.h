@@ -445,6 +445,12 @@ int  c2d_last_gen0_steps(c2d_ctx* ctx, int64_t* steps);
  * packet-steps / path-steps is the work sharing factor.  Either pointer may
  * be NULL. */
 int  c2d_last_path_steps(c2d_ctx* ctx, int64_t* gen0_paths, int64_t* all_paths);
+/* The in-place census of the last step (replaces the double-buffered
+ * dbufout/ibufout of imctrk2d.f:558-572 + imcfield2d.f:96-97): rounds of the
+ * compaction that closed its dead slots, records moved, and the physical
+ * slots the context holds (census_capacity + append slack).  Any pointer may
+ * be NULL. */
+int  c2d_last_compaction(c2d_ctx* ctx, int32_t* rounds, int64_t* moved, int64_t* physical);
 
 /* ------------------------------------------------------------------------
  * Multi-GPU tally reduction over RCCL (xGMI), for hosts that drive one

@@ -125,3 +125,57 @@ def test_census_overflow_is_reported(mode):
         small.transport_step(gc.step_inputs(0))
     assert e.value.code == -3, str(e.value)
     small.close()
+
+
+@pytest.mark.parametrize("mode", [abi.COMTOT_EXACT, abi.COMTOT_TABLE])
+def test_census_at_capacity_fits(mode):
+    """In-place census (c2d_device.hpp C2D_CENS_DEAD): a run whose census
+    reaches exactly the configured capacity succeeds and matches the
+    oracle's records; the append chunks' tails and the dead census slots are
+    compacted away, so the usable capacity is census_capacity itself."""
+    gc = GoldenCase("ssc_tau")
+    probe = Engine(gc.grid(comtot_mode=mode))
+    need = []
+    for n in range(gc.nsteps):
+        probe.transport_step(gc.step_inputs(n))
+        need.append(probe.census_count())
+    probe.close()
+    cap = max(need)
+    assert cap > 1000
+    eng = Engine(gc.grid(comtot_mode=mode, census_capacity=cap))
+    orc = OL.Oracle(gc.grid(), OL.RNG_LINEAGE, "det")
+    for n in range(gc.nsteps):
+        si = gc.step_inputs(n)
+        eng.transport_step(si)
+        assert orc.step(si) == 0
+        assert eng.census_count() == need[n]
+        if mode == abi.COMTOT_EXACT:
+            kg, ko = eng.census()[2], orc.census()[2]
+            np.testing.assert_array_equal(np.sort(kg), np.sort(ko))
+    eng.close()
+    orc.close()
+
+
+def test_census_compaction_in_many_rounds(monkeypatch):
+    """The compaction's work lists hold C2D_COMPACT_LIST dead/live slot pairs
+    per round; with a list of 7 every step needs many rounds, and the census
+    (and so the next step's histories) stays the oracle's."""
+    monkeypatch.setenv("C2D_COMPACT_LIST", "7")
+    gc = GoldenCase("ssc_tau")
+    eng = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT))
+    orc = OL.Oracle(gc.grid(), OL.RNG_LINEAGE, "det")
+    rounds = []
+    for n in range(gc.nsteps):
+        si = gc.step_inputs(n)
+        eng.transport_step(si)
+        assert orc.step(si) == 0
+        rounds.append(eng.last_compaction()[0])
+        kg, ko = eng.census()[2], orc.census()[2]
+        np.testing.assert_array_equal(np.sort(kg), np.sort(ko))
+        tg, to = eng.tallies(), orc.split()
+        sel = [abi.CNT_STEPS, abi.CNT_ESCAPES, abi.CNT_CENSUS, abi.CNT_COLLIDE, abi.CNT_KILLED,
+               abi.CNT_SOURCES, abi.CNT_COMPB, abi.CNT_EVENTS, abi.CNT_ESC_SCAT]
+        np.testing.assert_array_equal(tg["counters"][sel], to["counters"][sel])
+    assert max(rounds) > 10, rounds
+    eng.close()
+    orc.close()
