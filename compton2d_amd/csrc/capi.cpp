@@ -118,8 +118,10 @@ struct c2d_ctx {
   int64_t cens_phys = 0;
   uint32_t cens_chunk = 64;
   int64_t* cscan = nullptr;      /* [2][cscan_cap]: dead slots below W, live slots at/above W */
-  unsigned long long* cscan_n = nullptr;   /* [2] list lengths */
   int64_t cscan_cap = 0;
+  uint32_t* ctile_cnt = nullptr;           /* [tiles][2] holes, sources per tile       */
+  unsigned long long* ctile_off = nullptr; /* [tiles][2] + totals: exclusive prefixes  */
+  int64_t ctile_cap = 0;
   int last_compact_rounds = 0;
   int64_t last_compact_moved = 0;
   c2d_tally_layout L;
@@ -385,7 +387,6 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
     /* test knob: a short work list forces many compaction rounds */
     if (const char* e = getenv("C2D_COMPACT_LIST")) c->cscan_cap = std::max<long long>(1, atoll(e));
     HIPCHK(c, dalloc(&c->cscan, 2 * (size_t)c->cscan_cap));
-    HIPCHK(c, dalloc(&c->cscan_n, 2));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return C2D_OK;
@@ -401,7 +402,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
                   c->Pnt, c->n_e, c->vfrac, c->ewsv, c->surf_ew, c->surf_tbb, c->tbbl,
                   c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comS,
                   c->ev, c->q2[0], c->q2[1], c->q3[0], c->q3[1], c->T_own, c->nf_rep, c->ctl, c->derr, c->dP,
-                  c->cscan, c->cscan_n};
+                  c->cscan, c->ctile_cnt, c->ctile_off};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int f = 0; f < 6; f++)
@@ -652,34 +653,111 @@ __global__ void __launch_bounds__(256) c2d_nf_reduce(const double* __restrict__ 
 }
 
 /* In-place census compaction: W live records of the R slots [0, R); every
- * dead slot below W takes a live record from [W, R).  c2d_census_scan lists
- * both (wave-aggregated appends, at most cap each), c2d_census_fill moves
- * the pairs; rounds repeat while dead slots below W remain. */
-__global__ void __launch_bounds__(256) c2d_census_scan(const uint32_t* __restrict__ bins, int64_t R,
-                                                       int64_t W, int64_t cap, int64_t* __restrict__ holes,
-                                                       int64_t* __restrict__ srcs,
-                                                       unsigned long long* __restrict__ n) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const uint32_t lane = __lane_id();
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < R; base += stride) {
-    const int64_t i = base + threadIdx.x;
-    bool hole = false, src = false;
-    if (i < R) {
-      const bool dead = (bins[i] & C2D_CENS_DEAD) != 0u;
-      hole = dead && i < W;
-      src = !dead && i >= W;
+ * dead slot below W takes a live record from [W, R).  Tiles of CT_TILE
+ * slots: c2d_census_count counts a tile's holes (dead, below W) and sources
+ * (live, at or above W), c2d_census_scan forms the exclusive prefix of both
+ * over the tiles (one workgroup), c2d_census_emit writes the k-th hole's and
+ * the k-th source's slot into the two work lists (slot order: the moves are
+ * monotone, and no counter is contended), c2d_census_fill moves pair k.  A
+ * round moves at most `cap` pairs; rounds repeat while holes remain. */
+constexpr int CT_TILE = 4096, CT_BLOCK = 256;
+
+__device__ __forceinline__ void census_class(const uint32_t* bins, int64_t i, int64_t R, int64_t W,
+                                             bool& hole, bool& src) {
+  hole = src = false;
+  if (i < R) {
+    const bool dead = (bins[i] & C2D_CENS_DEAD) != 0u;
+    hole = dead && i < W;
+    src = !dead && i >= W;
+  }
+}
+
+__global__ void __launch_bounds__(CT_BLOCK) c2d_census_count(const uint32_t* __restrict__ bins, int64_t R,
+                                                             int64_t W, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t sh[2][CT_BLOCK / 64];
+  const int64_t t = blockIdx.x;
+  const int64_t base = t * CT_TILE;
+  uint32_t nh = 0, ns = 0;
+  for (int j = 0; j < CT_TILE / CT_BLOCK; j++) {
+    bool h, s;
+    census_class(bins, base + j * CT_BLOCK + threadIdx.x, R, W, h, s);
+    nh += (uint32_t)__popcll(__ballot(h));
+    ns += (uint32_t)__popcll(__ballot(s));
+  }
+  if (__lane_id() == 0) { sh[0][threadIdx.x >> 6] = nh; sh[1][threadIdx.x >> 6] = ns; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    uint32_t v = 0;
+    for (int w = 0; w < CT_BLOCK / 64; w++) v += sh[threadIdx.x][w];
+    cnt[2 * t + threadIdx.x] = v;
+  }
+}
+
+/* exclusive prefix over ntiles (holes, sources) pairs, in place, one
+ * workgroup of 1024 threads; totals at off[2 * ntiles], off[2 * ntiles + 1] */
+__global__ void __launch_bounds__(1024) c2d_census_scan(uint32_t* __restrict__ cnt, int64_t ntiles,
+                                                        unsigned long long* __restrict__ off) {
+  __shared__ unsigned long long sh[2][1024];
+  const int64_t per = (ntiles + 1023) / 1024;
+  const int64_t lo = threadIdx.x * per, hi = lo + per < ntiles ? lo + per : ntiles;
+  unsigned long long a = 0, b = 0;
+  for (int64_t t = lo; t < hi; t++) { a += cnt[2 * t]; b += cnt[2 * t + 1]; }
+  sh[0][threadIdx.x] = a;
+  sh[1][threadIdx.x] = b;
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    unsigned long long run = 0;
+    for (int i = 0; i < 1024; i++) {
+      const unsigned long long v = sh[threadIdx.x][i];
+      sh[threadIdx.x][i] = run;
+      run += v;
     }
-    for (int l = 0; l < 2; l++) {
-      const bool mine = l == 0 ? hole : src;
-      const unsigned long long m = __ballot(mine);
-      if (m == 0ull) continue;
-      const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);
-      unsigned long long b = 0;
-      if (lane == leader) b = atomicAdd(n + l, (unsigned long long)__popcll(m));
-      b = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(b >> 32), leader) << 32) |
-          __builtin_amdgcn_readlane((uint32_t)b, leader);
-      const unsigned long long r = b + __popcll(m & ((1ull << lane) - 1ull));
-      if (mine && (int64_t)r < cap) (l == 0 ? holes : srcs)[r] = i;
+    off[2 * ntiles + threadIdx.x] = run;
+  }
+  __syncthreads();
+  a = sh[0][threadIdx.x];
+  b = sh[1][threadIdx.x];
+  for (int64_t t = lo; t < hi; t++) {
+    const unsigned long long ca = cnt[2 * t], cb = cnt[2 * t + 1];
+    off[2 * t] = a;
+    off[2 * t + 1] = b;
+    a += ca;
+    b += cb;
+  }
+}
+
+__global__ void __launch_bounds__(CT_BLOCK) c2d_census_emit(const uint32_t* __restrict__ bins, int64_t R,
+                                                            int64_t W, const unsigned long long* __restrict__ off,
+                                                            int64_t cap, int64_t* __restrict__ holes,
+                                                            int64_t* __restrict__ srcs) {
+  __shared__ uint32_t sh[2][CT_BLOCK / 64];
+  const int64_t t = blockIdx.x;
+  const int64_t base = t * CT_TILE;
+  const int w = threadIdx.x >> 6;
+  const uint32_t lane = __lane_id();
+  const unsigned long long below = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  unsigned long long rh = off[2 * t], rs = off[2 * t + 1];
+  for (int j = 0; j < CT_TILE / CT_BLOCK; j++) {
+    const int64_t i = base + j * CT_BLOCK + threadIdx.x;
+    bool h, s;
+    census_class(bins, i, R, W, h, s);
+    const unsigned long long mh = __ballot(h), ms = __ballot(s);
+    if (lane == 0) { sh[0][w] = (uint32_t)__popcll(mh); sh[1][w] = (uint32_t)__popcll(ms); }
+    __syncthreads();
+    unsigned long long ph = rh, ps = rs;
+    for (int v = 0; v < CT_BLOCK / 64; v++) {
+      if (v < w) { ph += sh[0][v]; ps += sh[1][v]; }
+      rh += sh[0][v];
+      rs += sh[1][v];
+    }
+    __syncthreads();
+    if (h) {
+      const unsigned long long k = ph + __popcll(mh & below);
+      if ((int64_t)k < cap) holes[k] = i;
+    }
+    if (s) {
+      const unsigned long long k = ps + __popcll(ms & below);
+      if ((int64_t)k < cap) srcs[k] = i;
     }
   }
 }
@@ -700,17 +778,29 @@ static int census_compact(c2d_ctx* c, int64_t R, int64_t W) {
   c->last_compact_rounds = 0;
   c->last_compact_moved = 0;
   if (W >= R) return C2D_OK;               /* no dead slot */
+  const int64_t ntiles = (R + CT_TILE - 1) / CT_TILE;
+  if (ntiles > c->ctile_cap) {
+    if (c->ctile_cnt) (void)hipFree(c->ctile_cnt);
+    if (c->ctile_off) (void)hipFree(c->ctile_off);
+    c->ctile_cnt = nullptr;
+    c->ctile_off = nullptr;
+    HIPCHK(c, dalloc(&c->ctile_cnt, 2 * (size_t)ntiles));
+    HIPCHK(c, dalloc(&c->ctile_off, 2 * (size_t)ntiles + 2));
+    c->ctile_cap = ntiles;
+  }
   const CensusSoA cs = c->cens.soa();
   int64_t* holes = c->cscan;
   int64_t* srcs = c->cscan + c->cscan_cap;
   for (int round = 0;; round++) {
-    HIPCHK(c, hipMemsetAsync(c->cscan_n, 0, 2 * sizeof(unsigned long long), c->stream));
-    const int grid = (int)std::min<int64_t>((R + 255) / 256, (int64_t)c->n_cu * 16);
-    hipLaunchKernelGGL(c2d_census_scan, dim3(grid), dim3(256), 0, c->stream, c->cens.bins, R, W,
-                       c->cscan_cap, holes, srcs, c->cscan_n);
+    hipLaunchKernelGGL(c2d_census_count, dim3((unsigned)ntiles), dim3(CT_BLOCK), 0, c->stream,
+                       c->cens.bins, R, W, c->ctile_cnt);
+    hipLaunchKernelGGL(c2d_census_scan, dim3(1), dim3(1024), 0, c->stream, c->ctile_cnt, ntiles,
+                       c->ctile_off);
+    hipLaunchKernelGGL(c2d_census_emit, dim3((unsigned)ntiles), dim3(CT_BLOCK), 0, c->stream,
+                       c->cens.bins, R, W, c->ctile_off, c->cscan_cap, holes, srcs);
     HIPCHK(c, hipGetLastError());
     unsigned long long nn[2];
-    HIPCHK(c, hipMemcpyAsync(nn, c->cscan_n, sizeof nn, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(nn, c->ctile_off + 2 * ntiles, sizeof nn, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (nn[0] != nn[1])
       return fail(c, C2D_E_STATE, "census compaction: %llu dead slots below %lld, %llu live above",
@@ -1761,6 +1851,15 @@ extern "C" int c2d_obs_result(c2d_ctx* c, double* F, double* F2, double* count, 
 /* cens_add_up/E_add_up, src/update2d.f:1929-2078)                      */
 /* ------------------------------------------------------------------ */
 static_assert(sizeof(ncclUniqueId) == C2D_COMM_ID_BYTES, "RCCL unique id size");
+
+extern "C" int c2d_device_count(int32_t* n) {
+  if (!n) return C2D_E_ARG;
+  int d = 0;
+  *n = 0;
+  if (hipGetDeviceCount(&d) != hipSuccess) return C2D_E_HIP;
+  *n = d;
+  return C2D_OK;
+}
 
 extern "C" int c2d_comm_unique_id(void* id, int64_t cap) {
   if (!id || cap < C2D_COMM_ID_BYTES) return C2D_E_ARG;

@@ -469,6 +469,9 @@ int  c2d_comm_init(c2d_ctx* ctx, const void* id, int32_t rank, int32_t world);
 /* ncclAllReduce(sum, f64) in place on the context's tally buffer, on the
  * context's stream; synchronous.  Without c2d_comm_init: C2D_E_STATE. */
 int  c2d_allreduce_tallies(c2d_ctx* ctx);
+/* GPUs visible to this process (hipGetDeviceCount), so an MPI host can map
+ * its ranks to devices (c2d_config.device); 0 and C2D_E_HIP without one. */
+int  c2d_device_count(int32_t* n);
 
 /* Diagnostics: evaluate the transport kernels' elementary functions on the
  * device (fn 0 log, 1 exp, 2 cos, 3 acos, 4 cbrt-by-pow, 5 sqrt, 6 x/3,

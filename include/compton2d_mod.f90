@@ -301,6 +301,11 @@ module compton2d
        type(c_ptr), value :: ctx
      end function c2d_allreduce_tallies
 
+     integer(c_int) function c2d_device_count(n) bind(C, name='c2d_device_count')
+       import :: c_int, c_int32_t
+       integer(c_int32_t), intent(out) :: n
+     end function c2d_device_count
+
      integer(c_int) function c2d_electron_state(ctx, f_nt, Pnt) bind(C, name='c2d_electron_state')
        import :: c_int, c_ptr, c2d_marray3
        type(c_ptr), value :: ctx
