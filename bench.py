@@ -55,15 +55,21 @@ BYTES_PER_STEP = 160.0          # 80 B packet record in + out
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s
 N_SIMD = 1024                   # 256 CUs x 4 SIMDs
 CLOCK_HZ = 2.4e9                # MI355X peak engine clock
-CENSUS_BYTES = 64 * (1 + 1 / 16)  # in-place census SoA record + the append slack (capi.cpp cens_phys)
+# census bytes per record of capacity (c2d_device.hpp CensusSoA, capi.cpp cens_phys):
+# double-buffered in + out, or in place + 1/16 append slack
+CENSUS_BYTES = {0: 2 * 64, 1: 64 * (1 + 1 / 16)}
 DEFAULT_SOURCES = {"c3": 100_000_000, "c2": 10_000_000, "c4": 125_000_000, "c5": 20_000_000}
 # untimed census spin-up (steps before the warm-up): a C3 source stays in the
 # census ~16 steps (tools/c3_bench.py: the census saturates at 15.8 records
 # per source of a step after ~40 steps, profiles/r03a), so the timed steps
 # see the steady-state census of a long run instead of its growth
-SPINUP = {"c3": 40, "c4": 0, "c2": 0, "c5": 0}
+SPINUP = {"c3": 40, "c4": 60, "c2": 0, "c5": 0}
+# in-place census by default where the double buffer cannot hold the run: C4's
+# 1.25e8 sources per GPU on the 32x32 C2 medium saturate at 22.6 census
+# records per source of a step (2.8e9, tools/census_traj.py, profiles/r03e)
+INPLACE = {"c3": 0, "c4": 1, "c2": 0, "c5": 0}
 # census records per source of a step the capacity is sized for
-CENSUS_PER_SOURCE = {"c3": 20.0, "c4": 40.0, "c2": 40.0, "c5": 8.0}
+CENSUS_PER_SOURCE = {"c3": 20.0, "c4": 26.0, "c2": 40.0, "c5": 8.0}
 
 
 def cpu_share() -> tuple[int, int]:
@@ -199,11 +205,11 @@ def load_pmc(workload_key: str):
         return {}
 
 
-def census_capacity(sources: int, per_source: float, free: float, side: float) -> int:
+def census_capacity(sources: int, per_source: float, free: float, side: float, inplace: int) -> int:
     """Census records the run may hold: per_source x sources, within 85 % of
-    the free HBM beside the event and packet buffers (in-place census at 64 B
-    per record + its append slack, capi.cpp cens_phys)."""
-    return int(min(per_source * sources + (1 << 20), max(1 << 20, (0.85 * free - side) / CENSUS_BYTES)))
+    the free HBM beside the event and packet buffers."""
+    return int(min(per_source * sources + (1 << 20),
+                   max(1 << 20, (0.85 * free - side) / CENSUS_BYTES[inplace])))
 
 
 def tally_exchange(eng, T, rank, world, dev):
@@ -245,6 +251,7 @@ def build_c3(args, rank, world, local, dev, sources, ccap, ecap, mode):
     from compton2d_amd.engine import Engine
     wl = synth.c3_workload(sources=sources * world, comtot_mode=mode, rank=rank, world=world,
                            device=local, census_capacity=ccap, event_capacity=ecap)
+    wl.grid.census_inplace = args.inplace
     eng = Engine(wl.grid)
     T = torch.zeros(eng.layout.total, dtype=torch.float64, device=dev)
     eng.use_tally_tensor(T)
@@ -266,6 +273,7 @@ def build_c2(args, rank, world, local, dev, sources, ccap, ecap, mode):
     wl = synth.c2_workload(nz=args.grid, nr=args.grid, sources=sources * world, comtot_mode=mode,
                            rank=rank, world=world, device=local, census_capacity=ccap,
                            event_capacity=ecap)
+    wl.grid.census_inplace = args.inplace
     eng = Engine(wl.grid)
     T = torch.zeros(eng.layout.total, dtype=torch.float64, device=dev)
     eng.use_tally_tensor(T)
@@ -308,6 +316,7 @@ def build_c5(args, rank, world, local, dev, sources, ccap, ecap, mode):
     g_bulk, zmax, rmax, rmin = 25.0, 1.0e17, 1.0e17, 0.0
     wl = synth.c2_workload(nz=nz, nr=nr, sources=nst, comtot_mode=mode, rank=rank, world=world,
                            device=local, census_capacity=ccap, event_capacity=ecap)
+    wl.grid.census_inplace = args.inplace
     z, r, vol, zs = synth.zone_geometry(nz, nr, zmax, rmin, rmax)
     wl.grid.z, wl.grid.r = z, r
     dt = min(r[-1] / nr, z[-1] / nz) / (np.sqrt(1.0 - 1.0 / g_bulk ** 2) * synth.C_LIGHT)
@@ -365,6 +374,9 @@ def main():
     ap.add_argument("--spinup", type=int, default=None,
                     help="untimed steps before the warm-up that bring the census to its steady "
                          "state (default: c3 %d, c4 %d, else 0)" % (SPINUP["c3"], SPINUP["c4"]))
+    ap.add_argument("--census-inplace", type=int, choices=(0, 1), default=None,
+                    help="1: one in-place census SoA (half the memory), 0: in + out buffers "
+                         "(default: 1 for c4, else 0)")
     ap.add_argument("--grid", type=int, default=32, help="c2/c4 grid (NxN)")
     ap.add_argument("--grid-c5", type=int, default=16, help="c5 grid (NxN)")
     ap.add_argument("--mode", choices=("fast", "exact"), default="fast")
@@ -389,13 +401,16 @@ def main():
     args.workload = wk
     sources = args.sources or DEFAULT_SOURCES[wk]
     spinup = SPINUP.get(wk, 0) if args.spinup is None else args.spinup
+    inplace = INPLACE[wk] if args.census_inplace is None else args.census_inplace
     total_steps = spinup + args.warmup + args.steps
     free, _ = torch.cuda.mem_get_info(dev)
     mode = abi.COMTOT_TABLE if args.mode == "fast" else abi.COMTOT_EXACT
     per_gpu_items = sources * (1.5 if wk == "c5" else 1.0)
     ecap = int(2 * per_gpu_items) + (1 << 20)
     side = ecap * 56 + per_gpu_items * 80 + (4 << 30)
-    ccap = census_capacity(int(per_gpu_items), min(CENSUS_PER_SOURCE[wk], total_steps + 1), free, side)
+    ccap = census_capacity(int(per_gpu_items), min(CENSUS_PER_SOURCE[wk], total_steps + 1), free, side,
+                           inplace)
+    args.inplace = inplace
     build = {"c3": build_c3, "c2": build_c2, "c4": build_c2, "c5": build_c5}[wk]
     eng, run, one_step, wl, desc, ex_desc = build(args, rank, world, local, dev, sources, ccap, ecap,
                                                   mode)
@@ -511,7 +526,10 @@ def main():
                        "records_at_timed_start": census_timed_start,
                        "records_at_end": eng.census_count(),
                        "capacity_per_gpu": ccap, "physical_slots": phys,
-                       "bytes_per_record": 64, "layout": "in-place SoA (c2d_device.hpp C2D_CENS_DEAD)",
+                       "bytes_per_record_of_capacity": CENSUS_BYTES[inplace],
+                       "layout": ("in place: one SoA, dead slots compacted (c2d_device.hpp "
+                                  "C2D_CENS_DEAD)" if inplace else
+                                  "double-buffered SoA (in + out), chunk tails compacted"),
                        "last_compaction_rounds": rounds, "last_compaction_moved": moved},
             "packet_steps_timed": steps_global,
             "per_step": per_step,

@@ -70,7 +70,7 @@ class Config(C.Structure):
         ("pair_switch", C.c_int32), ("kappa_lag", C.c_int32), ("comtot_mode", C.c_int32),
         ("device", C.c_int32), ("seed", C.c_uint64), ("rank", C.c_int32), ("world", C.c_int32),
         ("census_capacity", C.c_int64), ("event_capacity", C.c_int64),
-        ("queue_capacity", C.c_int64),
+        ("queue_capacity", C.c_int64), ("census_inplace", C.c_int32),
     ]
 
 
@@ -179,6 +179,7 @@ class GridConfig:
     census_capacity: int = 1 << 20
     event_capacity: int = 1 << 20
     queue_capacity: int = 1 << 18
+    census_inplace: int = 0
 
     def to_ctypes(self) -> Config:
         self._keep = [np.ascontiguousarray(a, dtype=np.float64) for a in (
@@ -195,7 +196,7 @@ class GridConfig:
             kappa_lag=self.kappa_lag, comtot_mode=self.comtot_mode, device=self.device,
             seed=self.seed, rank=self.rank, world=self.world,
             census_capacity=self.census_capacity, event_capacity=self.event_capacity,
-            queue_capacity=self.queue_capacity)
+            queue_capacity=self.queue_capacity, census_inplace=self.census_inplace)
 
 
 @dataclass

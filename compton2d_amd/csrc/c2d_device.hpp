@@ -191,6 +191,7 @@ struct KParams {
   CensusSoA cin, cout;
   int64_t n_cin, cap_cout;
   uint32_t cens_chunk;       /* census slots per wave reservation (bundle kernel) */
+  int32_t cens_inplace;      /* 1: cin == cout, census items rewrite their own slot */
   unsigned long long* n_cout;
   /* events */
   double* ev;

@@ -112,9 +112,9 @@ struct c2d_ctx {
   /* generation 0 as probe bundles (c2d_bundle_kernel): its LDS and grid */
   int bundle = 1, bundle_grid = 0;
   size_t bundle_lds = 0;
-  /* in-place census (c2d_device.hpp C2D_CENS_DEAD): one SoA of cens_phys
-   * records = census_capacity + the slack the bundle kernel's append chunks
-   * need; the compaction's work lists (cscan_cap slots each) */
+  /* census SoA(s) of cens_phys records each: census_capacity + one append
+   * chunk per wave (+ 1/16 of the capacity in place, c2d_device.hpp
+   * C2D_CENS_DEAD); the compaction's work lists (cscan_cap slots each) */
   int64_t cens_phys = 0;
   uint32_t cens_chunk = 64;
   int64_t* cscan = nullptr;      /* [2][cscan_cap]: dead slots below W, live slots at/above W */
@@ -137,8 +137,9 @@ struct c2d_ctx {
   int n_spectra = 0;
   double* comtab = nullptr;
   double* comS = nullptr;
-  DevCensus cens;            /* the in-place census */
-  int64_t n_census = 0;      /* live records: cens[0, n_census) */
+  DevCensus cens[2];         /* census_inplace: cens[0] only; else in / out buffers */
+  int cur = 0;               /* the buffer holding the census */
+  int64_t n_census = 0;      /* live records: cens[cur][0, n_census) */
   double* ev = nullptr;
   int64_t n_ev = 0;
   int64_t ev_cnt[C2D_EV_SHARDS] = {};   /* events in each shard of the buffer (last step) */
@@ -367,22 +368,24 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
     c->bundle_grid = c->n_cu * std::max(1, b0);
   }
   {
-    /* the in-place census.  Append chunks per wave reservation: <= 1024
-     * slots, >= 64 (one reservation covers a wave's census lanes), and their
-     * tails (at most one per wave) at most 1/8 of the capacity.  The
-     * physical size adds room for every wave's chunk tail and 1/16 of the
-     * capacity for appends that land before the dead slots are closed, so a
-     * census whose compacted size fits the capacity never overflows. */
+    /* the census.  Append chunks per wave reservation: <= 1024 slots, >= 64
+     * (one reservation covers a wave's census lanes), and their tails (at
+     * most one per wave) at most 1/8 of the capacity.  The physical size
+     * adds room for every wave's chunk tail (and, in place, 1/16 of the
+     * capacity for appends that land before the dead slots are closed), so
+     * a census whose compacted size fits the capacity does not overflow. */
     const int64_t ccap = std::max<int64_t>(cfg->census_capacity, 1);
     const int64_t waves = (int64_t)c->bundle_grid * (C2D_TR_BLOCK / 64);
     int64_t ch = 1024;
     while (ch > 64 && ch * waves * 8 > ccap) ch >>= 1;
     c->cens_chunk = (uint32_t)ch;
-    c->cens_phys = ccap + waves * ch + ccap / 16 + 64;
-    for (int f = 0; f < 6; f++) HIPCHK(c, dalloc(&c->cens.d[f], (size_t)c->cens_phys));
-    HIPCHK(c, dalloc(&c->cens.jk, (size_t)c->cens_phys));
-    HIPCHK(c, dalloc(&c->cens.bins, (size_t)c->cens_phys));
-    HIPCHK(c, dalloc(&c->cens.key, (size_t)c->cens_phys));
+    c->cens_phys = ccap + waves * ch + (cfg->census_inplace ? ccap / 16 : 0) + 64;
+    for (int b = 0; b < (cfg->census_inplace ? 1 : 2); b++) {
+      for (int f = 0; f < 6; f++) HIPCHK(c, dalloc(&c->cens[b].d[f], (size_t)c->cens_phys));
+      HIPCHK(c, dalloc(&c->cens[b].jk, (size_t)c->cens_phys));
+      HIPCHK(c, dalloc(&c->cens[b].bins, (size_t)c->cens_phys));
+      HIPCHK(c, dalloc(&c->cens[b].key, (size_t)c->cens_phys));
+    }
     c->cscan_cap = std::min<int64_t>(int64_t(1) << 27, std::max<int64_t>(int64_t(1) << 16, ccap / 16));
     /* test knob: a short work list forces many compaction rounds */
     if (const char* e = getenv("C2D_COMPACT_LIST")) c->cscan_cap = std::max<long long>(1, atoll(e));
@@ -405,11 +408,13 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
                   c->cscan, c->ctile_cnt, c->ctile_off};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  for (int f = 0; f < 6; f++)
-    if (c->cens.d[f]) (void)hipFree(c->cens.d[f]);
-  if (c->cens.jk) (void)hipFree(c->cens.jk);
-  if (c->cens.bins) (void)hipFree(c->cens.bins);
-  if (c->cens.key) (void)hipFree(c->cens.key);
+  for (int b = 0; b < 2; b++) {
+    for (int f = 0; f < 6; f++)
+      if (c->cens[b].d[f]) (void)hipFree(c->cens[b].d[f]);
+    if (c->cens[b].jk) (void)hipFree(c->cens[b].jk);
+    if (c->cens[b].bins) (void)hipFree(c->cens[b].bins);
+    if (c->cens[b].key) (void)hipFree(c->cens[b].key);
+  }
   for (double* p : c->spec_bufs) (void)hipFree(p);
   void* optrs[] = {c->obs_edges, c->obs_hist, c->obs_ev};
   for (void* p : optrs)
@@ -774,7 +779,7 @@ __global__ void __launch_bounds__(256) c2d_census_fill(CensusSoA c, const int64_
   }
 }
 
-static int census_compact(c2d_ctx* c, int64_t R, int64_t W) {
+static int census_compact(c2d_ctx* c, const DevCensus& cb, int64_t R, int64_t W) {
   c->last_compact_rounds = 0;
   c->last_compact_moved = 0;
   if (W >= R) return C2D_OK;               /* no dead slot */
@@ -788,16 +793,16 @@ static int census_compact(c2d_ctx* c, int64_t R, int64_t W) {
     HIPCHK(c, dalloc(&c->ctile_off, 2 * (size_t)ntiles + 2));
     c->ctile_cap = ntiles;
   }
-  const CensusSoA cs = c->cens.soa();
+  const CensusSoA cs = cb.soa();
   int64_t* holes = c->cscan;
   int64_t* srcs = c->cscan + c->cscan_cap;
   for (int round = 0;; round++) {
     hipLaunchKernelGGL(c2d_census_count, dim3((unsigned)ntiles), dim3(CT_BLOCK), 0, c->stream,
-                       c->cens.bins, R, W, c->ctile_cnt);
+                       cb.bins, R, W, c->ctile_cnt);
     hipLaunchKernelGGL(c2d_census_scan, dim3(1), dim3(1024), 0, c->stream, c->ctile_cnt, ntiles,
                        c->ctile_off);
     hipLaunchKernelGGL(c2d_census_emit, dim3((unsigned)ntiles), dim3(CT_BLOCK), 0, c->stream,
-                       c->cens.bins, R, W, c->ctile_off, c->cscan_cap, holes, srcs);
+                       cb.bins, R, W, c->ctile_off, c->cscan_cap, holes, srcs);
     HIPCHK(c, hipGetLastError());
     unsigned long long nn[2];
     HIPCHK(c, hipMemcpyAsync(nn, c->ctile_off + 2 * ntiles, sizeof nn, hipMemcpyDeviceToHost, c->stream));
@@ -840,13 +845,17 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.comtab = c->comtab;
   P.comtab_du_inv = (double)(C2D_COMTAB_N - 1) / (C2D_COMTAB_U1 - C2D_COMTAB_U0);
   P.egg_min = c->egg_min;
-  /* in-place census: last step's records are this step's first items;
-   * appends start after them */
-  P.cin = c->cens.soa();
-  P.cout = c->cens.soa();
+  /* last step's census records are this step's first items.  In place
+   * (census_inplace) they are read and rewritten in one SoA and appends start
+   * after them; double-buffered the step writes the other buffer from 0. */
+  const int inplace = cfg.census_inplace ? 1 : 0;
+  const int out_buf = inplace ? 0 : 1 - c->cur;
+  P.cin = c->cens[c->cur].soa();
+  P.cout = c->cens[out_buf].soa();
   P.n_cin = c->n_census;
   P.cap_cout = c->cens_phys;
   P.cens_chunk = c->cens_chunk;
+  P.cens_inplace = inplace;
   P.n_cout = c->ctl + CTL_NCOUT;
   P.ev = c->ev; P.cap_ev = cfg.event_capacity;
   P.n_ev_sh = c->ctl + CTL_EVSH;
@@ -899,7 +908,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
                            c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl, 0, sizeof(unsigned long long) * CTL_WORDS, c->stream));
   {
-    const unsigned long long ncin = (unsigned long long)c->n_census;   /* appends start here */
+    const unsigned long long ncin = inplace ? (unsigned long long)c->n_census : 0ull;   /* appends start here */
     HIPCHK(c, hipMemcpyAsync(c->ctl + CTL_NCOUT, &ncin, sizeof ncin, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
@@ -1010,7 +1019,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     if (cens_live > cfg.census_capacity)
       return fail(c, C2D_E_CENSUS_OVERFLOW, "too many photons: census %lld > capacity %lld",
                   (long long)cens_live, (long long)cfg.census_capacity);
-    int rc = census_compact(c, R, cens_live);
+    int rc = census_compact(c, c->cens[out_buf], R, cens_live);
     if (rc) return rc;
   }
   {
@@ -1058,6 +1067,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     c->n_ev += c->ev_cnt[sh];
   }
   c->n_census = cens_live;
+  c->cur = out_buf;
   if (herr & ERR_EVENT) {
     unsigned long long fill = 0;
     for (int sh = 0; sh < C2D_EV_SHARDS; sh++)
@@ -1150,7 +1160,7 @@ extern "C" int c2d_census_export_range(c2d_ctx* c, int64_t first, int64_t stride
   const int64_t m = std::min(cap, avail);
   if (m <= 0) return C2D_OK;
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  const DevCensus& d = c->cens;
+  const DevCensus& d = c->cens[c->cur];
   std::vector<double> col(m);
   std::vector<uint32_t> jk(m), bins(m);
   HIPCHK(c, col_down(jk.data(), d.jk, first, stride, m));
@@ -1181,7 +1191,7 @@ extern "C" int c2d_census_export(c2d_ctx* c, double* d6, int32_t* i5, uint64_t* 
   const int64_t m = std::min(cap, c->n_census);
   if (m <= 0) return C2D_OK;
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  const DevCensus& d = c->cens;
+  const DevCensus& d = c->cens[c->cur];
   std::vector<double> col(m);
   std::vector<uint32_t> jk(m), bins(m);
   HIPCHK(c, hipMemcpy(jk.data(), d.jk, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -1211,7 +1221,7 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
   if (n > c->cfg.census_capacity)
     return fail(c, C2D_E_CENSUS_OVERFLOW, "census import %lld > capacity", (long long)n);
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  const DevCensus& d = c->cens;
+  const DevCensus& d = c->cens[c->cur];
   std::vector<double> col(n);
   const bool enc = cens_encoded(c);
   for (int f = 0; f < 6; f++) {
@@ -1288,7 +1298,7 @@ extern "C" int c2d_census_pack(c2d_ctx* c, int64_t first, int64_t n, uint64_t* d
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 8);
   hipLaunchKernelGGL(c2d_census_pack_kernel, dim3(grid), dim3(256), 0, c->stream,
-                     c->cens.soa(), first, n, d_rec);
+                     c->cens[c->cur].soa(), first, n, d_rec);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return C2D_OK;
@@ -1303,7 +1313,7 @@ extern "C" int c2d_census_append(c2d_ctx* c, const uint64_t* d_rec, int64_t n) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 8);
   hipLaunchKernelGGL(c2d_census_unpack_kernel, dim3(grid), dim3(256), 0, c->stream,
-                     c->cens.soa(), c->n_census, n, d_rec);
+                     c->cens[c->cur].soa(), c->n_census, n, d_rec);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->n_census += n;

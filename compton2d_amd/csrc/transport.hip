@@ -1869,7 +1869,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
         TP_COUNT(pf, TP_CENS_W, TP_CENS_L);
         /* a census source's one census record replaces its own (C2D_CENS_DEAD):
          * the recombined copy flies last, after every read of the record */
-        census_write(P, T, p, lc, cch, b.src < P.n_cens_items ? b.src : -1);
+        census_write(P, T, p, lc, cch, (P.cens_inplace && b.src < P.n_cens_items) ? b.src : -1);
         b.flags = (b.flags & ~BF_TRACK) | BF_CWROTE;
       }
     }
@@ -2050,7 +2050,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
           bundle_begin(P, T, b);
         } else {
           busy = false;
-          if (b.src < P.n_cens_items && !(b.flags & BF_CWROTE)) {
+          if (P.cens_inplace && b.src < P.n_cens_items && !(b.flags & BF_CWROTE)) {
             /* the census record of a packet that left, died or collided is free */
             gst(cold(P).cout.bins + b.src, C2D_CENS_DEAD);
             LC_ADD(lc, C2D_CNT_DEAD_INT);

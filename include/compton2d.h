@@ -115,6 +115,11 @@ typedef struct c2d_config {
                                      buffer is 32 equal shards, workgroup b appends to
                                      shard b % 32, and a full shard is an overflow     */
   int64_t queue_capacity;         /* scatter records per generation            */
+  int32_t census_inplace;         /* 0: census double-buffered (in + out, 128 B per
+                                     record, the reference's dbufin/dbufout); 1: one
+                                     in-place SoA (64 B per record + 1/16 slack,
+                                     dead slots compacted after the step: half the
+                                     memory, slower census writes)   */
 } c2d_config;
 
 /* Per-step inputs (what imcgen2d/volume_em/file_sp leave in COMMON). */

@@ -54,6 +54,7 @@ module compton2d
      integer(c_int32_t) :: rank = 0, world = 1
      integer(c_int64_t) :: census_capacity = 5000000, event_capacity = 5000000, &
           queue_capacity = 262144
+     integer(c_int32_t) :: census_inplace = 0
   end type c2d_config
 
   type, bind(C) :: c2d_step_in

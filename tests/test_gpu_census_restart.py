@@ -127,14 +127,16 @@ def test_census_overflow_is_reported(mode):
     small.close()
 
 
+@pytest.mark.parametrize("inplace", [0, 1])
 @pytest.mark.parametrize("mode", [abi.COMTOT_EXACT, abi.COMTOT_TABLE])
-def test_census_at_capacity_fits(mode):
-    """In-place census (c2d_device.hpp C2D_CENS_DEAD): a run whose census
-    reaches exactly the configured capacity succeeds and matches the
-    oracle's records; the append chunks' tails and the dead census slots are
-    compacted away, so the usable capacity is census_capacity itself."""
+def test_census_at_capacity_fits(mode, inplace):
+    """A run whose census reaches exactly the configured capacity succeeds
+    and matches the oracle's records, double-buffered or in place
+    (c2d_device.hpp C2D_CENS_DEAD): the append chunks' tails (and in place
+    the dead census slots) are compacted away, so the usable capacity is
+    census_capacity itself (chunk tails cost up to ~20 %)."""
     gc = GoldenCase("ssc_tau")
-    probe = Engine(gc.grid(comtot_mode=mode))
+    probe = Engine(gc.grid(comtot_mode=mode, census_inplace=inplace))
     need = []
     for n in range(gc.nsteps):
         probe.transport_step(gc.step_inputs(n))
@@ -142,7 +144,7 @@ def test_census_at_capacity_fits(mode):
     probe.close()
     cap = max(need)
     assert cap > 1000
-    eng = Engine(gc.grid(comtot_mode=mode, census_capacity=cap))
+    eng = Engine(gc.grid(comtot_mode=mode, census_capacity=cap, census_inplace=inplace))
     orc = OL.Oracle(gc.grid(), OL.RNG_LINEAGE, "det")
     for n in range(gc.nsteps):
         si = gc.step_inputs(n)
@@ -156,13 +158,14 @@ def test_census_at_capacity_fits(mode):
     orc.close()
 
 
-def test_census_compaction_in_many_rounds(monkeypatch):
+@pytest.mark.parametrize("inplace", [0, 1])
+def test_census_compaction_in_many_rounds(monkeypatch, inplace):
     """The compaction's work lists hold C2D_COMPACT_LIST dead/live slot pairs
     per round; with a list of 7 every step needs many rounds, and the census
     (and so the next step's histories) stays the oracle's."""
     monkeypatch.setenv("C2D_COMPACT_LIST", "7")
     gc = GoldenCase("ssc_tau")
-    eng = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT))
+    eng = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, census_inplace=inplace))
     orc = OL.Oracle(gc.grid(), OL.RNG_LINEAGE, "det")
     rounds = []
     for n in range(gc.nsteps):

@@ -72,6 +72,29 @@ def test_exact_kernel_bit_parity_with_oracle(name):
         np.testing.assert_array_equal(sort_rows(eg), sort_rows(eo))
 
 
+@pytest.mark.parametrize("name", ["ssc_tau", "c3_mrk421", "c1_ec1x1"])
+def test_exact_kernel_bit_parity_in_place_census(name):
+    """The in-place census mode (c2d_config.census_inplace) tracks the same
+    histories: counters and census records (by key) equal the oracle's."""
+    gc = GoldenCase(name)
+    eng = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, census_inplace=1))
+    orc = OL.Oracle(gc.grid(), OL.RNG_LINEAGE, "det")
+    for n in range(gc.nsteps):
+        si = gc.step_inputs(n)
+        eng.transport_step(si)
+        assert orc.step(si) == 0
+        tg, to = eng.tallies(), orc.split()
+        np.testing.assert_array_equal(tg["counters"][list(COUNTERS)], to["counters"][list(COUNTERS)])
+        d6g, i5g, kg = eng.census()
+        d6o, i5o, ko = orc.census()
+        og, oo = np.argsort(kg), np.argsort(ko)
+        np.testing.assert_array_equal(kg[og], ko[oo])
+        np.testing.assert_array_equal(d6g[og], d6o[oo])
+        np.testing.assert_array_equal(i5g[og], i5o[oo])
+    eng.close()
+    orc.close()
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_fast_kernel_close_to_oracle(name):
     for n, eng, orc in _run_pair(name, abi.COMTOT_TABLE):

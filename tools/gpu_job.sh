@@ -1,10 +1,10 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/r03e
-timeout -k 10 600 python -u -m pytest tests/test_gpu_census_restart.py tests/test_gpu_sharding.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r03e/pytest.log 2>&1; rc=$?
-grep -E "FAIL|Error|passed|failed" gpurun_out/r03e/pytest.log | tail -15
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/r03e/bench.json 2> gpurun_out/r03e/bench.err || { tail -5 gpurun_out/r03e/bench.err; exit 1; }
-python -c "import json;d=json.load(open('gpurun_out/r03e/bench.json'));print(d['value'],d['ms_per_step'],d['roofline']['frac'],d['config']['per_step']['transport_gen0_ms'],d['config']['per_step']['transport_all_ms'])"
-timeout -k 10 400 python -u tools/census_traj.py --sources 20000000 --steps 110 > gpurun_out/r03e/c4_traj.jsonl 2> gpurun_out/r03e/c4_traj.err || { tail -5 gpurun_out/r03e/c4_traj.err; exit 1; }
-tail -1 gpurun_out/r03e/c4_traj.jsonl
+O=gpurun_out/r03g; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+grep -E "passed|failed|FAIL|Compton," $O/pytest.log | tail -8; [ $rc -eq 0 ] || exit $rc
+s() { python -c "import json,sys;d=json.load(open(sys.argv[1]));ps=d['config']['per_step'];print(sys.argv[1],'%.3g'%d['value'],'%.1f'%d['ms_per_step'],'g0 %.1f'%ps['transport_gen0_ms'],'all %.1f'%ps['transport_all_ms'],'cens %.3g'%ps.get('census_records',0),'frac %.3f'%d['roofline']['frac'], (d.get('cpu_baseline') or {}).get('value'))" $1; }
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_c3.json 2> $O/e1.err || { tail -5 $O/e1.err; exit 1; }
+s $O/bench_c3.json
+timeout -k 10 400 python bench.py --workload c4 --steps 5 --warmup 2 > $O/bench_c4.json 2> $O/e2.err || { tail -5 $O/e2.err; exit 1; }
+s $O/bench_c4.json
