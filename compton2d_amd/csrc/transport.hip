@@ -88,6 +88,38 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 #define C2D_PT_SERIES 1
 #endif
 
+/* Fast build only (the exact build keeps the oracle's c2d_math and IEEE
+ * division bit for bit):
+ *   C2D_FAST_EXP  exp by the ROCm device library (branch-free, ~42 VALU
+ *                 instead of fdlibm's ~99 with its branches and division);
+ *   C2D_FAST_DIV  a / b for b > 0 finite as a * (1/b), the reciprocal from
+ *                 v_rcp_f64 and two Newton steps (~1 ulp);
+ *   C2D_RSQ_NR    Newton steps after v_rsq_f64 in the survivors' point loop. */
+#ifndef C2D_FAST_EXP
+#define C2D_FAST_EXP 0
+#endif
+#ifndef C2D_FAST_DIV
+#define C2D_FAST_DIV 0
+#endif
+#ifndef C2D_RSQ_NR
+#define C2D_RSQ_NR 2
+#endif
+#if C2D_TABLE_COMTOT && C2D_FAST_EXP
+#define FEXP(x) exp(x)
+#else
+#define FEXP(x) c2d_exp(x)
+#endif
+#if C2D_TABLE_COMTOT && C2D_FAST_DIV
+__device__ __forceinline__ double rcp_pos(double b) {
+  double y = __builtin_amdgcn_rcp(b);
+  y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+  return __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+}
+#define FDIV_POS(a, b) ((a) * rcp_pos(b))
+#else
+#define FDIV_POS(a, b) ((a) / (b))
+#endif
+
 /* Fortran REAL literals promoted to double (src/imcvol2d_para.f:204,221,247,268,336) */
 #define F32(x) ((double)(float)(x))
 
@@ -192,6 +224,12 @@ __device__ __forceinline__ const KParams& cold(const KParams& P) {
 #else
   return P;
 #endif
+}
+
+__device__ __forceinline__ const KParams& cold_always(const KParams& P) {
+  const KParams* q = &P;
+  asm volatile("" : "+s"(q));
+  return *q;
 }
 
 /* Next draw of the packet's stream (every key change sets ctr = 0; a packet
@@ -1629,7 +1667,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
   const double rnew = __builtin_sqrt(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
   const double znew = zpre + trld * wmu;
   const double xabs = sigabs * trld;
-  const double ewnew = (xabs < 100.0) ? b.ewp * c2d_exp(-xabs) : 0.0;
+  const double ewnew = (xabs < 100.0) ? b.ewp * FEXP(-xabs) : 0.0;
   double deleabs = b.ewp - ewnew;
   if (deleabs < 1.0e-50) deleabs = 1.0e-50;
   double wmustar;
@@ -1638,7 +1676,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
   } else {
     /* one draw: mr < 1 <= ew / deleabs always holds (ew >= 1e-40) */
     const double mr = UB(b);
-    const double sstar = -c2d_log_pos(1.0 - mr * deleabs / b.ewp) / sigabs;
+    const double sstar = FDIV_POS(-c2d_log_pos(1.0 - FDIV_POS(mr * deleabs, b.ewp)), sigabs);
     const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
     wmustar = (wmu * rpre + sstar) / denom;
   }
@@ -1671,9 +1709,14 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
 }
 
 /* one shared step of the bundle (flight() for every copy on the path) */
-__device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, const GenArgs& A,
+__device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, const GenArgs& A,
                                             Bundle& b, ComCache& cc, LaneCnt& lc, Prof& pf,
                                             CensChunk* cch) {
+#ifdef C2D_HOT_RELOAD
+  const KParams& P = cold_always(P1);
+#else
+  const KParams& P = P1;
+#endif
   const double lim8 = 9.9999999e-1, lim9 = 0.999999999;
   const Geo* g = T.g;
   Pkt& p = b.p;
@@ -1738,7 +1781,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
   if (dpbsq < 1.0e-6) dpbsq = 1.0e-6;
   const double disbr = (double)inout * __builtin_sqrt(dpbsq) - disp;
   const double swmu = __builtin_sqrt(1.0 - wmu * wmu);
-  double trldb = disbr / swmu;
+  double trldb = FDIV_POS(disbr, swmu);
   const double Zr = zpre + wmu * trldb;
   const double zlow = (p.jph == 1) ? P.zmin : g->z[p.jph - 1];
   const double zup = g->z[p.jph];
@@ -1761,7 +1804,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
   double sigabs = 1.0e-40 + 1.0 * kap_cell;
   if (sigabs < 1.0e-40) sigabs = 1.0e-40;
   const double xabs = sigabs * trld;
-  const double ex = (xabs < 100.0) ? c2d_exp(-xabs) : 0.0;
+  const double ex = (xabs < 100.0) ? FEXP(-xabs) : 0.0;
   const bool two = xabs > 0.00001;      /* the absorption point is sampled */
   TP_MARK(pf, TP_GEOM);
   /* ---- probes (mode -1): collisions and weights; their absorption-point
@@ -1774,7 +1817,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
     /* collisions inside the step (ikind 3: dcol < dcen, not trldb < dcol) */
     double dpos = 0.0;
     for (;;) {
-      const double dcol = dpos + b.tau / sigsc;
+      const double dcol = dpos + FDIV_POS(b.tau, sigsc);
       if (!(dcol < p.dcen && !(trldb < dcol))) break;
       int k = (int)(UB(b) * (double)n);
       if (k > n - 1) k = n - 1;
@@ -1796,7 +1839,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
       if (deleabs < 1.0e-50) deleabs = 1.0e-50;
       nabs = n;
       dabs = deleabs;
-      qabs = deleabs / b.ewp;
+      qabs = FDIV_POS(deleabs, b.ewp);
       if (ewnew <= b.wtminp) {
         atomicAdd(&c2d_cnt_lds[C2D_CNT_KILLED], (uint32_t)n);
         b.alive = 0;
@@ -1887,7 +1930,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
        * (c2d_abspt), fresh outputs per shared step */
       const uint32_t sub = C2D_SUB_ABSPT | (uint32_t)b.g0;
 #if C2D_TABLE_COMTOT
-      const double isig = 1.0 / sigabs;
+      const double isig = FDIV_POS(1.0, sigabs);
       const double Aw = wmu * rpre, Bw = rpre * rpre;
 #endif
       for (int t = 0; t < nabs; t += 2) {
@@ -1913,8 +1956,8 @@ __device__ __forceinline__ void bundle_step(const KParams& P, const Tal& T, cons
             const double d = Bw + sstar * (2.0 * Aw + sstar);
             const double h = 0.5 * d;
             double y = __builtin_amdgcn_rsq(d);
-            y = y * __builtin_fma(-h, y * y, 1.5);
-            y = y * __builtin_fma(-h, y * y, 1.5);
+#pragma unroll
+            for (int nr = 0; nr < C2D_RSQ_NR; nr++) y = y * __builtin_fma(-h, y * y, 1.5);
             sum_prdep += dabs * ((Aw + sstar) * y) * C_LIGHT;
 #else
             const double sstar = -c2d_log_pos(1.0 - x) / sigabs;

@@ -28,7 +28,7 @@ def _last_json(out: str) -> dict:
 
 
 def test_two_ranks_on_one_gpu_match_one_rank():
-    common = ["--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    common = ["--workload", "c3", "--spinup", "1", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
     one = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--sources", "8000000"] + common,
                          capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert one.returncode == 0, one.stderr[-2000:]

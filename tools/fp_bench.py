@@ -26,9 +26,9 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
 
 
-def tiled_case(nz: int, nr: int):
+def tiled_case(nz: int, nr: int, case: str = "fp_pick", vary: bool = False):
     from golden_io import FpGoldenCase
-    c = FpGoldenCase("fp_pick")
+    c = FpGoldenCase(case)
     n = c.steps[0]
     fi = c.fp_in(n)
     src_nz, src_nr = c.nz, c.nr
@@ -40,6 +40,12 @@ def tiled_case(nz: int, nr: int):
             tile[key] = v[jj][:, kk].copy()
         else:
             tile[key] = v
+    if vary:
+        # every zone its own state: n_e and tea perturbed per zone, so no two
+        # zones walk the same temperature-search chain (gamma_bar memo, fp.hip)
+        cell = np.arange(nz * nr, dtype=np.float64).reshape(nz, nr)
+        tile["n_e"] = tile["n_e"] * (1.0 + 0.013 * (cell % 53))
+        tile["tea"] = tile["tea"] * (1.0 + 0.007 * (cell % 41))
     # same cylinder (z(nz), r(nr) fix t_esc/t_acc, update2d.f:460-461) cut into nz x nr
     # zones; with the fixture's switches (no flare, no shock injection) a zone's result
     # depends only on its own inputs, which are the fixture zone's
@@ -53,10 +59,10 @@ def tiled_case(nz: int, nr: int):
 
 def _cpu_zone(args):
     """Oracle `update` on a 1 x m strip of zones (one process)."""
-    nz, nr, cols = args
+    nz, nr, cols, case, vary = args
     sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
     import oracle_lib as OL
-    c, g, tile = tiled_case(nz, nr)
+    c, g, tile = tiled_case(nz, nr, case, vary)
     sub = {k: (v[:1, cols[0]:cols[1]].copy() if isinstance(v, np.ndarray) else v)
            for k, v in tile.items()}
     g.nz, g.nr = 1, cols[1] - cols[0]
@@ -70,12 +76,17 @@ def _cpu_zone(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--grid", type=int, default=32)
+    ap.add_argument("--nz", type=int, default=None)
+    ap.add_argument("--nr", type=int, default=None)
+    ap.add_argument("--case", default="fp_pick")
+    ap.add_argument("--vary", action="store_true", help="perturb n_e, tea per zone")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu-zones", type=int, default=16)
     args = ap.parse_args()
     from compton2d_amd.engine import Engine
-    nz = nr = args.grid
-    c, g, tile = tiled_case(nz, nr)
+    nz = args.nz or args.grid
+    nr = args.nr or args.grid
+    c, g, tile = tiled_case(nz, nr, args.case, args.vary)
     g.device = 0
     eng = Engine(g)
     eng.fp_set_config(c.constants())
@@ -96,7 +107,7 @@ def main():
         ncpu = os.cpu_count() or 1
     cores = max(1, min(16, ncpu, m))
     bounds = np.linspace(0, m, cores + 1).astype(int)
-    jobs = [(nz, nr, (int(bounds[i]), int(bounds[i + 1]))) for i in range(cores)
+    jobs = [(nz, nr, (int(bounds[i]), int(bounds[i + 1])), args.case, args.vary) for i in range(cores)
             if bounds[i + 1] > bounds[i]]
     t0 = time.perf_counter()
     with mp.get_context("spawn").Pool(len(jobs)) as pool:
@@ -119,8 +130,10 @@ def main():
                          "sample": "%d zones of row 0 on %d processes (oracle, det math), "
                                    "%.1f s (pool wall %.1f s)" % (m, len(jobs), cpu_t, cpu_wall)},
         "gpu_equals_oracle_on_sample": same,
-        "workload": "fp_pick fixture zones (reference FP inputs after one transport step) "
-                    "tiled over %dx%d" % (nz, nr),
+        "workload": "%s fixture zones (reference FP inputs after one transport step) "
+                    "tiled over %dx%d%s" % (args.case, nz, nr, ", n_e/tea varied per zone" if args.vary else ""),
+        "memo": os.environ.get("C2D_FP_MEMO", "1"),
+        "Te_new_range": [float(r["Te_new"].min()), float(r["Te_new"].max())],
     }
     print(json.dumps(out))
     eng.close()
