@@ -489,6 +489,7 @@ def main():
                          "wait_frac": pmc.get("fp_wait_frac")}
         kernels["volume_em"] = {"ms_avg": per_step.get("vem_kernel_ms", 0.0), "zones": ncell}
     rounds, moved, phys = eng.last_compaction()
+    chunks, recycled, unrecycled, held = eng.last_census_chunks()
     out = {
         "metric": METRIC,
         "value": value,
@@ -527,10 +528,14 @@ def main():
                        "records_at_end": eng.census_count(),
                        "capacity_per_gpu": ccap, "physical_slots": phys,
                        "bytes_per_record_of_capacity": CENSUS_BYTES[inplace],
-                       "layout": ("in place: one SoA, dead slots compacted (c2d_device.hpp "
-                                  "C2D_CENS_DEAD)" if inplace else
+                       "layout": ("chunked: one SoA in 1024-record chunks, chunks of finished "
+                                  "census sources refilled within the step (c2d_device.hpp C2D_CCHUNK)"
+                                  if inplace else
                                   "double-buffered SoA (in + out), chunk tails compacted"),
-                       "last_compaction_rounds": rounds, "last_compaction_moved": moved},
+                       "last_close_rounds": rounds, "last_close_moved": moved,
+                       **({"chunks": chunks, "chunks_recycled_last_step": recycled,
+                           "chunks_not_counted_down_last_step": unrecycled, "chunks_held": held}
+                          if inplace else {})},
             "packet_steps_timed": steps_global,
             "per_step": per_step,
         },

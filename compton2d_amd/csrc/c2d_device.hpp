@@ -51,15 +51,26 @@ struct SpecDev {             /* file_sp table (imcsurf2d_para.f:544-685) */
  * with the same c2d_acos / c2d_cos (c2d_census_export / _import), so the
  * records it sees are the ones the fast kernel wrote before this encoding. */
 #define C2D_CENS_ESW (1u << 24)
-/* In-place census (one SoA per context, read and written by the same step):
- * the census packets of the previous step are the step's first items
- * [0, n_cin); the recombined copy of census item i writes its next-step
- * record back into slot i, every other census write appends at or after
- * n_cin.  A census item that ends without a census write, and the unused
- * tail of a wave's append chunk, are marked dead (bins = C2D_CENS_DEAD); the
- * host closes the dead slots below the live count after the step
- * (capi.cpp census_compact), so the census stays dense at 64 B per record. */
+/* Double-buffered census: a wave's unused tail of its last append chunk is
+ * marked dead (bins = C2D_CENS_DEAD) and closed by the host's compaction
+ * (capi.cpp census_compact). */
 #define C2D_CENS_DEAD (1u << 31)
+/* Chunked census (census_inplace = 1: one SoA per context, 64 B per record):
+ * the SoA is cut into chunks of C2D_CCHUNK slots.  The census is a list of
+ * chunks, all full but the last: census item i lives at slot
+ * clist[i >> 10] * 1024 + (i & 1023).  A step appends its census writes into
+ * wave-private chunks taken from the free pool; the bundle kernel counts the
+ * live sources of each census chunk it works on, and a chunk whose sources
+ * have all finished goes to the wave's stack of free chunks, taken before
+ * the pool; a full stack, and the stack a wave leaves at its end, go to the
+ * shared relist, taken after the stack and before the pool (by every wave of
+ * the step's launches).  After the step the partly filled chunks (one per wave slot at most)
+ * are packed into full ones and the chunks taken become the next list
+ * (capi.cpp census_chunks_close). */
+#define C2D_CCHUNK 1024
+#define C2D_CCHUNK_LOG 10
+#define C2D_CT_TRACK 16      /* census chunks a wave counts down at once (pow 2) */
+#define C2D_CT_STACK 8       /* freed chunks a wave holds for its next appends */
 struct CensusSoA {
   double* rpre; double* zpre; double* wmu; double* phi; double* ew; double* xnu;
   uint32_t* jk;      /* jph << 16 | kph (1-based)                  */
@@ -153,9 +164,13 @@ __device__ __forceinline__ void gor(int32_t* p, int32_t v) {
  * packet-step; the bundle kernel one per shared step of all copies on the
  * path.  The roofline's algorithmic bytes are priced on it. */
 #define C2D_CNT_PATHS_INT 10
-/* internal counter slot: census slots marked dead by the bundle kernel
- * (census items that did not return to the census + unused chunk tails) */
+/* internal counter slots: census slots marked dead (double-buffered census:
+ * the unused tails of the append chunks); chunked census: chunks recycled
+ * within the step, and census chunks whose sources the bundle kernel could
+ * not count down (all C2D_CT_TRACK slots busy, or the free stack full) */
 #define C2D_CNT_DEAD_INT 12
+#define C2D_CNT_CREUSE_INT 13
+#define C2D_CNT_CLOST_INT 14
 
 struct KParams {
   int32_t nz, nr, ncell, nphtotal, nph_lc, nmu;
@@ -186,13 +201,23 @@ struct KParams {
                                    reference evaluates comtot; 16 KB per cell)               */
   double comtab_du_inv;
   double egg_min;            /* E_field(1)^2 / E_field(2): n_field threshold (imctrk2d.f:547-556) */
-  /* census: cin and cout are the same in-place SoA (C2D_CENS_DEAD); cap_cout is
-   * its physical size (census_capacity + the slack the append chunks need) */
+  /* census: double-buffered cin -> cout (clist null), or one chunked SoA
+   * (cin == cout, clist = the input's chunk list); cap_cout = physical slots */
   CensusSoA cin, cout;
   int64_t n_cin, cap_cout;
-  uint32_t cens_chunk;       /* census slots per wave reservation (bundle kernel) */
-  int32_t cens_inplace;      /* 1: cin == cout, census items rewrite their own slot */
+  uint32_t cens_chunk;       /* census slots per wave reservation */
   unsigned long long* n_cout;
+  const int32_t* clist;      /* chunked: census item i at clist[i >> 10] * 1024 + (i & 1023) */
+  const int32_t* pool;       /* chunked: free chunks at the step's start ...            */
+  const unsigned long long* pool_n;   /* ... how many                                    */
+  unsigned long long* pool_head;      /* ... taken so far                                */
+  int32_t* out_list;         /* chunked: every chunk the step took, in order of taking   */
+  unsigned long long* n_out;
+  int32_t* relist;           /* chunked: freed chunks waves handed on (-1: not yet written) */
+  unsigned long long* n_relist;
+  unsigned long long* relist_head;
+  int64_t* cstate;           /* [2 * wave slot]: its partly filled chunk (first slot or -1,
+                                used) from launch to launch; closed after the step      */
   /* events */
   double* ev;
   int64_t cap_ev;

@@ -54,7 +54,8 @@ extern "C" int c2d_launch_tridag(const double* a, const double* b, const double*
 namespace {
 
 /* CTL_EVSH: the C2D_EV_SHARDS event counters, one per 128-B line */
-enum { CTL_WORK = 0, CTL_NCOUT = 1, CTL_N2 = 3, CTL_N3 = 4, CTL_NPK = 5, CTL_CNT = 8,
+enum { CTL_WORK = 0, CTL_NCOUT = 1, CTL_POOLH = 2, CTL_N2 = 3, CTL_N3 = 4, CTL_NPK = 5,
+       CTL_NOUT = 6, CTL_POOLN = 7, CTL_CNT = 8, CTL_RELN = CTL_CNT + C2D_NCOUNTERS, CTL_RELH,
        CTL_EVSH = 32, CTL_PROF = CTL_EVSH + C2D_EV_SHARDS * C2D_EV_SHARD_STRIDE,
        CTL_WSH = CTL_PROF + C2D_TR_PROF_WORDS,
        CTL_WORDS = CTL_WSH + C2D_WORK_SHARDS * C2D_EV_SHARD_STRIDE };
@@ -112,11 +113,29 @@ struct c2d_ctx {
   /* generation 0 as probe bundles (c2d_bundle_kernel): its LDS and grid */
   int bundle = 1, bundle_grid = 0;
   size_t bundle_lds = 0;
-  /* census SoA(s) of cens_phys records each: census_capacity + one append
-   * chunk per wave (+ 1/16 of the capacity in place, c2d_device.hpp
-   * C2D_CENS_DEAD); the compaction's work lists (cscan_cap slots each) */
+  /* census SoA(s) of cens_phys records each.  Double-buffered:
+   * census_capacity + one append chunk per wave slot; the compaction's work
+   * lists (cscan_cap slots each).  Chunked (census_inplace, c2d_device.hpp
+   * C2D_CCHUNK): nchunks chunks, the census's chunk list (clist[ccur],
+   * n_clist chunks, all full but the last) and the next step's. */
   int64_t cens_phys = 0;
   uint32_t cens_chunk = 64;
+  int64_t n_ws = 0;              /* wave slots: the largest grid's waves (cstate entries) */
+  int64_t* cstate = nullptr;     /* [n_ws][2] partly filled chunk per wave slot            */
+  int chunked = 0;
+  int64_t nchunks = 0;
+  int32_t* clist[2] = {nullptr, nullptr};
+  int ccur = 0;
+  int64_t n_clist = 0;
+  int32_t* pool = nullptr;       /* [nchunks] free chunks at the step's start */
+  int32_t* out_list = nullptr;   /* [nchunks] chunks the step took            */
+  int32_t* relist = nullptr;     /* [nchunks] chunks freed and handed on      */
+  uint8_t* cflag = nullptr;      /* [nchunks] in-use / partly-filled marks    */
+  int32_t* part_id = nullptr;    /* [n_ws] partly filled chunks ...            */
+  int64_t* part_off = nullptr;   /* [n_ws + 1] ... and their records' prefix   */
+  uint64_t* tmp_rec = nullptr;   /* packed records (moves, exports)           */
+  int64_t tmp_cap = 0;
+  int64_t last_creuse = 0, last_clost = 0;
   int64_t* cscan = nullptr;      /* [2][cscan_cap]: dead slots below W, live slots at/above W */
   int64_t cscan_cap = 0;
   uint32_t* ctile_cnt = nullptr;           /* [tiles][2] holes, sources per tile       */
@@ -368,28 +387,48 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
     c->bundle_grid = c->n_cu * std::max(1, b0);
   }
   {
-    /* the census.  Append chunks per wave reservation: <= 1024 slots, >= 64
-     * (one reservation covers a wave's census lanes), and their tails (at
-     * most one per wave) at most 1/8 of the capacity.  The physical size
-     * adds room for every wave's chunk tail (and, in place, 1/16 of the
-     * capacity for appends that land before the dead slots are closed), so
-     * a census whose compacted size fits the capacity does not overflow. */
+    /* the census.  A wave slot keeps one partly filled append chunk over
+     * the step's launches (cstate), so a step leaves at most n_ws of them. */
     const int64_t ccap = std::max<int64_t>(cfg->census_capacity, 1);
-    const int64_t waves = (int64_t)c->bundle_grid * (C2D_TR_BLOCK / 64);
-    int64_t ch = 1024;
-    while (ch > 64 && ch * waves * 8 > ccap) ch >>= 1;
-    c->cens_chunk = (uint32_t)ch;
-    c->cens_phys = ccap + waves * ch + (cfg->census_inplace ? ccap / 16 : 0) + 64;
-    for (int b = 0; b < (cfg->census_inplace ? 1 : 2); b++) {
+    c->n_ws = (int64_t)std::max(c->bundle_grid, c->max_grid) * (C2D_TR_BLOCK / 64);
+    HIPCHK(c, dalloc(&c->cstate, 2 * (size_t)c->n_ws));
+    HIPCHK(c, hipMemset(c->cstate, 0xff, 2 * sizeof(int64_t) * c->n_ws));
+    c->chunked = cfg->census_inplace ? 1 : 0;
+    if (c->chunked) {
+      /* chunked: the chunks of the census, the wave slots' partly filled
+       * ones, and 1/16 of the capacity for chunks whose sources are still
+       * in flight when the waves need new ones (c2d_device.hpp) */
+      c->cens_chunk = C2D_CCHUNK;
+      c->nchunks = (ccap + C2D_CCHUNK - 1) / C2D_CCHUNK + (ccap / 16 + C2D_CCHUNK - 1) / C2D_CCHUNK +
+                   4 * c->n_ws + 64;
+      c->cens_phys = c->nchunks * C2D_CCHUNK;
+      for (int b = 0; b < 2; b++) HIPCHK(c, dalloc(&c->clist[b], (size_t)c->nchunks));
+      HIPCHK(c, dalloc(&c->pool, (size_t)c->nchunks));
+      HIPCHK(c, dalloc(&c->out_list, (size_t)c->nchunks));
+      HIPCHK(c, dalloc(&c->relist, (size_t)c->nchunks));
+      HIPCHK(c, dalloc(&c->cflag, (size_t)c->nchunks));
+      HIPCHK(c, dalloc(&c->part_id, (size_t)c->n_ws));
+      HIPCHK(c, dalloc(&c->part_off, (size_t)c->n_ws + 1));
+    } else {
+      /* double-buffered: append chunks <= 1024 slots, >= 64 (one reservation
+       * covers a wave's census lanes), their tails at most 1/8 of the
+       * capacity; the physical size adds room for every tail, so a census
+       * whose compacted size fits the capacity does not overflow */
+      int64_t ch = 1024;
+      while (ch > 64 && ch * c->n_ws * 8 > ccap) ch >>= 1;
+      c->cens_chunk = (uint32_t)ch;
+      c->cens_phys = ccap + c->n_ws * ch + 64;
+      c->cscan_cap = std::min<int64_t>(int64_t(1) << 27, std::max<int64_t>(int64_t(1) << 16, ccap / 16));
+      /* test knob: a short work list forces many compaction rounds */
+      if (const char* e = getenv("C2D_COMPACT_LIST")) c->cscan_cap = std::max<long long>(1, atoll(e));
+      HIPCHK(c, dalloc(&c->cscan, 2 * (size_t)c->cscan_cap));
+    }
+    for (int b = 0; b < (c->chunked ? 1 : 2); b++) {
       for (int f = 0; f < 6; f++) HIPCHK(c, dalloc(&c->cens[b].d[f], (size_t)c->cens_phys));
       HIPCHK(c, dalloc(&c->cens[b].jk, (size_t)c->cens_phys));
       HIPCHK(c, dalloc(&c->cens[b].bins, (size_t)c->cens_phys));
       HIPCHK(c, dalloc(&c->cens[b].key, (size_t)c->cens_phys));
     }
-    c->cscan_cap = std::min<int64_t>(int64_t(1) << 27, std::max<int64_t>(int64_t(1) << 16, ccap / 16));
-    /* test knob: a short work list forces many compaction rounds */
-    if (const char* e = getenv("C2D_COMPACT_LIST")) c->cscan_cap = std::max<long long>(1, atoll(e));
-    HIPCHK(c, dalloc(&c->cscan, 2 * (size_t)c->cscan_cap));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return C2D_OK;
@@ -405,7 +444,8 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
                   c->Pnt, c->n_e, c->vfrac, c->ewsv, c->surf_ew, c->surf_tbb, c->tbbl,
                   c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comS,
                   c->ev, c->q2[0], c->q2[1], c->q3[0], c->q3[1], c->T_own, c->nf_rep, c->ctl, c->derr, c->dP,
-                  c->cscan, c->ctile_cnt, c->ctile_off};
+                  c->cscan, c->ctile_cnt, c->ctile_off, c->cstate, c->clist[0], c->clist[1],
+                  c->pool, c->out_list, c->relist, c->cflag, c->part_id, c->part_off, c->tmp_rec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int b = 0; b < 2; b++) {
@@ -779,6 +819,246 @@ __global__ void __launch_bounds__(256) c2d_census_fill(CensusSoA c, const int64_
   }
 }
 
+/* ---- census records: packed 8-word form (C2D_CENSUS_REC_WORDS), bit-exact ---- */
+__device__ __forceinline__ void rec_pack(const CensusSoA& cs, int64_t s, uint64_t* r) {
+  r[0] = __double_as_longlong(cs.rpre[s]);
+  r[1] = __double_as_longlong(cs.zpre[s]);
+  r[2] = __double_as_longlong(cs.wmu[s]);
+  r[3] = __double_as_longlong(cs.phi[s]);
+  r[4] = __double_as_longlong(cs.ew[s]);
+  r[5] = __double_as_longlong(cs.xnu[s]);
+  r[6] = (uint64_t)cs.jk[s] | ((uint64_t)cs.bins[s] << 32);
+  r[7] = cs.key[s];
+}
+__device__ __forceinline__ void rec_unpack(const CensusSoA& cs, int64_t d, const uint64_t* r) {
+  cs.rpre[d] = __longlong_as_double(r[0]);
+  cs.zpre[d] = __longlong_as_double(r[1]);
+  cs.wmu[d] = __longlong_as_double(r[2]);
+  cs.phi[d] = __longlong_as_double(r[3]);
+  cs.ew[d] = __longlong_as_double(r[4]);
+  cs.xnu[d] = __longlong_as_double(r[5]);
+  cs.jk[d] = (uint32_t)(r[6] & 0xffffffffull);
+  cs.bins[d] = (uint32_t)(r[6] >> 32);
+  cs.key[d] = r[7];
+}
+/* census record i -> its slot (chunked: through the chunk list) */
+__device__ __forceinline__ int64_t cens_slot(const int32_t* clist, int64_t i) {
+  return clist ? ((int64_t)clist[i >> C2D_CCHUNK_LOG] << C2D_CCHUNK_LOG) + (i & (C2D_CCHUNK - 1)) : i;
+}
+
+/* ---- chunked census (c2d_device.hpp C2D_CCHUNK) ---- */
+/* mark the chunks of a list */
+__global__ void __launch_bounds__(256) c2d_chunk_mark(const int32_t* __restrict__ list, int64_t n,
+                                                      uint8_t* __restrict__ flag) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    flag[list[i]] = 1;
+}
+
+/* append the ids i < n with flag[i] == 0 (pool), or the entries of list with
+ * flag[list[j]] == 0 (list != null), to out; one atomic per wave */
+__global__ void __launch_bounds__(256) c2d_chunk_select(const int32_t* __restrict__ list, int64_t n,
+                                                        const uint8_t* __restrict__ flag,
+                                                        int32_t* __restrict__ out,
+                                                        unsigned long long* __restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = b + threadIdx.x;
+    int32_t id = 0;
+    bool keep = false;
+    if (i < n) {
+      id = list ? list[i] : (int32_t)i;
+      keep = flag[id] == 0;
+    }
+    const unsigned long long m = __ballot(keep);
+    if (m == 0ull) continue;
+    const int leader = __ffsll((long long)m) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(cnt, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader);
+    if (keep) out[base + __popcll(m & ((1ull << lane) - 1ull))] = id;
+  }
+}
+
+/* double-buffered census after the step: the unused tail of each wave
+ * slot's last chunk (one workgroup per slot) is marked dead and counted */
+__global__ void __launch_bounds__(256) c2d_chunk_tails(const int64_t* __restrict__ cstate, uint32_t chunk,
+                                                       int64_t cap, uint32_t* __restrict__ bins,
+                                                       unsigned long long* __restrict__ dead) {
+  const int64_t base = cstate[2 * blockIdx.x], used = cstate[2 * blockIdx.x + 1];
+  if (base < 0 || used <= 0 || used >= (int64_t)chunk || base >= cap) return;
+  const int64_t t1 = base + chunk < cap ? base + chunk : cap;
+  for (int64_t s = base + used + threadIdx.x; s < t1; s += blockDim.x) bins[s] = C2D_CENS_DEAD;
+  if (threadIdx.x == 0 && t1 > base + used) atomicAdd(dead, (unsigned long long)(t1 - base - used));
+}
+
+/* chunked census after the step: the wave slots' partly filled chunks, in
+ * slot order: ids, exclusive prefix of their records (part_off[np] = total),
+ * flags; out = {np, total}.  One workgroup of 1024. */
+__global__ void __launch_bounds__(1024) c2d_chunk_partials(const int64_t* __restrict__ cstate, int64_t n_ws,
+                                                           uint32_t chunk, int64_t cap,
+                                                           int32_t* __restrict__ part_id,
+                                                           int64_t* __restrict__ part_off,
+                                                           uint8_t* __restrict__ flag,
+                                                           unsigned long long* __restrict__ out) {
+  __shared__ int64_t sc[1024], su[1024];
+  __shared__ int64_t np_s, tot_s;
+  const int t = threadIdx.x;
+  if (t == 0) { np_s = 0; tot_s = 0; }
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < n_ws; b0 += 1024) {
+    const int64_t i = b0 + t;
+    int64_t base = -1, used = 0;
+    if (i < n_ws) {
+      base = cstate[2 * i];
+      used = cstate[2 * i + 1];
+    }
+    const bool part = base >= 0 && used > 0 && used < (int64_t)chunk && base < cap;
+    sc[t] = part ? 1 : 0;
+    su[t] = part ? used : 0;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {     /* inclusive scan */
+      const int64_t a = t >= off ? sc[t - off] : 0, u = t >= off ? su[t - off] : 0;
+      __syncthreads();
+      sc[t] += a;
+      su[t] += u;
+      __syncthreads();
+    }
+    if (part) {
+      const int64_t k = np_s + sc[t] - 1;
+      part_id[k] = (int32_t)(base >> C2D_CCHUNK_LOG);
+      part_off[k] = tot_s + su[t] - used;
+      flag[base >> C2D_CCHUNK_LOG] = 1;
+    }
+    __syncthreads();
+    if (t == 1023) { np_s += sc[t]; tot_s += su[t]; }
+    __syncthreads();
+  }
+  if (t == 0) {
+    part_off[np_s] = tot_s;
+    out[0] = (unsigned long long)np_s;
+    out[1] = (unsigned long long)tot_s;
+  }
+}
+
+/* packing the partly filled chunks, in two phases per batch [r0, r1) of
+ * their records (record r goes to slot r of the chunks part_id[0, ...):
+ * never after its source, so a batch reads nothing an earlier one wrote) */
+__global__ void __launch_bounds__(256) c2d_chunk_gather(CensusSoA cs, const int32_t* __restrict__ part_id,
+                                                        const int64_t* __restrict__ part_off, int64_t r0,
+                                                        int64_t r1, uint64_t* __restrict__ tmp) {
+  const int64_t j = blockIdx.x;
+  const int64_t off = part_off[j], fill = part_off[j + 1] - off;
+  for (int64_t s = threadIdx.x; s < fill; s += blockDim.x) {
+    const int64_t r = off + s;
+    if (r < r0 || r >= r1) continue;
+    rec_pack(cs, ((int64_t)part_id[j] << C2D_CCHUNK_LOG) + s, tmp + (r - r0) * C2D_CENSUS_REC_WORDS);
+  }
+}
+__global__ void __launch_bounds__(256) c2d_chunk_scatter(CensusSoA cs, const int32_t* __restrict__ part_id,
+                                                         int64_t r0, int64_t r1,
+                                                         const uint64_t* __restrict__ tmp) {
+  for (int64_t r = r0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < r1;
+       r += (int64_t)gridDim.x * blockDim.x)
+    rec_unpack(cs, ((int64_t)part_id[r >> C2D_CCHUNK_LOG] << C2D_CCHUNK_LOG) + (r & (C2D_CCHUNK - 1)),
+               tmp + (r - r0) * C2D_CENSUS_REC_WORDS);
+}
+
+static int ensure_tmp(c2d_ctx* c, int64_t want) {
+  want = std::max<int64_t>(want, 1 << 16);
+  if (c->tmp_cap >= want) return C2D_OK;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->tmp_rec) (void)hipFree(c->tmp_rec);
+  c->tmp_rec = nullptr;
+  c->tmp_cap = 0;
+  HIPCHK(c, dalloc(&c->tmp_rec, (size_t)want * C2D_CENSUS_REC_WORDS));
+  c->tmp_cap = want;
+  return C2D_OK;
+}
+
+/* the free chunks (not in the census's list) into the pool; returns their
+ * number (the pool counter at ctl[CTL_POOLN]) */
+static int chunk_pool_build(c2d_ctx* c, int64_t* n_free) {
+  HIPCHK(c, hipMemsetAsync(c->cflag, 0, (size_t)c->nchunks, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->ctl + CTL_POOLN, 0, sizeof(unsigned long long), c->stream));
+  const int gm = (int)std::max<int64_t>(1, std::min<int64_t>((c->n_clist + 255) / 256, (int64_t)c->n_cu * 8));
+  if (c->n_clist > 0)
+    hipLaunchKernelGGL(c2d_chunk_mark, dim3(gm), dim3(256), 0, c->stream, c->clist[c->ccur], c->n_clist,
+                       c->cflag);
+  const int gp = (int)std::max<int64_t>(1, std::min<int64_t>((c->nchunks + 255) / 256, (int64_t)c->n_cu * 8));
+  hipLaunchKernelGGL(c2d_chunk_select, dim3(gp), dim3(256), 0, c->stream, (const int32_t*)nullptr,
+                     c->nchunks, c->cflag, c->pool, c->ctl + CTL_POOLN);
+  HIPCHK(c, hipGetLastError());
+  if (n_free) {
+    unsigned long long n = 0;
+    HIPCHK(c, hipMemcpyAsync(&n, c->ctl + CTL_POOLN, sizeof n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *n_free = (int64_t)n;
+  }
+  return C2D_OK;
+}
+
+/* after the last generation (chunked): pack the partly filled chunks, and
+ * the chunks taken (those emptied by the packing aside) become the census's
+ * list, the packed ones last.  *n_records = the census's records. */
+static int census_chunks_close(c2d_ctx* c, int64_t* n_records) {
+  HIPCHK(c, hipMemsetAsync(c->cflag, 0, (size_t)c->nchunks, c->stream));
+  hipLaunchKernelGGL(c2d_chunk_partials, dim3(1), dim3(1024), 0, c->stream, c->cstate, c->n_ws,
+                     (uint32_t)C2D_CCHUNK, c->cens_phys, c->part_id, c->part_off, c->cflag,
+                     c->ctl + CTL_NCOUT);      /* {np, total} into the (unused) NCOUT, POOLH words */
+  HIPCHK(c, hipGetLastError());
+  unsigned long long pr[2], n_out = 0;
+  HIPCHK(c, hipMemcpyAsync(pr, c->ctl + CTL_NCOUT, sizeof pr, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&n_out, c->ctl + CTL_NOUT, sizeof n_out, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int64_t np = (int64_t)pr[0], tot = (int64_t)pr[1];
+  if (np > c->n_ws || (int64_t)n_out > c->nchunks || np > (int64_t)n_out)
+    return fail(c, C2D_E_STATE, "census chunks: %lld partly filled of %llu taken", (long long)np, n_out);
+  const CensusSoA cs = c->cens[0].soa();
+  c->last_compact_rounds = 0;
+  c->last_compact_moved = 0;
+  if (np > 1) {
+    int rc = ensure_tmp(c, std::min<int64_t>(tot, int64_t(1) << 22));
+    if (rc) return rc;
+    int64_t B = c->tmp_cap;
+    /* test knob: short batches force many two-phase rounds */
+    if (const char* e = getenv("C2D_CHUNK_BATCH")) B = std::max<int64_t>(1, std::min<int64_t>(B, atoll(e)));
+    for (int64_t r0 = 0; r0 < tot; r0 += B) {
+      const int64_t r1 = std::min(tot, r0 + B);
+      hipLaunchKernelGGL(c2d_chunk_gather, dim3((unsigned)np), dim3(256), 0, c->stream, cs, c->part_id,
+                         c->part_off, r0, r1, c->tmp_rec);
+      const int g = (int)std::min<int64_t>((r1 - r0 + 255) / 256, (int64_t)c->n_cu * 8);
+      hipLaunchKernelGGL(c2d_chunk_scatter, dim3(g), dim3(256), 0, c->stream, cs, c->part_id, r0, r1,
+                         c->tmp_rec);
+      HIPCHK(c, hipGetLastError());
+      c->last_compact_rounds++;
+    }
+    c->last_compact_moved = tot;
+  }
+  /* the full chunks taken, then the packed ones */
+  const int nxt = 1 - c->ccur;
+  const int64_t kp = (tot + C2D_CCHUNK - 1) / C2D_CCHUNK;
+  HIPCHK(c, hipMemsetAsync(c->ctl + CTL_NOUT, 0, sizeof(unsigned long long), c->stream));
+  if (n_out > 0) {
+    const int g = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)n_out + 255) / 256, (int64_t)c->n_cu * 8));
+    hipLaunchKernelGGL(c2d_chunk_select, dim3(g), dim3(256), 0, c->stream, c->out_list, (int64_t)n_out,
+                       c->cflag, c->clist[nxt], c->ctl + CTL_NOUT);
+    HIPCHK(c, hipGetLastError());
+  }
+  unsigned long long n_full = 0;
+  HIPCHK(c, hipMemcpyAsync(&n_full, c->ctl + CTL_NOUT, sizeof n_full, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if ((int64_t)n_full != (int64_t)n_out - np)
+    return fail(c, C2D_E_STATE, "census chunks: %llu full of %llu taken, %lld partly filled", n_full, n_out,
+                (long long)np);
+  if (kp > 0)
+    HIPCHK(c, hipMemcpyAsync(c->clist[nxt] + n_full, c->part_id, sizeof(int32_t) * kp,
+                             hipMemcpyDeviceToDevice, c->stream));
+  c->ccur = nxt;
+  c->n_clist = (int64_t)n_full + kp;
+  *n_records = (int64_t)n_full * C2D_CCHUNK + tot;
+  return C2D_OK;
+}
+
 static int census_compact(c2d_ctx* c, const DevCensus& cb, int64_t R, int64_t W) {
   c->last_compact_rounds = 0;
   c->last_compact_moved = 0;
@@ -845,18 +1125,27 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   P.comtab = c->comtab;
   P.comtab_du_inv = (double)(C2D_COMTAB_N - 1) / (C2D_COMTAB_U1 - C2D_COMTAB_U0);
   P.egg_min = c->egg_min;
-  /* last step's census records are this step's first items.  In place
-   * (census_inplace) they are read and rewritten in one SoA and appends start
-   * after them; double-buffered the step writes the other buffer from 0. */
-  const int inplace = cfg.census_inplace ? 1 : 0;
-  const int out_buf = inplace ? 0 : 1 - c->cur;
+  /* last step's census records are this step's first items.  Chunked
+   * (census_inplace) they are read through the chunk list and the step's
+   * census writes fill free chunks of the same SoA; double-buffered the step
+   * writes the other buffer from 0. */
+  const int out_buf = c->chunked ? 0 : 1 - c->cur;
   P.cin = c->cens[c->cur].soa();
   P.cout = c->cens[out_buf].soa();
   P.n_cin = c->n_census;
   P.cap_cout = c->cens_phys;
   P.cens_chunk = c->cens_chunk;
-  P.cens_inplace = inplace;
   P.n_cout = c->ctl + CTL_NCOUT;
+  P.clist = c->chunked ? c->clist[c->ccur] : nullptr;
+  P.pool = c->pool;
+  P.pool_n = c->ctl + CTL_POOLN;
+  P.pool_head = c->ctl + CTL_POOLH;
+  P.out_list = c->out_list;
+  P.n_out = c->ctl + CTL_NOUT;
+  P.relist = c->relist;
+  P.n_relist = c->ctl + CTL_RELN;
+  P.relist_head = c->ctl + CTL_RELH;
+  P.cstate = c->cstate;
   P.ev = c->ev; P.cap_ev = cfg.event_capacity;
   P.n_ev_sh = c->ctl + CTL_EVSH;
   c->ev_cap_sh = std::max<int64_t>(cfg.event_capacity / C2D_EV_SHARDS, 0);
@@ -907,10 +1196,11 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   HIPCHK(c, hipMemsetAsync(c->nf_rep, 0, sizeof(double) * C2D_NF_REPL * c->ncell * C2D_NPHFIELD,
                            c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl, 0, sizeof(unsigned long long) * CTL_WORDS, c->stream));
-  {
-    const unsigned long long ncin = inplace ? (unsigned long long)c->n_census : 0ull;   /* appends start here */
-    HIPCHK(c, hipMemcpyAsync(c->ctl + CTL_NCOUT, &ncin, sizeof ncin, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemsetAsync(c->cstate, 0xff, 2 * sizeof(int64_t) * c->n_ws, c->stream));  /* no chunk */
+  if (c->chunked) {
+    HIPCHK(c, hipMemsetAsync(c->relist, 0xff, sizeof(int32_t) * c->nchunks, c->stream));
+    int rc = chunk_pool_build(c, nullptr);
+    if (rc) return rc;
   }
   HIPCHK(c, hipMemsetAsync(c->derr, 0, sizeof(int32_t), c->stream));
 
@@ -948,8 +1238,12 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     HIPCHK(c, hipEventRecord(c->ev_g0t, c->stream));
     if (A.n_items > 0) {
       auto launch_b = fast ? c2d_launch_bundle_fast : c2d_launch_bundle_exact;
+      int64_t gmax = c->bundle_grid;
+      /* test knob: a few workgroups, so every wave runs many work chunks and
+       * crosses chunk boundaries within one refill */
+      if (const char* e = getenv("C2D_BUNDLE_GRID")) gmax = std::max<int64_t>(1, std::min<int64_t>(gmax, atoll(e)));
       const int grid = (int)std::max<int64_t>(
-          1, std::min<int64_t>(c->bundle_grid, (A.n_items + C2D_TR_BLOCK - 1) / C2D_TR_BLOCK));
+          1, std::min<int64_t>(gmax, (A.n_items + C2D_TR_BLOCK - 1) / C2D_TR_BLOCK));
       int rc = launch_b(c->dP, &A, grid, c->bundle_lds, c->stream);
       if (rc) return fail(c, C2D_E_HIP, "bundle launch (gen 0): %s", hipGetErrorString((hipError_t)rc));
       launches++;
@@ -995,32 +1289,55 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     gen++;
   }
-  /* close the in-place census's dead slots (C2D_CENS_DEAD): census items that
-   * did not return to the census and the unused tails of the append chunks */
+  /* close the census: chunked, pack the partly filled chunks into the next
+   * chunk list; double-buffered, mark the unused chunk tails dead and close
+   * the dead slots below the live count */
   int64_t cens_live = 0;
   {
-    unsigned long long cw[2];
+    if (!c->chunked && c->n_ws > 0) {
+      hipLaunchKernelGGL(c2d_chunk_tails, dim3((unsigned)c->n_ws), dim3(256), 0, c->stream, c->cstate,
+                         c->cens_chunk, c->cens_phys, c->cens[out_buf].bins,
+                         c->ctl + CTL_CNT + C2D_CNT_DEAD_INT);
+      HIPCHK(c, hipGetLastError());
+    }
+    unsigned long long cw[3];
     int32_t herr0 = 0;
     HIPCHK(c, hipMemcpyAsync(cw, c->ctl + CTL_NCOUT, sizeof cw[0], hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(cw + 1, c->ctl + CTL_CNT + C2D_CNT_DEAD_INT, sizeof cw[1],
                              hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(cw + 2, c->ctl + CTL_CNT + C2D_CNT_CENSUS, sizeof cw[2],
+                             hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&herr0, c->derr, sizeof herr0, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     /* a record slot beyond the physical census: the census is incomplete */
-    if (herr0 & ERR_CENSUS)
+    if (herr0 & ERR_CENSUS) {
+      if (c->chunked)
+        return fail(c, C2D_E_CENSUS_OVERFLOW, "census overflow: no free census chunk left (%lld chunks "
+                    "of %d for capacity %lld)", (long long)c->nchunks, C2D_CCHUNK, (long long)cfg.census_capacity);
       return fail(c, C2D_E_CENSUS_OVERFLOW, "census overflow: more than %lld records before "
                   "compaction (capacity %lld)", (long long)c->cens_phys, (long long)cfg.census_capacity);
-    /* reservations past the physical end are chunk tails (never written) */
-    const int64_t R = std::min<int64_t>((int64_t)cw[0], c->cens_phys);
-    const int64_t D = (int64_t)cw[1];
-    cens_live = R - D;
-    if (cens_live < 0 || D > R)
-      return fail(c, C2D_E_STATE, "census compaction: %lld dead of %lld slots", (long long)D, (long long)R);
-    if (cens_live > cfg.census_capacity)
-      return fail(c, C2D_E_CENSUS_OVERFLOW, "too many photons: census %lld > capacity %lld",
-                  (long long)cens_live, (long long)cfg.census_capacity);
-    int rc = census_compact(c, c->cens[out_buf], R, cens_live);
-    if (rc) return rc;
+    }
+    if (c->chunked) {
+      int rc = census_chunks_close(c, &cens_live);
+      if (rc) return rc;
+      if (cens_live != (int64_t)cw[2])
+        return fail(c, C2D_E_STATE, "census chunks hold %lld records, %llu written", (long long)cens_live, cw[2]);
+      if (cens_live > cfg.census_capacity)
+        return fail(c, C2D_E_CENSUS_OVERFLOW, "too many photons: census %lld > capacity %lld",
+                    (long long)cens_live, (long long)cfg.census_capacity);
+    } else {
+      /* reservations past the physical end are chunk tails (never written) */
+      const int64_t R = std::min<int64_t>((int64_t)cw[0], c->cens_phys);
+      const int64_t D = (int64_t)cw[1];
+      cens_live = R - D;
+      if (cens_live < 0 || D > R)
+        return fail(c, C2D_E_STATE, "census compaction: %lld dead of %lld slots", (long long)D, (long long)R);
+      if (cens_live > cfg.census_capacity)
+        return fail(c, C2D_E_CENSUS_OVERFLOW, "too many photons: census %lld > capacity %lld",
+                    (long long)cens_live, (long long)cfg.census_capacity);
+      int rc = census_compact(c, c->cens[out_buf], R, cens_live);
+      if (rc) return rc;
+    }
   }
   {
     const int64_t n = (int64_t)c->ncell * C2D_NPHFIELD;
@@ -1055,6 +1372,10 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   c->last_all_paths = (int64_t)ctl[CTL_CNT + C2D_CNT_PATHS_INT];
   hc[C2D_CNT_PATHS_INT] = 0.0;              /* internal: not tally counters */
   hc[C2D_CNT_DEAD_INT] = 0.0;
+  c->last_creuse = (int64_t)ctl[CTL_CNT + C2D_CNT_CREUSE_INT];
+  c->last_clost = (int64_t)ctl[CTL_CNT + C2D_CNT_CLOST_INT];
+  hc[C2D_CNT_CREUSE_INT] = 0.0;
+  hc[C2D_CNT_CLOST_INT] = 0.0;
   hc[C2D_CNT_GENS] = (double)gen;
   HIPCHK(c, hipMemcpyAsync(c->T + c->L.counters, hc, sizeof hc, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1144,12 +1465,68 @@ extern "C" int c2d_census_count(c2d_ctx* c, int64_t* n) {
   return C2D_OK;
 }
 
-/* strided column copy device -> host (stride 1: one contiguous copy) */
-template <class T>
-static hipError_t col_down(T* dst, const T* src, int64_t first, int64_t stride, int64_t m) {
-  if (stride == 1) return hipMemcpy(dst, src + first, m * sizeof(T), hipMemcpyDeviceToHost);
-  return hipMemcpy2D(dst, sizeof(T), src + first, stride * sizeof(T), sizeof(T), m,
-                     hipMemcpyDeviceToHost);
+/* census records first, first + stride, ... -> packed records (the chunk
+ * list maps them to slots in the chunked census) */
+__global__ void __launch_bounds__(256) c2d_census_pack_kernel(CensusSoA cs, const int32_t* __restrict__ clist,
+                                                              int64_t first, int64_t stride, int64_t n,
+                                                              uint64_t* __restrict__ rec) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    rec_pack(cs, cens_slot(clist, first + i * stride), rec + i * C2D_CENSUS_REC_WORDS);
+}
+
+/* packed records -> census records first, first + 1, ... */
+__global__ void __launch_bounds__(256) c2d_census_unpack_kernel(CensusSoA cs, const int32_t* __restrict__ clist,
+                                                                int64_t first, int64_t n,
+                                                                const uint64_t* __restrict__ rec) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    rec_unpack(cs, cens_slot(clist, first + i), rec + i * C2D_CENSUS_REC_WORDS);
+}
+
+static const int32_t* cens_list(const c2d_ctx* c) { return c->chunked ? c->clist[c->ccur] : nullptr; }
+
+/* m census records first, first + stride, ... to the host, as the
+ * reference's record (d6: rpre zpre wmu phi ew xnu; i5: jgpsp jgplc jgpmu
+ * jph kph; keys), in batches through the packed form */
+static int census_download(c2d_ctx* c, int64_t first, int64_t stride, int64_t m, double* d6, int32_t* i5,
+                           uint64_t* keys) {
+  int rc = ensure_tmp(c, std::min<int64_t>(m, int64_t(1) << 20));
+  if (rc) return rc;
+  const int64_t B = std::min<int64_t>(c->tmp_cap, int64_t(1) << 20);
+  std::vector<uint64_t> h((size_t)std::min(m, B) * C2D_CENSUS_REC_WORDS);
+  const bool enc = cens_encoded(c);
+  const CensusSoA cs = c->cens[c->cur].soa();
+  for (int64_t b0 = 0; b0 < m; b0 += B) {
+    const int64_t nb = std::min(B, m - b0);
+    const int g = (int)std::min<int64_t>((nb + 255) / 256, (int64_t)c->n_cu * 8);
+    hipLaunchKernelGGL(c2d_census_pack_kernel, dim3(g), dim3(256), 0, c->stream, cs, cens_list(c),
+                       first + b0 * stride, stride, nb, c->tmp_rec);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(h.data(), c->tmp_rec, sizeof(uint64_t) * C2D_CENSUS_REC_WORDS * nb,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int64_t t = 0; t < nb; t++) {
+      const uint64_t* r = h.data() + t * C2D_CENSUS_REC_WORDS;
+      const int64_t o = b0 + t;
+      const uint32_t jk = (uint32_t)(r[6] & 0xffffffffull), bins = (uint32_t)(r[6] >> 32);
+      if (d6)
+        for (int f = 0; f < 6; f++) {
+          double v;
+          memcpy(&v, r + f, sizeof v);
+          d6[6 * o + f] = (f == 3 && enc) ? cens_phi_decode(v, bins) : v;
+        }
+      if (i5) {
+        i5[5 * o + 0] = (int32_t)(bins & 0xff);
+        i5[5 * o + 1] = (int32_t)((bins >> 8) & 0xff);
+        i5[5 * o + 2] = (int32_t)((bins >> 16) & 0xff);
+        i5[5 * o + 3] = (int32_t)(jk >> 16);
+        i5[5 * o + 4] = (int32_t)(jk & 0xffff);
+      }
+      if (keys) keys[o] = r[7];
+    }
+  }
+  return C2D_OK;
 }
 
 extern "C" int c2d_census_export_range(c2d_ctx* c, int64_t first, int64_t stride, double* d6,
@@ -1160,28 +1537,7 @@ extern "C" int c2d_census_export_range(c2d_ctx* c, int64_t first, int64_t stride
   const int64_t m = std::min(cap, avail);
   if (m <= 0) return C2D_OK;
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  const DevCensus& d = c->cens[c->cur];
-  std::vector<double> col(m);
-  std::vector<uint32_t> jk(m), bins(m);
-  HIPCHK(c, col_down(jk.data(), d.jk, first, stride, m));
-  HIPCHK(c, col_down(bins.data(), d.bins, first, stride, m));
-  const bool enc = cens_encoded(c);
-  for (int f = 0; f < 6; f++) {
-    HIPCHK(c, col_down(col.data(), d.d[f], first, stride, m));
-    if (d6)
-      for (int64_t i = 0; i < m; i++)
-        d6[6 * i + f] = (f == 3 && enc) ? cens_phi_decode(col[i], bins[i]) : col[i];
-  }
-  if (i5)
-    for (int64_t i = 0; i < m; i++) {
-      i5[5 * i + 0] = (int32_t)(bins[i] & 0xff);
-      i5[5 * i + 1] = (int32_t)((bins[i] >> 8) & 0xff);
-      i5[5 * i + 2] = (int32_t)((bins[i] >> 16) & 0xff);
-      i5[5 * i + 3] = (int32_t)(jk[i] >> 16);
-      i5[5 * i + 4] = (int32_t)(jk[i] & 0xffff);
-    }
-  if (keys) HIPCHK(c, col_down(keys, d.key, first, stride, m));
-  return C2D_OK;
+  return census_download(c, first, stride, m, d6, i5, keys);
 }
 
 extern "C" int c2d_census_export(c2d_ctx* c, double* d6, int32_t* i5, uint64_t* keys, int64_t cap,
@@ -1191,28 +1547,7 @@ extern "C" int c2d_census_export(c2d_ctx* c, double* d6, int32_t* i5, uint64_t* 
   const int64_t m = std::min(cap, c->n_census);
   if (m <= 0) return C2D_OK;
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  const DevCensus& d = c->cens[c->cur];
-  std::vector<double> col(m);
-  std::vector<uint32_t> jk(m), bins(m);
-  HIPCHK(c, hipMemcpy(jk.data(), d.jk, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  HIPCHK(c, hipMemcpy(bins.data(), d.bins, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  const bool enc = cens_encoded(c);
-  for (int f = 0; f < 6; f++) {
-    HIPCHK(c, hipMemcpy(col.data(), d.d[f], m * sizeof(double), hipMemcpyDeviceToHost));
-    if (d6)
-      for (int64_t i = 0; i < m; i++)
-        d6[6 * i + f] = (f == 3 && enc) ? cens_phi_decode(col[i], bins[i]) : col[i];
-  }
-  if (i5)
-    for (int64_t i = 0; i < m; i++) {
-      i5[5 * i + 0] = (int32_t)(bins[i] & 0xff);
-      i5[5 * i + 1] = (int32_t)((bins[i] >> 8) & 0xff);
-      i5[5 * i + 2] = (int32_t)((bins[i] >> 16) & 0xff);
-      i5[5 * i + 3] = (int32_t)(jk[i] >> 16);
-      i5[5 * i + 4] = (int32_t)(jk[i] & 0xffff);
-    }
-  if (keys) HIPCHK(c, hipMemcpy(keys, d.key, m * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  return C2D_OK;
+  return census_download(c, 0, 1, m, d6, i5, keys);
 }
 
 extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5,
@@ -1221,6 +1556,8 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
   if (n > c->cfg.census_capacity)
     return fail(c, C2D_E_CENSUS_OVERFLOW, "census import %lld > capacity", (long long)n);
   HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  /* records [0, n) of the SoA (chunked: the list's chunks 0, 1, ...) */
   const DevCensus& d = c->cens[c->cur];
   std::vector<double> col(n);
   const bool enc = cens_encoded(c);
@@ -1249,44 +1586,15 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
     HIPCHK(c, hipMemcpy(d.bins, bins.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(d.key, keys, n * sizeof(uint64_t), hipMemcpyHostToDevice));
   }
+  if (c->chunked) {
+    const int64_t k = (n + C2D_CCHUNK - 1) / C2D_CCHUNK;
+    std::vector<int32_t> ids(k);
+    for (int64_t i = 0; i < k; i++) ids[i] = (int32_t)i;
+    if (k) HIPCHK(c, hipMemcpy(c->clist[c->ccur], ids.data(), k * sizeof(int32_t), hipMemcpyHostToDevice));
+    c->n_clist = k;
+  }
   c->n_census = n;
   return C2D_OK;
-}
-
-/* census SoA <-> packed 8-word records (C2D_CENSUS_REC_WORDS), bit-exact */
-__global__ void __launch_bounds__(256) c2d_census_pack_kernel(CensusSoA cs, int64_t first, int64_t n,
-                                                              uint64_t* __restrict__ rec) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = first + i;
-    uint64_t* r = rec + i * C2D_CENSUS_REC_WORDS;
-    r[0] = __double_as_longlong(cs.rpre[s]);
-    r[1] = __double_as_longlong(cs.zpre[s]);
-    r[2] = __double_as_longlong(cs.wmu[s]);
-    r[3] = __double_as_longlong(cs.phi[s]);
-    r[4] = __double_as_longlong(cs.ew[s]);
-    r[5] = __double_as_longlong(cs.xnu[s]);
-    r[6] = (uint64_t)cs.jk[s] | ((uint64_t)cs.bins[s] << 32);
-    r[7] = cs.key[s];
-  }
-}
-
-__global__ void __launch_bounds__(256) c2d_census_unpack_kernel(CensusSoA cs, int64_t first, int64_t n,
-                                                                const uint64_t* __restrict__ rec) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t d = first + i;
-    const uint64_t* r = rec + i * C2D_CENSUS_REC_WORDS;
-    cs.rpre[d] = __longlong_as_double(r[0]);
-    cs.zpre[d] = __longlong_as_double(r[1]);
-    cs.wmu[d] = __longlong_as_double(r[2]);
-    cs.phi[d] = __longlong_as_double(r[3]);
-    cs.ew[d] = __longlong_as_double(r[4]);
-    cs.xnu[d] = __longlong_as_double(r[5]);
-    cs.jk[d] = (uint32_t)(r[6] & 0xffffffffull);
-    cs.bins[d] = (uint32_t)(r[6] >> 32);
-    cs.key[d] = r[7];
-  }
 }
 
 extern "C" int c2d_census_pack(c2d_ctx* c, int64_t first, int64_t n, uint64_t* d_rec) {
@@ -1298,7 +1606,7 @@ extern "C" int c2d_census_pack(c2d_ctx* c, int64_t first, int64_t n, uint64_t* d
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 8);
   hipLaunchKernelGGL(c2d_census_pack_kernel, dim3(grid), dim3(256), 0, c->stream,
-                     c->cens[c->cur].soa(), first, n, d_rec);
+                     c->cens[c->cur].soa(), cens_list(c), first, (int64_t)1, n, d_rec);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return C2D_OK;
@@ -1311,9 +1619,24 @@ extern "C" int c2d_census_append(c2d_ctx* c, const uint64_t* d_rec, int64_t n) {
                 (long long)c->n_census, (long long)n, (long long)c->cfg.census_capacity);
   if (n == 0) return C2D_OK;
   HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (c->chunked) {
+    /* the list's last chunk fills up first, then free chunks join the list */
+    const int64_t k = (c->n_census + n + C2D_CCHUNK - 1) / C2D_CCHUNK - c->n_clist;
+    if (k > 0) {
+      int64_t n_free = 0;
+      int rc = chunk_pool_build(c, &n_free);
+      if (rc) return rc;
+      if (n_free < k)
+        return fail(c, C2D_E_CENSUS_OVERFLOW, "c2d_census_append: %lld free census chunks, %lld needed",
+                    (long long)n_free, (long long)k);
+      HIPCHK(c, hipMemcpyAsync(c->clist[c->ccur] + c->n_clist, c->pool, sizeof(int32_t) * k,
+                               hipMemcpyDeviceToDevice, c->stream));
+      c->n_clist += k;
+    }
+  }
   const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 8);
   hipLaunchKernelGGL(c2d_census_unpack_kernel, dim3(grid), dim3(256), 0, c->stream,
-                     c->cens[c->cur].soa(), c->n_census, n, d_rec);
+                     c->cens[c->cur].soa(), cens_list(c), c->n_census, n, d_rec);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->n_census += n;
@@ -1323,6 +1646,7 @@ extern "C" int c2d_census_append(c2d_ctx* c, const uint64_t* d_rec, int64_t n) {
 extern "C" int c2d_census_truncate(c2d_ctx* c, int64_t n) {
   if (!c || n < 0 || n > c->n_census) return C2D_E_ARG;
   c->n_census = n;
+  if (c->chunked) c->n_clist = (n + C2D_CCHUNK - 1) / C2D_CCHUNK;
   return C2D_OK;
 }
 
@@ -1369,6 +1693,16 @@ extern "C" int c2d_last_compaction(c2d_ctx* c, int32_t* rounds, int64_t* moved, 
   if (rounds) *rounds = c->last_compact_rounds;
   if (moved) *moved = c->last_compact_moved;
   if (physical) *physical = c->cens_phys;
+  return C2D_OK;
+}
+
+extern "C" int c2d_last_census_chunks(c2d_ctx* c, int64_t* chunks, int64_t* recycled, int64_t* unrecycled,
+                                      int64_t* physical) {
+  if (!c) return C2D_E_ARG;
+  if (chunks) *chunks = c->chunked ? c->n_clist : 0;
+  if (recycled) *recycled = c->last_creuse;
+  if (unrecycled) *unrecycled = c->last_clost;
+  if (physical) *physical = c->chunked ? c->nchunks : 0;
   return C2D_OK;
 }
 

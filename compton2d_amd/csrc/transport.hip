@@ -94,12 +94,15 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
  *                 instead of fdlibm's ~99 with its branches and division);
  *   C2D_FAST_DIV  a / b for b > 0 finite as a * (1/b), the reciprocal from
  *                 v_rcp_f64 and two Newton steps (~1 ulp);
- *   C2D_RSQ_NR    Newton steps after v_rsq_f64 in the survivors' point loop. */
+ *   C2D_RSQ_NR    Newton steps after v_rsq_f64 in the survivors' point loop.
+ * A/B on the C3 census (profiles/r03_microopt.txt): FAST_DIV +2 % (on),
+ * FAST_EXP -4 % (off: ocml's exp keeps more VGPRs live), RSQ_NR=1 +1 %
+ * (within noise; kept at 2 for the geometry's precision). */
 #ifndef C2D_FAST_EXP
 #define C2D_FAST_EXP 0
 #endif
 #ifndef C2D_FAST_DIV
-#define C2D_FAST_DIV 0
+#define C2D_FAST_DIV 1
 #endif
 #ifndef C2D_RSQ_NR
 #define C2D_RSQ_NR 2
@@ -619,20 +622,62 @@ C2D_COLD_FN int imcleak(const KParams& P0, const Tal& T, Pkt& p, LaneCnt& lc) {
   return 1;
 }
 
-/* Census appends of the bundle kernel come from wave-private chunks of
- * P.cens_chunk slots (host: up to 1024, and at most 1/8 of the capacity over
- * all waves: 256 -> 1024 slots was +1 %), reserved with one atomic on the
- * census counter (a single address every wave appends to: per-write
- * reservations were the kernel's limiter).  A wave's last chunk leaves a tail
- * [used, CENS_CHUNK) that the kernel marks dead at its end; the host's
- * compaction closes it with the other dead slots (C2D_CENS_DEAD). */
+/* Census appends come from wave-private chunks of P.cens_chunk slots,
+ * reserved with one atomic (a single address every wave appends to:
+ * per-write reservations were the kernel's limiter).
+ *   double-buffered: chunks of up to 1024 slots (host: at most 1/8 of the
+ *     capacity over all waves; 256 -> 1024 was +1 %) cut from the output
+ *     counter; a wave's last chunk leaves a tail [used, chunk) that the
+ *     kernel marks dead at its end, closed by the host's compaction;
+ *   chunked: C2D_CCHUNK-slot chunks, first from the wave's stack of chunks
+ *     its finished census sources freed, then from the step's free pool; each
+ *     is listed in out_list when taken, and a wave slot's partly filled chunk
+ *     carries over to the next launch (cstate). */
 /* per wave of the workgroup, in LDS (updated by the lanes that write) */
-__shared__ unsigned long long c2d_cch_base[16];
-__shared__ uint32_t c2d_cch_used[16];
-struct CensChunk {
-  int dummy;
-};
-__device__ __forceinline__ unsigned long long census_slot_chunk(const KParams& P0, CensChunk&) {
+__shared__ unsigned long long c2d_cch_base[C2D_TR_BLOCK / 64];
+__shared__ uint32_t c2d_cch_used[C2D_TR_BLOCK / 64];
+/* chunked census, bundle kernel: the census chunks each wave counts down
+ * (chunk index in the input list, -1 free; sources not yet finished) and its
+ * stack of freed chunks */
+__shared__ int32_t c2d_ct_idx[C2D_TR_BLOCK / 64][C2D_CT_TRACK];
+__shared__ uint32_t c2d_ct_rem[C2D_TR_BLOCK / 64][C2D_CT_TRACK];
+__shared__ int32_t c2d_fs[C2D_TR_BLOCK / 64][C2D_CT_STACK];
+__shared__ uint32_t c2d_fs_n[C2D_TR_BLOCK / 64];
+static_assert(C2D_WORK_CHUNK == C2D_CCHUNK, "a work chunk must cover exactly one census chunk");
+
+/* the next chunk of the wave (leader lane): its first slot, or cap_cout when
+ * none is left (the writes then fail with ERR_CENSUS) */
+C2D_COLD_FN unsigned long long census_new_chunk(const KParams& P0, int w) {
+  const KParams& P = cold(P0);
+  if (!P.clist)
+    return __hip_atomic_fetch_add((C2D_GLOBAL unsigned long long*)P.n_cout, (unsigned long long)P.cens_chunk,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int32_t id = -1;
+  const uint32_t ns = c2d_fs_n[w];
+  if (ns > 0) {
+    id = c2d_fs[w][ns - 1];
+    c2d_fs_n[w] = ns - 1;
+  } else {
+    /* an entry reserved but not yet written reads -1: its chunk sits out the step */
+    if (__hip_atomic_load((C2D_GLOBAL unsigned long long*)P.n_relist, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT) > __hip_atomic_load((C2D_GLOBAL unsigned long long*)
+                                                                          P.relist_head, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT)) {
+      const unsigned long long h = atomicAdd(P.relist_head, 1ull);
+      if (h < gld(P.n_relist))
+        id = __hip_atomic_load((C2D_GLOBAL int32_t*)(P.relist + h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (id < 0) {
+      const unsigned long long h = atomicAdd(P.pool_head, 1ull);
+      if (h < gld(P.pool_n)) id = gld(P.pool + h);
+    }
+  }
+  if (id < 0) return (unsigned long long)P.cap_cout;
+  gst(P.out_list + atomicAdd(P.n_out, 1ull), id);
+  return (unsigned long long)id << C2D_CCHUNK_LOG;
+}
+
+__device__ __forceinline__ unsigned long long census_slot_chunk(const KParams& P0) {
   const KParams& P = cold(P0);
   const int w = (int)(threadIdx.x >> 6);
   const unsigned long long mask = __ballot(1);
@@ -649,9 +694,7 @@ __device__ __forceinline__ unsigned long long census_slot_chunk(const KParams& P
     return base + used + rank;
   }
   unsigned long long nb = 0;
-  if (lane == leader)
-    nb = __hip_atomic_fetch_add((C2D_GLOBAL unsigned long long*)P.n_cout, (unsigned long long)CENS_CHUNK,
-                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == leader) nb = census_new_chunk(P, w);
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)nb, leader);
   const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(nb >> 32), leader);
   nb = ((unsigned long long)hi << 32) | lo;
@@ -659,11 +702,79 @@ __device__ __forceinline__ unsigned long long census_slot_chunk(const KParams& P
   return rank < rem ? base + used + rank : nb + (rank - rem);
 }
 
-/* census write (src/imctrk2d.f:528-578).  inplace >= 0: the packet's source
- * is census record `inplace`, which it replaces (in-place census); else the
- * record is appended. */
-C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, LaneCnt& lc,
-                              CensChunk* cch = nullptr, long long inplace = -1) {
+/* A wave slot's partly filled chunk carries over from launch to launch of
+ * the step (cstate), so each wave slot leaves at most one per step: the
+ * host closes them after the last generation (capi.cpp). */
+__device__ __forceinline__ void census_chunk_load(const KParams& P0, int w, uint32_t lane) {
+  const KParams& P = cold(P0);
+  if (lane != 0) return;
+  c2d_cch_base[w] = 0ull;
+  c2d_cch_used[w] = P.cens_chunk;
+  c2d_fs_n[w] = 0u;
+  for (int e = 0; e < C2D_CT_TRACK; e++) c2d_ct_idx[w][e] = -1;
+  const int64_t ws = (int64_t)blockIdx.x * (C2D_TR_BLOCK / 64) + w;
+  const int64_t base = gld(P.cstate + 2 * ws);
+  if (base >= 0) {
+    c2d_cch_base[w] = (unsigned long long)base;
+    c2d_cch_used[w] = (uint32_t)gld(P.cstate + 2 * ws + 1);
+  }
+}
+
+/* a freed chunk the wave cannot keep goes to the relist */
+__device__ __forceinline__ void census_relist(const KParams& P, int32_t id) {
+  const unsigned long long h = atomicAdd(P.n_relist, 1ull);
+  __hip_atomic_store((C2D_GLOBAL int32_t*)(P.relist + h), id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void census_chunk_store(const KParams& P0, int w, uint32_t lane) {
+  const KParams& P = cold(P0);
+  if (lane != 0) return;
+  if (P.clist)
+    for (uint32_t i = 0; i < c2d_fs_n[w]; i++) census_relist(P, c2d_fs[w][i]);
+  const uint32_t used = c2d_cch_used[w];
+  const unsigned long long base = c2d_cch_base[w];
+  const int64_t ws = (int64_t)blockIdx.x * (C2D_TR_BLOCK / 64) + w;
+  const bool part = used < P.cens_chunk && base < (unsigned long long)P.cap_cout;
+  gst(P.cstate + 2 * ws, part ? (int64_t)base : (int64_t)-1);
+  gst(P.cstate + 2 * ws + 1, (int64_t)used);
+}
+
+/* chunked census, bundle kernel (lane 0): the wave took the work chunk that
+ * holds the n census items of (physical) chunk id.  Direct-mapped count-down
+ * slots (id mod C2D_CT_TRACK: no search in the lane loop); a chunk whose slot
+ * is busy is not counted down and waits for the next step. */
+__device__ __forceinline__ void census_track(int w, int32_t id, uint32_t n) {
+  const int e = id & (C2D_CT_TRACK - 1);
+  if (c2d_ct_idx[w][e] < 0) {
+    c2d_ct_idx[w][e] = id;
+    c2d_ct_rem[w][e] = n;
+  } else {
+    atomicAdd(&c2d_cnt_lds[C2D_CNT_CLOST_INT], 1u);
+  }
+}
+
+/* the census source in slot `slot` finished: the last one of its chunk frees
+ * the chunk */
+C2D_COLD_FN void census_item_done(const KParams& P0, long long slot) {
+  const KParams& P = cold(P0);
+  const int w = (int)(threadIdx.x >> 6);
+  const int32_t id = (int32_t)(slot >> C2D_CCHUNK_LOG);
+  const int e = id & (C2D_CT_TRACK - 1);
+  if (c2d_ct_idx[w][e] != id) return;
+  if (atomicSub(&c2d_ct_rem[w][e], 1u) != 1u) return;
+  c2d_ct_idx[w][e] = -1;
+  const uint32_t s = atomicAdd(&c2d_fs_n[w], 1u);
+  if (s < C2D_CT_STACK) {
+    c2d_fs[w][s] = id;
+  } else {
+    atomicSub(&c2d_fs_n[w], 1u);
+    census_relist(P, id);
+  }
+  atomicAdd(&c2d_cnt_lds[C2D_CNT_CREUSE_INT], 1u);
+}
+
+/* census write (src/imctrk2d.f:528-578): appended to the wave's chunk */
+C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, LaneCnt& lc) {
   const KParams& P = cold(P0);
   const Geo* g = T.g;
   int cell = (p.jph - 1) * P.nr + (p.kph - 1);
@@ -678,9 +789,7 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
     gadd(&P.nf_rep[(int64_t)(blockIdx.x % C2D_NF_REPL) * P.ncell * C2D_NPHFIELD +
                    (int64_t)cell * C2D_NPHFIELD + (i - 1)], 6.25e8 * p.ew / p.xnu);
   }
-  unsigned long long slot;
-  if (inplace >= 0) slot = (unsigned long long)inplace;
-  else slot = cch ? census_slot_chunk(P, *cch) : wave_reserve(P.n_cout);
+  const unsigned long long slot = census_slot_chunk(P);
   if (slot < (unsigned long long)P.cap_cout) {
     gst(P.cout.rpre + slot, p.rpre);
     gst(P.cout.zpre + slot, p.zpre);
@@ -1408,11 +1517,13 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
 }
 
 /* a generation-0 source record: census packet (imcfield2d.f:98-117) or a
- * sampled volume/surface packet from the packet store */
-__device__ __forceinline__ void load_source(const KParams& P0, Pkt& p, long long item) {
+ * sampled volume/surface packet from the packet store.  src >= 0: the census
+ * slot (the fetch resolved the chunk list once per work chunk); src < 0:
+ * packet-store entry -src - 1 */
+__device__ __forceinline__ void load_source(const KParams& P0, Pkt& p, long long src) {
   const KParams& P = cold(P0);
-  if (item < P.n_cens_items) {
-    const int64_t i = item;
+  if (src >= 0) {
+    const int64_t i = src;
     p.rpre = gld(P.cin.rpre + i); p.zpre = gld(P.cin.zpre + i);
     p.wmu = clampd(gld(P.cin.wmu + i), 0.99999999);
     p.ew = gld(P.cin.ew + i); p.xnu = gld(P.cin.xnu + i);
@@ -1430,7 +1541,7 @@ __device__ __forceinline__ void load_source(const KParams& P0, Pkt& p, long long
     p.sub = 0;
     p.dcen = P.cdt;                                    /* imcfield2d.f:117 */
   } else {
-    load_pk(p, P.pk, item - P.n_cens_items);
+    load_pk(p, P.pk, -src - 1);
     set_phi(p, p.phi);
   }
 }
@@ -1462,6 +1573,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
     for (int i = tid; i < n_cells_lds + n_esc; i += BLOCK) cells_lds[i] = 0.0;
   }
   init_counters(c2d_cnt_lds);
+  census_chunk_load(P, tid >> 6, lane);
   __syncthreads();
   const long long n_items = (long long)rfl64(*A.n_pk);
 
@@ -1541,6 +1653,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
     for (int i = 0; i < C2D_TR_PROF_WORDS; i++)
       if (pf.acc[i]) atomicAdd(&P.prof[i], (unsigned long long)pf.acc[i]);
 #endif
+  census_chunk_store(P, tid >> 6, lane);
 
   /* ---- flush: LDS tallies and counters ---- */
   __syncthreads();
@@ -1602,8 +1715,7 @@ enum : int32_t {
   BF_SPEC = 2,      /* ... with a weight that assumes no more collisions */
   BF_RERUN = 4,     /* a collision cancelled it: refly alone afterwards  */
   BF_TKILL = 8,     /* it ended KILLED / ABORTED: counted at the bundle end */
-  BF_TABORT = 16,
-  BF_CWROTE = 32    /* it wrote its census record in place (census source)  */
+  BF_TABORT = 16
 };
 struct Bundle {
   Pkt p;              /* shared path; p.ew, p.wtmin, p.ctr: the recombined copy's */
@@ -1710,8 +1822,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
 
 /* one shared step of the bundle (flight() for every copy on the path) */
 __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, const GenArgs& A,
-                                            Bundle& b, ComCache& cc, LaneCnt& lc, Prof& pf,
-                                            CensChunk* cch) {
+                                            Bundle& b, ComCache& cc, LaneCnt& lc, Prof& pf) {
 #ifdef C2D_HOT_RELOAD
   const KParams& P = cold_always(P1);
 #else
@@ -1910,10 +2021,8 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
       b.alive = 0;
       if (b.flags & BF_TRACK) {
         TP_COUNT(pf, TP_CENS_W, TP_CENS_L);
-        /* a census source's one census record replaces its own (C2D_CENS_DEAD):
-         * the recombined copy flies last, after every read of the record */
-        census_write(P, T, p, lc, cch, (P.cens_inplace && b.src < P.n_cens_items) ? b.src : -1);
-        b.flags = (b.flags & ~BF_TRACK) | BF_CWROTE;
+        census_write(P, T, p, lc);
+        b.flags &= ~BF_TRACK;
       }
     }
   }
@@ -2006,6 +2115,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
   ComCache cc = {-1, -1, 0.0, 0.0};
   LaneCnt lc = {0u};
   long long chunk_base = 0, chunk_end = 0;
+  long long chunk_slot = 0;        /* census slot of the work chunk's first item */
   bool exhausted = false;
   int shard_try = 0;
   const int shard0 = (int)(blockIdx.x % C2D_WORK_SHARDS);
@@ -2014,9 +2124,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
   for (int i = 0; i < C2D_TR_PROF_WORDS; i++) pf.acc[i] = 0;
   pf.t = clock64();
 #endif
-  CensChunk cch = {0};
-  const uint32_t CENS_CHUNK = cold(P).cens_chunk;
-  if (lane == 0) { c2d_cch_base[tid >> 6] = 0ull; c2d_cch_used[tid >> 6] = CENS_CHUNK; }
+  census_chunk_load(P, tid >> 6, lane);
 
   for (;;) {
     /* ---- refill idle lanes: chunked, wave-aggregated work fetch from the
@@ -2029,9 +2137,11 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
         if (chunk_base >= chunk_end) {
           for (;;) {
             if (shard_try >= C2D_WORK_SHARDS) { exhausted = true; break; }
+            /* shard bounds on work-chunk (= census-chunk) boundaries */
             const int s = (shard0 + shard_try) % C2D_WORK_SHARDS;
-            const long long lo = n_items * s / C2D_WORK_SHARDS;
-            const long long hi = n_items * (s + 1) / C2D_WORK_SHARDS;
+            const long long lo = (n_items * s / C2D_WORK_SHARDS) & ~(CHUNK - 1);
+            const long long hi = s + 1 == C2D_WORK_SHARDS
+                                     ? n_items : (n_items * (s + 1) / C2D_WORK_SHARDS) & ~(CHUNK - 1);
             unsigned long long nb = 0;
             if (lane == 0)
               nb = atomicAdd(A.work_sh + (size_t)s * C2D_EV_SHARD_STRIDE, (unsigned long long)CHUNK);
@@ -2039,6 +2149,14 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
             if (lo + (long long)nb < hi) {
               chunk_base = lo + (long long)nb;
               chunk_end = chunk_base + CHUNK < hi ? chunk_base + CHUNK : hi;
+              chunk_slot = chunk_base;
+              if (cold(P).clist && chunk_base < cold(P).n_cens_items) {
+                const int32_t id = __builtin_amdgcn_readfirstlane(gld(cold(P).clist + (chunk_base >> C2D_CCHUNK_LOG)));
+                chunk_slot = (long long)id << C2D_CCHUNK_LOG;
+                if (lane == 0)
+                  census_track(tid >> 6, id,
+                               (uint32_t)(min(chunk_end, (long long)cold(P).n_cens_items) - chunk_base));
+              }
               break;
             }
             shard_try++;
@@ -2050,7 +2168,10 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
         const long long rank = __popcll(lt);
         const long long nneed = __popcll(needm);
         if (((needm >> lane) & 1ull) && rank < avail) {
-          item = chunk_base + rank;
+          /* the source: its census slot (this work chunk's) or packet-store entry */
+          const long long it = chunk_base + rank;
+          item = it < cold(P).n_cens_items ? chunk_slot + (it & (CHUNK - 1))
+                                           : -(it - cold(P).n_cens_items) - 1;
           got = true;
         }
         chunk_base += (nneed < avail ? nneed : avail);
@@ -2077,7 +2198,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
 #ifdef C2D_TR_PROF
       pf.acc[TP_LANES] += __popcll(__ballot(1));
 #endif
-      bundle_step(P, T, A, b, cc, lc, pf, &cch);
+      bundle_step(P, T, A, b, cc, lc, pf);
       TP_MARK(pf, TP_EVENT);
       if (!b.alive && !(b.flags & BF_TRACK)) {
         if ((b.flags & (BF_TKILL | BF_RERUN)) == BF_TKILL)
@@ -2093,11 +2214,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
           bundle_begin(P, T, b);
         } else {
           busy = false;
-          if (P.cens_inplace && b.src < P.n_cens_items && !(b.flags & BF_CWROTE)) {
-            /* the census record of a packet that left, died or collided is free */
-            gst(cold(P).cout.bins + b.src, C2D_CENS_DEAD);
-            LC_ADD(lc, C2D_CNT_DEAD_INT);
-          }
+          if (cold(P).clist && b.src >= 0) census_item_done(P, b.src);
         }
       }
     }
@@ -2110,18 +2227,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
       if (pf.acc[i]) atomicAdd(&P.prof[i], (unsigned long long)pf.acc[i]);
 #endif
 
-  /* the unused tail of this wave's last census chunk: dead slots (those past
-   * the physical end of the census were never reserved for a record) */
-  {
-    const unsigned long long t0 = c2d_cch_base[tid >> 6] + c2d_cch_used[tid >> 6];
-    unsigned long long t1 = c2d_cch_base[tid >> 6] + CENS_CHUNK;
-    const unsigned long long cap = (unsigned long long)cold(P).cap_cout;
-    if (t1 > cap) t1 = cap;
-    if (c2d_cch_used[tid >> 6] < CENS_CHUNK && t0 < t1) {
-      for (unsigned long long i = t0 + lane; i < t1; i += 64) gst(cold(P).cout.bins + i, C2D_CENS_DEAD);
-      if (lane == 0) atomicAdd(&c2d_cnt_lds[C2D_CNT_DEAD_INT], (uint32_t)(t1 - t0));
-    }
-  }
+  census_chunk_store(P, tid >> 6, lane);
 
   /* ---- flush: LDS tallies and counters ---- */
   __syncthreads();

@@ -102,6 +102,8 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_last_compaction.restype = C.c_int
     lib.c2d_last_compaction.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
                                         C.POINTER(C.c_int64)]
+    lib.c2d_last_census_chunks.restype = C.c_int
+    lib.c2d_last_census_chunks.argtypes = [vp] + [C.POINTER(C.c_int64)] * 4
     lib.c2d_last_kernel_ms.restype = C.c_int
     lib.c2d_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                        C.POINTER(C.c_int32)]
@@ -316,11 +318,20 @@ class Engine:
         return g0.value, al.value
 
     def last_compaction(self) -> tuple[int, int, int]:
-        """(rounds, records moved, physical slots) of the last step's in-place
-        census compaction (c2d_last_compaction)."""
+        """(rounds, records moved, physical slots) of the last step's census
+        close: the dead-tail compaction (double-buffered) or the packing of
+        the partly filled chunks (chunked) (c2d_last_compaction)."""
         r, m, ph = C.c_int32(), C.c_int64(), C.c_int64()
         self._check(self.lib.c2d_last_compaction(self.ctx, C.byref(r), C.byref(m), C.byref(ph)))
         return r.value, m.value, ph.value
+
+    def last_census_chunks(self) -> tuple[int, int, int, int]:
+        """Chunked census: (chunks in the census, chunks recycled within the
+        last step, census chunks not counted down, chunks held)
+        (c2d_last_census_chunks); zeros when double-buffered."""
+        v = [C.c_int64() for _ in range(4)]
+        self._check(self.lib.c2d_last_census_chunks(self.ctx, *[C.byref(x) for x in v]))
+        return tuple(x.value for x in v)
 
     # -- Fokker-Planck -------------------------------------------------------
     def fp_set_config(self, const: abi.FpConstants) -> None:

@@ -117,9 +117,9 @@ typedef struct c2d_config {
   int64_t queue_capacity;         /* scatter records per generation            */
   int32_t census_inplace;         /* 0: census double-buffered (in + out, 128 B per
                                      record, the reference's dbufin/dbufout); 1: one
-                                     in-place SoA (64 B per record + 1/16 slack,
-                                     dead slots compacted after the step: half the
-                                     memory, slower census writes)   */
+                                     chunked SoA (64 B per record + 1/16 slack: a
+                                     step refills the 1024-record chunks its census
+                                     sources have finished with)     */
 } c2d_config;
 
 /* Per-step inputs (what imcgen2d/volume_em/file_sp leave in COMMON). */
@@ -450,12 +450,20 @@ int  c2d_last_gen0_steps(c2d_ctx* ctx, int64_t* steps);
  * packet-steps / path-steps is the work sharing factor.  Either pointer may
  * be NULL. */
 int  c2d_last_path_steps(c2d_ctx* ctx, int64_t* gen0_paths, int64_t* all_paths);
-/* The in-place census of the last step (replaces the double-buffered
- * dbufout/ibufout of imctrk2d.f:558-572 + imcfield2d.f:96-97): rounds of the
- * compaction that closed its dead slots, records moved, and the physical
- * slots the context holds (census_capacity + append slack).  Any pointer may
- * be NULL. */
+/* How the last step closed its census (the dbufout/ibufout of
+ * imctrk2d.f:558-572 + imcfield2d.f:96-97): double-buffered, the rounds of
+ * the compaction that closed the dead chunk tails and the records it moved;
+ * chunked (census_inplace), the batches that packed the partly filled chunks
+ * and their records.  physical = the census slots the context holds.  Any
+ * pointer may be NULL. */
 int  c2d_last_compaction(c2d_ctx* ctx, int32_t* rounds, int64_t* moved, int64_t* physical);
+/* Chunked census (census_inplace = 1): the chunks the census occupies, the
+ * chunks the last step's bundle kernel freed and refilled within the step,
+ * the census chunks it could not count down (these wait for the next step),
+ * and the chunks the context holds (1024 records each).  Double-buffered:
+ * zeros.  Any pointer may be NULL. */
+int  c2d_last_census_chunks(c2d_ctx* ctx, int64_t* chunks, int64_t* recycled, int64_t* unrecycled,
+                            int64_t* physical);
 
 /* ------------------------------------------------------------------------
  * Multi-GPU tally reduction over RCCL (xGMI), for hosts that drive one

@@ -108,8 +108,9 @@ def test_fast_census_azimuth_encoding():
     b.close()
 
 
+@pytest.mark.parametrize("inplace", [0, 1])
 @pytest.mark.parametrize("mode", [abi.COMTOT_EXACT, abi.COMTOT_TABLE])
-def test_census_overflow_is_reported(mode):
+def test_census_overflow_is_reported(mode, inplace):
     """A step whose census does not fit fails with C2D_E_CENSUS_OVERFLOW (the
     reference's `stop 'too many photons'`, src/imctrk2d.f:573-577) instead of
     writing past the buffer."""
@@ -120,7 +121,7 @@ def test_census_overflow_is_reported(mode):
     need = full.census_count()
     full.close()
     assert need > 200
-    small = Engine(gc.grid(comtot_mode=mode, census_capacity=need // 4))
+    small = Engine(gc.grid(comtot_mode=mode, census_capacity=need // 4, census_inplace=inplace))
     with pytest.raises(C2DError) as e:
         small.transport_step(gc.step_inputs(0))
     assert e.value.code == -3, str(e.value)
@@ -160,10 +161,13 @@ def test_census_at_capacity_fits(mode, inplace):
 
 @pytest.mark.parametrize("inplace", [0, 1])
 def test_census_compaction_in_many_rounds(monkeypatch, inplace):
-    """The compaction's work lists hold C2D_COMPACT_LIST dead/live slot pairs
-    per round; with a list of 7 every step needs many rounds, and the census
-    (and so the next step's histories) stays the oracle's."""
+    """The census close in many rounds: double-buffered, the compaction's
+    work lists hold C2D_COMPACT_LIST dead/live slot pairs per round; chunked,
+    the packing of the partly filled chunks moves C2D_CHUNK_BATCH records per
+    two-phase round.  With 7 / 100 every step needs many rounds, and the
+    census (and so the next step's histories) stays the oracle's."""
     monkeypatch.setenv("C2D_COMPACT_LIST", "7")
+    monkeypatch.setenv("C2D_CHUNK_BATCH", "100")
     gc = GoldenCase("ssc_tau")
     eng = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, census_inplace=inplace))
     orc = OL.Oracle(gc.grid(), OL.RNG_LINEAGE, "det")
@@ -179,6 +183,42 @@ def test_census_compaction_in_many_rounds(monkeypatch, inplace):
         sel = [abi.CNT_STEPS, abi.CNT_ESCAPES, abi.CNT_CENSUS, abi.CNT_COLLIDE, abi.CNT_KILLED,
                abi.CNT_SOURCES, abi.CNT_COMPB, abi.CNT_EVENTS, abi.CNT_ESC_SCAT]
         np.testing.assert_array_equal(tg["counters"][sel], to["counters"][sel])
+        if inplace:
+            chunks, _, _, held = eng.last_census_chunks()
+            assert chunks == -(-eng.census_count() // 1024) and held > chunks
     assert max(rounds) > 10, rounds
+    eng.close()
+    orc.close()
+
+
+def test_chunked_census_recycles_chunks():
+    """Chunked census over several steps of a census-dominated run: the
+    bundle kernel refills the chunks its finished census sources leave (most
+    of the census chunks), the census stays the oracle's record for record,
+    and a capacity just above the census suffices."""
+    gc = GoldenCase("c3_mrk421")
+    probe = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, census_inplace=1))
+    need = []
+    for n in range(gc.nsteps):
+        probe.transport_step(gc.step_inputs(n))
+        need.append(probe.census_count())
+    probe.close()
+    eng = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, census_inplace=1, census_capacity=max(need)))
+    orc = OL.Oracle(gc.grid(), OL.RNG_LINEAGE, "det")
+    reused = []
+    for n in range(gc.nsteps):
+        si = gc.step_inputs(n)
+        eng.transport_step(si)
+        assert orc.step(si) == 0
+        d6g, i5g, kg = eng.census()
+        d6o, i5o, ko = orc.census()
+        og, oo = np.argsort(kg), np.argsort(ko)
+        np.testing.assert_array_equal(kg[og], ko[oo])
+        np.testing.assert_array_equal(d6g[og], d6o[oo])
+        np.testing.assert_array_equal(i5g[og], i5o[oo])
+        chunks, rec, lost, held = eng.last_census_chunks()
+        reused.append((rec, lost, chunks))
+    # the census of step n-1 is step n's first items: its chunks come back
+    assert any(r > 0 for r, _, _ in reused[1:]), reused
     eng.close()
     orc.close()

@@ -10,5 +10,5 @@ for spec in "$@"; do
   out=$ROOT/compton2d_amd/sweep/$tag
   mkdir -p "$out"
   make -s -C "$ROOT/compton2d_amd/csrc" OUT="$out/libcompton2d.so" BUILD="$ROOT/build/sweep/$tag" \
-       WPE="$wpe" FAST_CONTRACT="$con" FAST_FLAGS="${flags//,/ }" TRBLOCK="${trb:-512}" EXTRA="${extra//,/ }" -j4
+       WPE="$wpe" FAST_CONTRACT="$con" FAST_FLAGS="${flags//,/ }" TRBLOCK="${trb:-256}" EXTRA="${extra//,/ }" -j4
 done
