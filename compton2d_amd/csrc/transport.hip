@@ -92,8 +92,8 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
  * division bit for bit):
  *   C2D_FAST_EXP  exp by the ROCm device library (branch-free, ~42 VALU
  *                 instead of fdlibm's ~99 with its branches and division);
- *   C2D_FAST_DIV  a / b for b > 0 finite as a * (1/b), the reciprocal from
- *                 v_rcp_f64 and two Newton steps (~1 ulp);
+ *   C2D_FAST_DIV  a / b for b finite and nonzero as a * (1/b), the reciprocal
+ *                 from v_rcp_f64 and two Newton steps (~1 ulp);
  *   C2D_RSQ_NR    Newton steps after v_rsq_f64 in the survivors' point loop.
  * A/B on the C3 census (profiles/r03_microopt.txt): FAST_DIV +2 % (on),
  * FAST_EXP -4 % (off: ocml's exp keeps more VGPRs live), RSQ_NR=1 +1 %
@@ -575,7 +575,7 @@ __device__ __forceinline__ void push_event(const KParams& P0, double tb, const P
 __device__ __forceinline__ void escape_tally(const KParams& P0, const Tal& T, const Pkt& p) {
   const KParams& P = cold(P0);
   const int32_t jgpsp = JGPSP(p), jgplc = JGPLC(p), jgpmu = JGPMU(p);
-  if (jgplc > 0) atomicAdd(&T_EDOUT(P, T)[(jgpmu - 1) * C2D_NPHLCMAX + (jgplc - 1)], p.ew / P.dt);
+  if (jgplc > 0) atomicAdd(&T_EDOUT(P, T)[(jgpmu - 1) * C2D_NPHLCMAX + (jgplc - 1)], FDIV_POS(p.ew, P.dt));
   if (jgpsp > 0 && P.spec_switch == 0)
     atomicAdd(&T_FOUT(P, T)[(jgpmu - 1) * C2D_NPHOMAX + (jgpsp - 1)], p.ew);
 }
@@ -627,12 +627,13 @@ C2D_COLD_FN int imcleak(const KParams& P0, const Tal& T, Pkt& p, LaneCnt& lc) {
  * per-write reservations were the kernel's limiter).
  *   double-buffered: chunks of up to 1024 slots (host: at most 1/8 of the
  *     capacity over all waves; 256 -> 1024 was +1 %) cut from the output
- *     counter; a wave's last chunk leaves a tail [used, chunk) that the
- *     kernel marks dead at its end, closed by the host's compaction;
+ *     counter; after the step the host marks the unused tail of each wave
+ *     slot's last chunk dead and its compaction closes them;
  *   chunked: C2D_CCHUNK-slot chunks, first from the wave's stack of chunks
- *     its finished census sources freed, then from the step's free pool; each
- *     is listed in out_list when taken, and a wave slot's partly filled chunk
- *     carries over to the next launch (cstate). */
+ *     its finished census sources freed, then from the relist, then from the
+ *     step's free pool; each is listed in out_list when taken.
+ * In both, a wave slot's partly filled chunk carries over to the next launch
+ * of the step (cstate). */
 /* per wave of the workgroup, in LDS (updated by the lanes that write) */
 __shared__ unsigned long long c2d_cch_base[C2D_TR_BLOCK / 64];
 __shared__ uint32_t c2d_cch_used[C2D_TR_BLOCK / 64];
@@ -787,7 +788,7 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
 #endif
     const int i = grid_lookup(g->E_field, C2D_NPHFIELD, g->efl_start, g->efl_k0, p.xnu);
     gadd(&P.nf_rep[(int64_t)(blockIdx.x % C2D_NF_REPL) * P.ncell * C2D_NPHFIELD +
-                   (int64_t)cell * C2D_NPHFIELD + (i - 1)], 6.25e8 * p.ew / p.xnu);
+                   (int64_t)cell * C2D_NPHFIELD + (i - 1)], FDIV_POS(6.25e8 * p.ew, p.xnu));
   }
   const unsigned long long slot = census_slot_chunk(P);
   if (slot < (unsigned long long)P.cap_cout) {
@@ -1900,7 +1901,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
     Zbnd = (Zr > zup) ? zup : zlow;
     knew = p.kph;
     jnew = (Zr > zup) ? p.jph + 1 : p.jph - 1;
-    const double f = (Zbnd - zpre) * swmu / wmu;
+    const double f = FDIV_POS((Zbnd - zpre) * swmu, wmu);   /* wmu != 0 on a z crossing */
     rbnd = __builtin_sqrt(rpre * rpre + f * f + 2.0 * rpre * f * Eta);
     trldb = __builtin_sqrt(f * f + (Zbnd - zpre) * (Zbnd - zpre));
   } else {
@@ -1940,7 +1941,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
       probe_collide(P, T, A, b, i, dcol, sigabs, Eta, swmu, eta_switch, cell, lc);
       dpos = dcol;
       if (n == 0) break;
-      b.tau = -c2d_log_pos(UB(b)) / (double)n;
+      b.tau = FDIV_POS(-c2d_log_pos(UB(b)), (double)n);
     }
     if (n > 0) {
       b.tau = b.tau - sigsc * (trld - dpos);
