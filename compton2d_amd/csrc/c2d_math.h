@@ -23,6 +23,14 @@
 #define C2D_HD static inline
 #endif
 
+/* The divisions of the series below (never by zero or a non-finite value on
+ * the finite positive arguments the transport passes).  The fast transport
+ * build may define it as a reciprocal-based division (~1 ulp); everything
+ * else, the oracle included, keeps the IEEE quotient. */
+#ifndef C2D_MDIV
+#define C2D_MDIV(a, b) ((a) / (b))
+#endif
+
 C2D_HD uint64_t c2d_bits(double x) {
   uint64_t u;
   __builtin_memcpy(&u, &x, sizeof u);
@@ -79,7 +87,7 @@ C2D_HD double c2d_log(double x) {
     dk = (double)k;
     return dk * ln2_hi - ((R - dk * ln2_lo) - f);
   }
-  double s = f / (2.0 + f);
+  double s = C2D_MDIV(f, 2.0 + f);
   dk = (double)k;
   double z = s * s;
   i = hx - 0x6147a;
@@ -123,7 +131,7 @@ C2D_HD double c2d_log_pos(double x) {
   /* -2^-20 <= f < 2^-20 */
   const double Rs = f * f * (0.5 - 0.33333333333333333 * f);
   const double small = dk * ln2_hi - ((Rs - dk * ln2_lo) - f);
-  const double s = f / (2.0 + f);
+  const double s = C2D_MDIV(f, 2.0 + f);
   const double z = s * s;
   const double w = z * z;
   const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
@@ -178,8 +186,8 @@ C2D_HD double c2d_exp(double x) {
   }
   double t = x * x;
   double c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
-  if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
-  double y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
+  if (k == 0) return 1.0 - (C2D_MDIV(x * c, c - 2.0) - x);
+  double y = 1.0 - ((lo - C2D_MDIV(x * c, 2.0 - c)) - hi);
   if (k >= -1021) return c2d_with_hi(y, (int32_t)((uint32_t)c2d_hi(y) + ((uint32_t)k << 20)));
   y = c2d_with_hi(y, (int32_t)((uint32_t)c2d_hi(y) + ((uint32_t)(k + 1000) << 20)));
   return y * twom1000;
@@ -285,24 +293,24 @@ C2D_HD double c2d_acos(double x) {
     double z = x * x;
     double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
     double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-    double r = p / q;
+    double r = C2D_MDIV(p, q);
     return pio2_hi - (x - (pio2_lo - x * r));
   } else if (hx < 0) {                       /* x < -0.5 */
     double z = (1.0 + x) * 0.5;
     double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
     double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
     double s = __builtin_sqrt(z);
-    double r = p / q;
+    double r = C2D_MDIV(p, q);
     double w = r * s - pio2_lo;
     return pi - 2.0 * (s + w);
   } else {                                   /* x > 0.5 */
     double z = (1.0 - x) * 0.5;
     double s = __builtin_sqrt(z);
     double df = c2d_with_lo0(s);
-    double c = (z - df * df) / (s + df);
+    double c = C2D_MDIV(z - df * df, s + df);
     double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
     double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-    double r = p / q;
+    double r = C2D_MDIV(p, q);
     double w = r * s + c;
     return 2.0 * (df + w);
   }

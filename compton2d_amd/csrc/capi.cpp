@@ -1451,10 +1451,15 @@ extern "C" int c2d_events(c2d_ctx* c, double* buf, int64_t cap, int64_t* n) {
 /* Fast contexts keep the census azimuth encoded (CensusSoA): phi column =
  * cos(phi), C2D_CENS_ESW in bins = the quadrant switch.  The host sees the
  * reference's phi: decoded with the kernel's own c2d_acos, encoded with its
- * c2d_cos (the value the kernel's set_phi would compute). */
+ * c2d_cos (the value the kernel's set_phi would compute).  The kernel clamps
+ * the cosine it stores to 0.999999999 (imctrk2d.f:472-477), so cos(phi) ==
+ * 1.0 with the switch set only comes from an import of phi < 1e-10 (or of
+ * phi within 1e-10 of 2*pi, which the kernel treats identically): it
+ * decodes to 0.0, so an import of phi = 0 exports 0. */
 static constexpr double C2D_PI_REF = 3.1415926536;   /* general.pa:24 */
 static inline bool cens_encoded(const c2d_ctx* c) { return c->cfg.comtot_mode == C2D_COMTOT_TABLE; }
 static inline double cens_phi_decode(double eta, uint32_t bins) {
+  if (eta == 1.0 && (bins & C2D_CENS_ESW)) return 0.0;
   const double ph = c2d_acos(eta);
   return (bins & C2D_CENS_ESW) ? 2.0 * C2D_PI_REF - ph : ph;
 }
@@ -1859,14 +1864,21 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   P.inj_t = f.inj_t; P.inj_L = f.inj_L; P.pick_rate = f.pick_rate; P.inj_gg = f.inj_gg;
   P.inj_sigma = f.inj_sigma; P.inj_v = f.inj_v;
   P.geo = c->geo; P.gnt = c->gnt; P.FT = c->fp_FT; P.mcd = c->fp_mcd; P.zin = c->fp_zin;
-  /* device electron state: updated in place (each zone's workgroup reads its
-   * row into LDS before it writes the row back) */
+  /* device electron state: the kernel writes the staging rows (seeded with
+   * the current state, so skipped zones carry it), which replace the state
+   * only once the step has succeeded: after C2D_E_FP the device electrons
+   * are those before the call, as the caller's arrays are in host mode */
+  const size_t nt_bytes = (size_t)nc * C2D_NUM_NT * sizeof(double);
+  if (el_dev) {
+    HIPCHK(c, hipMemcpyAsync(c->fp_fout, c->f_nt, nt_bytes, hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->fp_Pout, c->Pnt, nt_bytes, hipMemcpyDeviceToDevice, st));
+  }
   P.f_in = el_dev ? c->f_nt : c->fp_fin;
   P.P_in = el_dev ? c->Pnt : c->fp_Pin;
   P.nf = nf_dev ? c->T + c->L.n_field : c->fp_nf;    /* tally layout: [cell][nphfield] */
   P.ecens = ecens_dev ? c->T + c->L.ecens : nullptr;
-  P.f_out = el_dev ? c->f_nt : c->fp_fout;
-  P.P_out = el_dev ? c->Pnt : c->fp_Pout;
+  P.f_out = c->fp_fout;
+  P.P_out = c->fp_Pout;
   P.zout = c->fp_zout; P.err = c->fp_err;
   P.gb_key = c->fp_gb_key; P.gb_val = c->fp_gb_val; P.gb_mask = C2D_FP_MEMO_SLOTS - 1u;
   HIPCHK(c, hipEventRecord(c->ev_g0a, st));
@@ -1888,6 +1900,11 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   if (herr & FPERR_STEPS)
     return fail(c, C2D_E_FP, "FP sub-step limit exceeded (reference stops, update2d.f:585-599)");
   if (herr & FPERR_GUARD) return fail(c, C2D_E_FP, "FP temperature/McDonald iteration guard tripped");
+  if (el_dev) {
+    HIPCHK(c, hipMemcpyAsync(c->f_nt, c->fp_fout, nt_bytes, hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->Pnt, c->fp_Pout, nt_bytes, hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+  }
   /* scatter back in zone order; E_add_up sums, dT_max, tea (update2d.f:266-276) */
   double E_old = 0.0, E_new = 0.0, hr = 0.0, hr_st = 0.0;
   double dT_max = (in->ncycle <= 1) ? f.df_T : 0.0;   /* photon_fill, update2d.f:1912 */

@@ -34,9 +34,26 @@
  * Built twice (see Makefile): C2D_VARIANT=0 "exact" (comtot by the full
  * 199-term sum, -ffp-contract=off: bit-identical to the oracle's lineage
  * mode) and C2D_VARIANT=1 "fast" (comtot from the per-step cubic table,
- * cos(phi) carried between packet-steps, FMA contraction).
+ * cos(phi) carried between packet-steps, reciprocal-based division; also
+ * -ffp-contract=off: contraction measured -3.3x).
  */
 #include <hip/hip_runtime.h>
+
+/* C2D_FAST_MDIV (fast build): the divisions inside c2d_math.h's log / exp /
+ * acos series as a * (1/b) with the reciprocal from v_rcp_f64 and two Newton
+ * steps (~1 ulp; the exact build keeps the IEEE quotient of the oracle) */
+#ifndef C2D_FAST_MDIV
+#define C2D_FAST_MDIV 1
+#endif
+#if defined(C2D_VARIANT) && C2D_VARIANT == 1 && C2D_FAST_MDIV
+__device__ __forceinline__ double c2d_mdiv_rcp(double a, double b) {
+  double y = __builtin_amdgcn_rcp(b);
+  y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+  y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+  return a * y;
+}
+#define C2D_MDIV(a, b) c2d_mdiv_rcp((a), (b))
+#endif
 
 #include "c2d_device.hpp"
 #include "c2d_math.h"
@@ -119,8 +136,12 @@ __device__ __forceinline__ double rcp_pos(double b) {
   return __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
 }
 #define FDIV_POS(a, b) ((a) * rcp_pos(b))
+/* b >= 0 that may be 0 (a radius): b floored at 1e-300, so a / 0 gives a
+ * huge value of a's sign (clamped by the caller) and 0 / 0 gives 0 */
+#define FDIV_NN(a, b) ((a) * rcp_pos(fmax((b), 1.0e-300)))
 #else
 #define FDIV_POS(a, b) ((a) / (b))
+#define FDIV_NN(a, b) ((a) / (b))
 #endif
 
 /* Fortran REAL literals promoted to double (src/imcvol2d_para.f:204,221,247,268,336) */
@@ -853,7 +874,7 @@ __device__ __forceinline__ void load_rec(Pkt& p, const ScatRec& r) {
 __device__ __forceinline__ void cache_energy(const KParams& P, const Geo* g, Pkt& p) {
   p.ie = grid_lookup(g->E_ph, C2D_N_VOL, g->eph_start, g->eph_k0, p.xnu);
 #if C2D_TABLE_COMTOT
-  const double s = (c2d_log(p.xnu) - C2D_COMTAB_U0) * P.comtab_du_inv;
+  const double s = (c2d_log_pos(p.xnu) - C2D_COMTAB_U0) * P.comtab_du_inv;   /* = c2d_log, branch-free */
   if (s >= 1.0 && s < (double)(C2D_COMTAB_N - 3)) {
     p.tg = (int32_t)s;
     p.tt = s - (double)p.tg;
@@ -1742,7 +1763,7 @@ __device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bun
   Pkt& p = b.p;
   load_source(P, p, b.src);
   const double ew0 = p.ew;
-  const double s_ew = ew0 / P.split1;          /* imctrk2d.f:106-123 */
+  const double s_ew = FDIV_POS(ew0, (double)P.split1);   /* imctrk2d.f:106-123 */
   const int G = min(P.split1 - b.g0, BUNDLE_MAX);
   b.ewp = s_ew;
   b.wtminp = 1.0e-10 * ew0;
@@ -1752,7 +1773,7 @@ __device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bun
   b.flags = 0;
   b.tsteps = 0;
   b.tau = 0.0;
-  if (G > 0) b.tau = -c2d_log_pos(UB(b)) / (double)G;
+  if (G > 0) b.tau = FDIV_POS(-c2d_log_pos(UB(b)), (double)G);
   p.nflight = 0;
   p.mode = 0;
   if (b.g0 + G == P.split1 && P.split1 - b.nscat > 0) {
@@ -1791,7 +1812,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
     const double mr = UB(b);
     const double sstar = FDIV_POS(-c2d_log_pos(1.0 - FDIV_POS(mr * deleabs, b.ewp)), sigabs);
     const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
-    wmustar = (wmu * rpre + sstar) / denom;
+    wmustar = FDIV_POS(wmu * rpre + sstar, denom);
   }
   cell_add(P, T, TC_EDEP, cell, deleabs);
   cell_add(P, T, TC_PRDEP, cell, deleabs * wmustar * C_LIGHT);
@@ -1800,7 +1821,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
     return;
   }
   LC_ADD(lc, C2D_CNT_COLLIDE);
-  double Eta2 = clampd((trld + Eta * rpre) / rnew, lim9);   /* H1 */
+  double Eta2 = clampd(FDIV_NN(trld + Eta * rpre, rnew), lim9);   /* H1 */
   double phi = c2d_acos(Eta2);
   if (eta_switch == -1) phi = 2.0 * PI_REF - phi;
   ScatRec r;
@@ -1988,7 +2009,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
       znew = zpre + trld * wmu;
     }
     p.dcen = p.dcen - trld;
-    double Etan = (trld + Eta * rpre) / rnew;   /* hazard H1: trld, not f (imctrk2d.f:472) */
+    double Etan = FDIV_NN(trld + Eta * rpre, rnew);   /* hazard H1: trld, not f (imctrk2d.f:472) */
     Etan = clampd(Etan, lim9);
     const bool leaves = bnd && (jnew == P.nz + 1 || jnew == 0 || knew == P.nr + 1 || knew == 0);
 #if C2D_TABLE_COMTOT

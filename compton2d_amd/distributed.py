@@ -52,10 +52,17 @@ def is_dist() -> bool:
 
 
 def allreduce_tallies(tensor) -> None:
-    """Sum the fused tally buffer over all ranks in place (no-op for one rank)."""
+    """Sum the fused tally buffer over all ranks in place (no-op for one rank).
+
+    The reduction is ordered on torch's stream only, while the engine reads
+    the tallies (n_field, ecens for c2d_fp_step) on its own non-blocking HIP
+    stream: wait for it here so the engine never sees un-reduced tallies."""
     if is_dist():
+        import torch
         import torch.distributed as dist
         dist.all_reduce(tensor, op=dist.ReduceOp.SUM)
+        if tensor.is_cuda:
+            torch.cuda.synchronize(tensor.device)
 
 
 def allreduce_max(value: float, device=None) -> float:

@@ -3,7 +3,7 @@ algorithm with the reference's own lagged-Fibonacci streams (C oracle, glibc;
 bit-exact to the Fortran reference, tests/test_oracle_golden.py) on the
 north-star spectrum workload (tests/spectrum_case.py), 3 seeds, and the
 light curves of the lineage-stream run's 8 shards (the oracle's lineage mode:
-the GPU's streams and probe bundles), whose shard-to-shard scatter sizes the
+the GPU's SplitMix64 draw streams, Philox-derived keys, and probe bundles), whose shard-to-shard scatter sizes the
 statistical error of a 1e7-packet run.  The GPU spectrum test compares the
 fast kernel against it.
 

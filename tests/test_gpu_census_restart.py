@@ -108,6 +108,30 @@ def test_fast_census_azimuth_encoding():
     b.close()
 
 
+def test_fast_census_small_azimuth_round_trip():
+    """phi < 1e-10 is the reference's eta_switch = -1 case (imctrk2d.f:228-232):
+    the import encodes cos(phi) = 1.0 with the switch, which the kernel never
+    writes itself (it clamps the cosine to 0.999999999), and the export
+    decodes it to 0.0 — so an imported phi = 0 comes back as 0."""
+    gc = GoldenCase("c3_mrk421")
+    a = Engine(gc.grid(comtot_mode=abi.COMTOT_TABLE))
+    a.transport_step(gc.step_inputs(0))
+    d6, i5, keys = a.census()
+    a.close()
+    phis = np.array([0.0, 5.0e-11, 1.0e-10, 1.0e-6, 1.0, 3.0, 4.0, 6.0])
+    m = len(phis)
+    d6, i5, keys = d6[:m].copy(), i5[:m].copy(), keys[:m].copy()
+    d6[:, 3] = phis
+    b = Engine(gc.grid(comtot_mode=abi.COMTOT_TABLE))
+    b.import_census(d6, i5, keys)
+    e6, _, ekeys = b.census()
+    b.close()
+    back = dict(zip(ekeys.tolist(), e6[:, 3].tolist()))
+    got = np.array([back[k] for k in keys.tolist()])
+    assert got[0] == 0.0 and got[1] == 0.0, got
+    np.testing.assert_allclose(got[2:], phis[2:], rtol=0, atol=1e-9)
+
+
 @pytest.mark.parametrize("inplace", [0, 1])
 @pytest.mark.parametrize("mode", [abi.COMTOT_EXACT, abi.COMTOT_TABLE])
 def test_census_overflow_is_reported(mode, inplace):

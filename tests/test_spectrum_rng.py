@@ -2,8 +2,8 @@
 L2 on F(E) of spb.dat between the reference's algorithm with the reference's
 own lagged-Fibonacci streams (C oracle, glibc, rand_switch = 1: bit-exact to
 the Fortran reference, tests/test_oracle_golden.py) and the same algorithm
-with the engine's per-packet Philox lineage streams — the RNG swap the GPU
-makes — with the reference's own seed-to-seed floor reported beside it.
+with the engine's per-packet lineage streams (SplitMix64 draw streams whose
+keys are derived with Philox, csrc/c2d_rng.h) — the RNG swap the GPU makes — with the reference's own seed-to-seed floor reported beside it.
 Reference side: 3 seeds x ~1.9e6 escapes, averaged; lineage side: ~9.5e6
 escapes (tests/spectrum_case.py).  Same for the light curves (edout).
 
