@@ -30,6 +30,11 @@
 #ifndef C2D_MDIV
 #define C2D_MDIV(a, b) ((a) / (b))
 #endif
+/* a * b + c in the series' polynomial (Horner) steps: two roundings here;
+ * the fast transport build may define it as one fused multiply-add */
+#ifndef C2D_MADD
+#define C2D_MADD(a, b, c) ((a) * (b) + (c))
+#endif
 
 C2D_HD uint64_t c2d_bits(double x) {
   uint64_t u;
@@ -134,8 +139,8 @@ C2D_HD double c2d_log_pos(double x) {
   const double s = C2D_MDIV(f, 2.0 + f);
   const double z = s * s;
   const double w = z * z;
-  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
-  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  const double t1 = w * C2D_MADD(w, C2D_MADD(w, Lg6, Lg4), Lg2);
+  const double t2 = z * C2D_MADD(w, C2D_MADD(w, C2D_MADD(w, Lg7, Lg5), Lg3), Lg1);
   const double R = t2 + t1;
   const double hfsq = 0.5 * f * f;
   const double big_a = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
@@ -185,7 +190,7 @@ C2D_HD double c2d_exp(double x) {
     k = 0;
   }
   double t = x * x;
-  double c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+  double c = x - t * C2D_MADD(t, C2D_MADD(t, C2D_MADD(t, C2D_MADD(t, P5, P4), P3), P2), P1);
   if (k == 0) return 1.0 - (C2D_MDIV(x * c, c - 2.0) - x);
   double y = 1.0 - ((lo - C2D_MDIV(x * c, 2.0 - c)) - hi);
   if (k >= -1021) return c2d_with_hi(y, (int32_t)((uint32_t)c2d_hi(y) + ((uint32_t)k << 20)));
@@ -291,14 +296,14 @@ C2D_HD double c2d_acos(double x) {
   if (ix < 0x3fe00000) {                     /* |x| < 0.5 */
     if (ix <= 0x3c600000) return pio2_hi + pio2_lo;
     double z = x * x;
-    double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-    double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    double p = z * C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, pS5, pS4), pS3), pS2), pS1), pS0);
+    double q = C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, qS4, qS3), qS2), qS1), 1.0);
     double r = C2D_MDIV(p, q);
     return pio2_hi - (x - (pio2_lo - x * r));
   } else if (hx < 0) {                       /* x < -0.5 */
     double z = (1.0 + x) * 0.5;
-    double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-    double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    double p = z * C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, pS5, pS4), pS3), pS2), pS1), pS0);
+    double q = C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, qS4, qS3), qS2), qS1), 1.0);
     double s = __builtin_sqrt(z);
     double r = C2D_MDIV(p, q);
     double w = r * s - pio2_lo;
@@ -308,8 +313,8 @@ C2D_HD double c2d_acos(double x) {
     double s = __builtin_sqrt(z);
     double df = c2d_with_lo0(s);
     double c = C2D_MDIV(z - df * df, s + df);
-    double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-    double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    double p = z * C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, pS5, pS4), pS3), pS2), pS1), pS0);
+    double q = C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, C2D_MADD(z, qS4, qS3), qS2), qS1), 1.0);
     double r = C2D_MDIV(p, q);
     double w = r * s + c;
     return 2.0 * (df + w);

@@ -54,6 +54,17 @@ __device__ __forceinline__ double c2d_mdiv_rcp(double a, double b) {
 }
 #define C2D_MDIV(a, b) c2d_mdiv_rcp((a), (b))
 #endif
+/* C2D_FAST_FMA (fast build): the Horner steps of those series (and of the
+ * point loop's -log(1-x) series) as fused multiply-adds.  Off: gfx950's
+ * v_fmac_f64 takes the addend in the destination VGPR, so each f64
+ * coefficient costs two v_mov_b32 instead of two s_mov_b32 (+83 VALU
+ * instructions in the bundle kernel, -117 in all) */
+#ifndef C2D_FAST_FMA
+#define C2D_FAST_FMA 0
+#endif
+#if defined(C2D_VARIANT) && C2D_VARIANT == 1 && C2D_FAST_FMA
+#define C2D_MADD(a, b, c) __builtin_fma((a), (b), (c))
+#endif
 
 #include "c2d_device.hpp"
 #include "c2d_math.h"
@@ -107,16 +118,19 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 
 /* Fast build only (the exact build keeps the oracle's c2d_math and IEEE
  * division bit for bit):
- *   C2D_FAST_EXP  exp by the ROCm device library (branch-free, ~42 VALU
+ *   C2D_FAST_EXP  1: exp by the ROCm device library (branch-free, ~42 VALU
  *                 instead of fdlibm's ~99 with its branches and division);
+ *                 2: fdlibm's general path without its branches (exp_neg);
  *   C2D_FAST_DIV  a / b for b finite and nonzero as a * (1/b), the reciprocal
  *                 from v_rcp_f64 and two Newton steps (~1 ulp);
  *   C2D_RSQ_NR    Newton steps after v_rsq_f64 in the survivors' point loop.
  * A/B on the C3 census (profiles/r03_microopt.txt): FAST_DIV +2 % (on),
- * FAST_EXP -4 % (off: ocml's exp keeps more VGPRs live), RSQ_NR=1 +1 %
- * (within noise; kept at 2 for the geometry's precision). */
+ * FAST_EXP=1 -4 % (ocml's exp keeps more VGPRs live), RSQ_NR=1 +1 %
+ * (within noise; kept at 2 for the geometry's precision).  On the
+ * steady-state C3 census (profiles/r03k): FAST_EXP=2 +1 % (default),
+ * C2D_FAST_MDIV +1.2 %. */
 #ifndef C2D_FAST_EXP
-#define C2D_FAST_EXP 0
+#define C2D_FAST_EXP 2
 #endif
 #ifndef C2D_FAST_DIV
 #define C2D_FAST_DIV 1
@@ -124,8 +138,30 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 #ifndef C2D_RSQ_NR
 #define C2D_RSQ_NR 2
 #endif
-#if C2D_TABLE_COMTOT && C2D_FAST_EXP
+#if C2D_TABLE_COMTOT && C2D_FAST_EXP == 1
 #define FEXP(x) exp(x)
+#elif C2D_TABLE_COMTOT && C2D_FAST_EXP == 2
+/* exp(x) for -100 < x <= 0 (every use: exp(-xabs) with xabs < 100) without
+ * branches: fdlibm's general reduction x = k ln2 + r for every x.  Its
+ * |x| < 1.5 ln2 special cases are this path with k = 0 / -1 (same hi, lo and
+ * result), and 2^k never leaves the normal range, so the result equals
+ * c2d_exp except that |x| < 2^-28 gives 1 + x + x^2/2 before rounding. */
+__device__ __forceinline__ double exp_neg(double x) {
+  const double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10,
+               invln2 = 1.44269504088896338700e+00,
+               P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+               P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+               P5 = 4.13813679705723846039e-08;
+  const int32_t k = (int32_t)(invln2 * x - 0.5);
+  const double t = (double)k;
+  const double hi = x - t * ln2HI, lo = t * ln2LO;
+  const double r = hi - lo;
+  const double rr = r * r;
+  const double c = r - rr * (P1 + rr * (P2 + rr * (P3 + rr * (P4 + rr * P5))));
+  const double y = 1.0 - ((lo - C2D_MDIV(r * c, 2.0 - c)) - hi);
+  return c2d_with_hi(y, (int32_t)((uint32_t)c2d_hi(y) + ((uint32_t)k << 20)));
+}
+#define FEXP(x) exp_neg(x)
 #else
 #define FEXP(x) c2d_exp(x)
 #endif
@@ -2076,8 +2112,9 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
              * 1e-4 with 4 terms -3 %, 0.05 with 12 terms or 2 atanh(x/(2-x))
              * below 0.2: no better, r02ap-aq) */
             const double L = (x < 1.0e-2)
-                ? x * (1.0 + x * (0.5 + x * (0.33333333333333333 + x * (0.25 + x * (0.2 + x * (
-                      0.16666666666666667 + x * (0.14285714285714286 + x * 0.125)))))))
+                ? x * C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x,
+                      C2D_MADD(x, 0.125, 0.14285714285714286), 0.16666666666666667), 0.2), 0.25),
+                      0.33333333333333333), 0.5), 1.0)
                 : -c2d_log_pos(1.0 - x);
 #else
             const double L = -c2d_log_pos(1.0 - x);
