@@ -15,14 +15,21 @@ sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
 def main():
     from compton2d_amd.engine import Engine
     from fp_bench import tiled_case
-    c, g, tile = tiled_case(8, 8)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nz", type=int, default=8)
+    ap.add_argument("--nr", type=int, default=8)
+    ap.add_argument("--vary", action="store_true")
+    args = ap.parse_args()
+    c, g, tile = tiled_case(args.nz, args.nr, vary=args.vary)
     g.device = 0
     eng = Engine(g)
     eng.fp_set_config(c.constants())
     r = eng.fp_step(tile["ncycle"], tile["time"], tile["dt"], tile, tile)
     d = np.asarray(r["zone_diag"]).reshape(-1, 8)
     steps = d[:, 5]
-    out = {"zones": len(d), "substeps_mean": float(steps.mean()), "kernel_ms": eng.last_fp_ms()}
+    out = {"zones": len(d), "substeps_mean": float(steps.mean()), "kernel_ms": eng.last_fp_ms(),
+           "waves_per_zone": eng.last_fp_waves() if hasattr(eng, "last_fp_waves") else None}
     for i, k in enumerate(("search_cycles", "tridag_cycles", "loop_cycles", "search_calls")):
         out[k + "_per_substep"] = float((d[:, i] / steps).mean())
     print(json.dumps(out))

@@ -15,6 +15,7 @@
 #   profile        rocprofv3 kernel trace + PMC passes of the C3 bench (tools/gpu_profile.sh)
 #   fp             tools/fp_bench.py off the clamp: 30x9, varied zones, memo on and off
 #   fppmc          rocprofv3 kernel trace + SQ counters of that FP run (memo on)
+#   fpprof         FP section timers off the clamp (sweep build "fpprof", tools/fp_prof.py)
 #   trprof         wave section timers of the C3 run (sweep build "prof", tools/tr_prof.py)
 #   n2             rehearse bench.py's N>1 path: 2 gloo ranks on device 0 vs 1 rank
 set -o pipefail
@@ -84,6 +85,9 @@ for r in "$@"; do
             --output-format csv -- python3 $FPB > "$F/sq.out" 2> "$F/sq.err" ) \
         || { echo "fppmc failed"; tail -5 "$F"/*.err; exit 1; }
       python3 tools/pmc_summary.py "$F" > "$F/summary.txt"; grep -E "FP kernel|fp sq|c2d_fp" "$F/summary.txt" ;;
+    fpprof)  # FP section timers of the -DC2D_FP_PROF build (make FP_FLAGS=-DC2D_FP_PROF OUT=sweep/fpprof/...)
+      C2D_LIBRARY=$PWD/compton2d_amd/sweep/fpprof/libcompton2d.so run 300 fpprof python tools/fp_prof.py --nz 30 --nr 9 --vary
+      tail -1 "$O/fpprof.out" ;;
     trprof)  # section timers of the -DC2D_TR_PROF build (tools/build_sweep.sh prof:3:off:...,-DC2D_TR_PROF)
       C2D_LIBRARY=$PWD/compton2d_amd/sweep/prof/libcompton2d.so run 300 trprof python tools/tr_prof.py --steps ${STEPS}
       tail -2 "$O/trprof.out" ;;
