@@ -59,6 +59,55 @@ __device__ __forceinline__ void seq_sum2(double& a1, double& a2, int lo, int hi,
   }
 }
 
+/* The same in-order sums with the lane-parallel values staged through `scr`
+ * (LDS, FPB doubles per value owned by this wave): every lane reads them back
+ * with broadcast loads that issue ahead of the add chain, so the chain runs
+ * at the adds' latency instead of a readlane's SGPR hazards (mcdonald23_from
+ * below measured ~15 against ~108 cycles per term). */
+__device__ __forceinline__ void wave_sync();
+template <class F>
+__device__ __forceinline__ double seq_sum_lds(double acc, int lo, int hi, int lane, double* scr, F f) {
+  for (int c0 = lo; c0 <= hi; c0 += FPB) {
+    const int i = c0 + lane;
+    scr[lane] = (i <= hi) ? f(i) : 0.0;
+    wave_sync();
+    const int mn = (hi - c0 + 1) < FPB ? (hi - c0 + 1) : FPB;
+    if (mn == FPB) {
+#pragma unroll 16
+      for (int m = 0; m < FPB; m++) acc = acc + scr[m];
+    } else {
+      for (int m = 0; m < mn; m++) acc = acc + scr[m];
+    }
+    wave_sync();
+  }
+  return acc;
+}
+/* two interleaved in-order sums; scr holds 2*FPB doubles */
+template <class F, class G>
+__device__ __forceinline__ void seq_sum2_lds(double& a1, double& a2, int lo, int hi, int lane, double* scr,
+                                             F f, G g) {
+  for (int c0 = lo; c0 <= hi; c0 += FPB) {
+    const int i = c0 + lane;
+    scr[lane] = (i <= hi) ? f(i) : 0.0;
+    scr[FPB + lane] = (i <= hi) ? g(i) : 0.0;
+    wave_sync();
+    const int mn = (hi - c0 + 1) < FPB ? (hi - c0 + 1) : FPB;
+    if (mn == FPB) {
+#pragma unroll 16
+      for (int m = 0; m < FPB; m++) {
+        a1 = a1 + scr[m];
+        a2 = a2 + scr[FPB + m];
+      }
+    } else {
+      for (int m = 0; m < mn; m++) {
+        a1 = a1 + scr[m];
+        a2 = a2 + scr[FPB + m];
+      }
+    }
+    wave_sync();
+  }
+}
+
 /* gammln (volume2d.f:647-668) */
 __device__ inline double gammln(double xx) {
   const double cof[6] = {76.18009172947146, -86.50532032941677, 24.01409824083091,

@@ -483,6 +483,7 @@ __shared__ double s_a[NT + 2], s_b[NT + 2], s_c[NT + 2];
 __shared__ double s_mcd[4 * FPB];   /* McDonald term exchange (c2d_wave.hpp) */
 __shared__ double s_smw[NT + 2], s_bigW[NT + 2], s_bigC[NT + 2], s_em[NT + 2], s_inj[NT + 2];
 __shared__ double s_Pnt[NT + 2], s_nf[NPH];
+__shared__ double s_seq[2 * FPB];  /* in-order sums: wave 0's staged values (seq_sum_lds) */
 __shared__ McdCoop s_coop;
 __shared__ McdBatch<FPB> s_batch1;
 __shared__ McdBatch<NB_MAX> s_batch8;
@@ -537,12 +538,12 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
 
   /* E_el, normalisation (:482-509) */
   double E_el = 0.0, E_pos = 0.0;
-  E_el = seq_sum(E_el, 2, NT, lane,
+  E_el = seq_sum_lds(E_el, 2, NT, lane, s_seq,
                  [&](int i) { return (s_gnt[i] - s_gnt[i - 1]) * s_gam[i] * s_fold[i]; });
   E_el = E_el * ne * 8.176e-7 * volume;
   double e_old = 0.0 + E_el + E_pos + zin[FZ_ECOLD];
   double e_new = 0.0 + ecens;
-  double sum_p = seq_sum(0., 1, NT - 1, lane,
+  double sum_p = seq_sum_lds(0., 1, NT - 1, lane, s_seq,
                          [&](int i) { return (s_gnt[i + 1] - s_gnt[i]) * s_fold[i]; });
   fp_sync<WMAX>();
   for (int i = lane + 1; i <= NT; i += FPB) s_fold[i] = s_fold[i] / sum_p;
@@ -614,14 +615,15 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
    * the walk follows its chain, by a new batch once this search has taken
    * FP_NSINGLE steps (it is walking far), else singly (memo / cooperative
    * series).  bdir = 0: no usable batch. */
-  int bdir = 0, bpos = 0;
+  int bdir = 0, bpos = 0, bn = 0;
   auto search_eval = [&](double prev, double next, int dir, int k) -> double {
     auto& B = batch_lds<WMAX>();
-    if (bdir == dir && bpos < fp_nwaves<WMAX>() * FPB && B.bc[bpos] == next) return B.bg[bpos++];
+    if (bdir == dir && bpos < bn && B.bc[bpos] == next) return B.bg[bpos++];
     if (k >= FP_NSINGLE && next >= F32(0.2)) {
       search_batch<WMAX>(s_coop, B, prev, dir, lane, P.mcd, guard, memo);
       bdir = dir;
       bpos = 1;
+      bn = fp_nwaves<WMAX>() * FPB;
       return B.bg[0];
     }
     bdir = 0;
@@ -639,7 +641,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
     /* label 200 (:577) */
     double g_av = (fp_steps == 0) ? gamma_bar_m(Th_e) : g_av_next;
     /* hr_th_c = hr_th_c - x_i, i.e. + (-x_i) bit for bit */
-    const double hr_th_c = seq_sum(0.0, 1, NT - 1, lane, [&](int i) {
+    const double hr_th_c = seq_sum_lds(0.0, 1, NT - 1, lane, s_seq, [&](int i) {
       return -(8.176e-7 * s_dgic[i] * s_fold[i] * (s_gnt[i + 1] - s_gnt[i]) * volume * n_lept);
     });
     if (fp_steps > MAX_FP_STEPS) {
@@ -681,12 +683,16 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
         st = gi > g_thr;
       }
       const unsigned long long stm = __ballot(st);
+      s_seq[lane] = v;
+      wave_sync();
       const int mn = (NT - c0) < FPB ? (NT - c0) : FPB;
+#pragma unroll 8
       for (int m = 0; m < mn; m++) {
-        const double x = rl(v, m);
+        const double x = s_seq[m];
         hr_nt_A = hr_nt_A + x;
         if ((stm >> m) & 1ull) hr_st_A = hr_st_A + x;
       }
+      wave_sync();
     }
     hr_st_A = hr_st_A * 8.176e-7 * n_lept * volume;
     hr_nt_A = hr_nt_A * 8.176e-7 * n_lept * volume;
@@ -723,7 +729,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
                    (P.inj_sigma * __builtin_sqrt(2.0 * PI_REF));
       }
       fp_sync<WMAX>();
-      inj_sum = seq_sum(0.0, 1, NT - 1, lane,
+      inj_sum = seq_sum_lds(0.0, 1, NT - 1, lane, s_seq,
                         [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); });
       inj_rho = P.pick_rate * d_t;
       inj_any = true;
@@ -736,7 +742,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
         s_fold[i] = s_fold[i] + v / ne;
       }
       fp_sync<WMAX>();
-      n_inject = seq_sum(n_inject, 1, NT - 1, lane,
+      n_inject = seq_sum_lds(n_inject, 1, NT - 1, lane, s_seq,
                          [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); });
     }
     if (P.inj_switch != 0) {
@@ -764,7 +770,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
         }
         fp_sync<WMAX>();
         double isum = 0.0, inj_E = 0.0;
-        seq_sum2(isum, inj_E, 1, NT - 1, lane,
+        seq_sum2_lds(isum, inj_E, 1, NT - 1, lane, s_seq,
                  [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); },
                  [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]) * s_gam[i]; });
         inj_E = inj_E / isum;
@@ -777,7 +783,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
           s_fold[i] = s_fold[i] + v / ne;
         }
         fp_sync<WMAX>();
-        n_inject = seq_sum(n_inject, 1, NT - 1, lane,
+        n_inject = seq_sum_lds(n_inject, 1, NT - 1, lane, s_seq,
                            [&](int i) { return s_inj[i] * (s_gnt[i + 1] - s_gnt[i]); });
       }
     }
@@ -823,35 +829,33 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
     fp_sync<WMAX>();
     PF_BEGIN();
     /* tridag (:2476-2518): the recurrences run in the reference order on
-     * wave-uniform values (readlane) with each 64-bin chunk's operands staged
-     * in registers; gam is kept in s_smw */
+     * wave-uniform values read by every lane from LDS (broadcast loads that
+     * issue ahead of the chain).  The bet/gam recurrence and the u
+     * recurrence are independent but for bet_i, so their divisions overlap;
+     * no branch per element: a vanishing bet is flagged and the solution
+     * zeroed after the sweep, as the reference's early return leaves it.
+     * Lane m keeps element c0 + m of each 64-bin chunk; gam is kept in s_smw. */
     {
       double bet = s_b[1];
       double u = s_fold[1] / bet;
       bool zero = false;
       if (lane == 0) s_fnew[1] = u;
-      for (int c0 = 2; c0 <= NT && !zero; c0 += FPB) {
-        const int i = c0 + lane;
-        const bool in = i <= NT;
-        const double av = in ? s_a[i] : 0.0, bv = in ? s_b[i] : 0.0;
-        const double cv = in ? s_c[i - 1] : 0.0, rv = in ? s_fold[i] : 0.0;
+      for (int c0 = 2; c0 <= NT; c0 += FPB) {
         double gmine = 0.0, umine = 0.0;
         const int mn = (NT - c0 + 1) < FPB ? (NT - c0 + 1) : FPB;
+#pragma unroll 4
         for (int m = 0; m < mn; m++) {
-          const double am = rl(av, m);
-          const double gam = rl(cv, m) / bet;
-          bet = rl(bv, m) - am * gam;
-          if (fabs(bet) <= 1.0e-100) {
-            zero = true;
-            break;
-          }
-          u = (rl(rv, m) - am * u) / bet;
-          if (lane == m) {
-            gmine = gam;
-            umine = u;
-          }
+          const int i = c0 + m;
+          const double am = s_a[i], bm = s_b[i], cm = s_c[i - 1], rm = s_fold[i];
+          const double gam = cm / bet;
+          bet = bm - am * gam;
+          zero = zero || (fabs(bet) <= 1.0e-100);
+          u = (rm - am * u) / bet;
+          gmine = (lane == m) ? gam : gmine;
+          umine = (lane == m) ? u : umine;
         }
-        if (!zero && in) {
+        const int i = c0 + lane;
+        if (i <= NT) {
           s_smw[i] = gmine;
           s_fnew[i] = umine;
         }
@@ -864,16 +868,16 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
          * clipping of u(2..num_nt) (each u(i+1) is clipped after u(i) used it) */
         double up = s_fnew[NT];
         for (int c1 = NT - 1; c1 >= 1; c1 -= FPB) {
-          const int i = c1 - lane;
-          const bool in = i >= 1;
-          const double fv = in ? s_fnew[i] : 0.0, gv = in ? s_smw[i + 1] : 0.0;
           double mine = 0.0;
           const int mn = c1 < FPB ? c1 : FPB;
+#pragma unroll 8
           for (int m = 0; m < mn; m++) {
-            up = rl(fv, m) - rl(gv, m) * up;
-            if (lane == m) mine = up;
+            const int i = c1 - m;
+            up = s_fnew[i] - s_smw[i + 1] * up;
+            mine = (lane == m) ? up : mine;
           }
-          if (in) s_fnew[i] = mine;
+          const int i = c1 - lane;
+          if (i >= 1) s_fnew[i] = mine;
         }
         fp_sync<WMAX>();
         for (int i = lane + 2; i <= NT; i += FPB)
@@ -897,13 +901,18 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
         av = dg * fi;
         bv = dg * s_gam[i] * fi;
       }
+      s_seq[lane] = av;
+      s_seq[FPB + lane] = bv;
+      wave_sync();
       double mine = 0.0;
       const int mn = (NT - c0) < FPB ? (NT - c0) : FPB;
+#pragma unroll 8
       for (int m = 0; m < mn; m++) {
-        sum_p = sum_p + rl(av, m);
-        sE = sE + rl(bv, m);
-        if (lane == m) mine = sum_p;
+        sum_p = sum_p + s_seq[m];
+        sE = sE + s_seq[FPB + m];
+        mine = (lane == m) ? sum_p : mine;
       }
+      wave_sync();
       if (i <= NT - 1) s_Pnt[i] = mine;
     }
     sum_E = sE / sum_p;
@@ -917,7 +926,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
     }
     fp_sync<WMAX>();
     /* new temperature (:1440-1468) */
-    const double gbar = seq_sum(0.0, 1, NT - 1, lane, [&](int i) {
+    const double gbar = seq_sum_lds(0.0, 1, NT - 1, lane, s_seq, [&](int i) {
       return s_gam[i] * s_fnew[i] * (s_gnt[i + 1] - s_gnt[i]);
     });
     double The_new = Th_e;
@@ -960,7 +969,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
   /* outputs (:1481-1500) */
   E_el = 0.0;
   E_pos = 0.0;
-  E_el = seq_sum(E_el, 2, NT, lane,
+  E_el = seq_sum_lds(E_el, 2, NT, lane, s_seq,
                  [&](int i) { return s_fnew[i] * s_gam[i] * (s_gnt[i] - s_gnt[i - 1]); });
   E_el = E_el * ne * 8.176e-7 * volume;
   e_new = e_new + E_el + E_pos;
@@ -978,8 +987,8 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
     if (s_fnew[i] > 1.0e-15) break;
   const double gmax = s_gam[i];
   const auto dfn = [&](int q) { return (s_gam[q + 1] - s_gam[q]) * s_fnew[q]; };
-  const double sum_th = seq_sum(0.0, 1, i_nt - 1, lane, dfn);
-  const double sum_nt = seq_sum(0.0, i_nt, NT - 1, lane, dfn);
+  const double sum_th = seq_sum_lds(0.0, 1, i_nt - 1, lane, s_seq, dfn);
+  const double sum_nt = seq_sum_lds(0.0, i_nt, NT - 1, lane, s_seq, dfn);
   double amxwl = sum_th / (sum_nt + sum_th);
   double p_nth = zin[FZ_PNTH];
   if (amxwl > 9.999e-1) {
@@ -1012,11 +1021,16 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
           v1 = f_pl * s_gam[q] * (s_gnt[q + 1] - s_gnt[q]);
           v2 = f_pl * (s_gnt[q + 1] - s_gnt[q]);
         }
+        s_seq[lane] = v1;
+        s_seq[FPB + lane] = v2;
+        wave_sync();
         const int mn = (i_end - c0) < FPB ? (i_end - c0) : FPB;
+#pragma unroll 8
         for (int m = 0; m < mn; m++) {
-          sum_g = sum_g + rl(v1, m);
-          sum_gg = sum_gg + rl(v2, m);
+          sum_g = sum_g + s_seq[m];
+          sum_gg = sum_gg + s_seq[FPB + m];
         }
+        wave_sync();
       }
       sum_g = sum_g / sum_gg;
       sum_g = fabs(sum_g - sum_E);

@@ -172,12 +172,34 @@ __device__ __forceinline__ double rcp_pos(double b) {
   return __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
 }
 #define FDIV_POS(a, b) ((a) * rcp_pos(b))
+/* C2D_FAST_SQRT: the bundle step's square roots (distances, radii, |sin|)
+ * as x * rsq(x) with two Newton steps on rsq (~1 ulp; max rel. error of the
+ * same sequence in the point loop 2.6e-16 on the box) instead of the
+ * correctly rounded ~17-instruction sequence; x floored at 1e-300 so a zero
+ * radius gives a tiny one (the quotients by it are clamped, FDIV_NN) */
+#ifndef C2D_FAST_SQRT
+#define C2D_FAST_SQRT 1
+#endif
+#if C2D_FAST_SQRT
+__device__ __forceinline__ double fsqrt_nn(double x) {
+  x = fmax(x, 1.0e-300);
+  const double h = 0.5 * x;
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * __builtin_fma(-h, y * y, 1.5);
+  y = y * __builtin_fma(-h, y * y, 1.5);
+  return x * y;
+}
+#define FSQRT(x) fsqrt_nn(x)
+#else
+#define FSQRT(x) __builtin_sqrt(x)
+#endif
 /* b >= 0 that may be 0 (a radius): b floored at 1e-300, so a / 0 gives a
  * huge value of a's sign (clamped by the caller) and 0 / 0 gives 0 */
 #define FDIV_NN(a, b) ((a) * rcp_pos(fmax((b), 1.0e-300)))
 #else
 #define FDIV_POS(a, b) ((a) / (b))
 #define FDIV_NN(a, b) ((a) / (b))
+#define FSQRT(x) __builtin_sqrt(x)
 #endif
 
 /* Fortran REAL literals promoted to double (src/imcvol2d_para.f:204,221,247,268,336) */
@@ -951,6 +973,7 @@ enum : int {
   TP_ABS = 3,       /* flight: absorption, wmustar sampling, deposits     */
   TP_EVENT = 4,     /* flight: acos, census write, escape, collision      */
   TP_POST = 5,      /* push_scat, probe restart from the source record    */
+  TP_PTS = 6,       /* bundle: the survivors' absorption points           */
   TP_ITER = 8,      /* loop iterations (waves)                            */
   TP_LANES = 9,     /* sum of lanes in flight over iterations             */
   TP_GOT_W = 10, TP_GOT_L = 11,       /* new items: waves, lanes        */
@@ -1834,7 +1857,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
   const double rpre = p.rpre, zpre = p.zpre, wmu = p.wmu;
   const double trld = dcol;
   const double f = trld * swmu;
-  const double rnew = __builtin_sqrt(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
+  const double rnew = FSQRT(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
   const double znew = zpre + trld * wmu;
   const double xabs = sigabs * trld;
   const double ewnew = (xabs < 100.0) ? b.ewp * FEXP(-xabs) : 0.0;
@@ -1847,7 +1870,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
     /* one draw: mr < 1 <= ew / deleabs always holds (ew >= 1e-40) */
     const double mr = UB(b);
     const double sstar = FDIV_POS(-c2d_log_pos(1.0 - FDIV_POS(mr * deleabs, b.ewp)), sigabs);
-    const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
+    const double denom = FSQRT(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
     wmustar = FDIV_POS(wmu * rpre + sstar, denom);
   }
   cell_add(P, T, TC_EDEP, cell, deleabs);
@@ -1948,8 +1971,8 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
   }
   double dpbsq = rbnd * rbnd - psq;
   if (dpbsq < 1.0e-6) dpbsq = 1.0e-6;
-  const double disbr = (double)inout * __builtin_sqrt(dpbsq) - disp;
-  const double swmu = __builtin_sqrt(1.0 - wmu * wmu);
+  const double disbr = (double)inout * FSQRT(dpbsq) - disp;
+  const double swmu = FSQRT(1.0 - wmu * wmu);
   double trldb = FDIV_POS(disbr, swmu);
   const double Zr = zpre + wmu * trldb;
   const double zlow = (p.jph == 1) ? P.zmin : g->z[p.jph - 1];
@@ -1959,8 +1982,8 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
     knew = p.kph;
     jnew = (Zr > zup) ? p.jph + 1 : p.jph - 1;
     const double f = FDIV_POS((Zbnd - zpre) * swmu, wmu);   /* wmu != 0 on a z crossing */
-    rbnd = __builtin_sqrt(rpre * rpre + f * f + 2.0 * rpre * f * Eta);
-    trldb = __builtin_sqrt(f * f + (Zbnd - zpre) * (Zbnd - zpre));
+    rbnd = FSQRT(rpre * rpre + f * f + 2.0 * rpre * f * Eta);
+    trldb = FSQRT(f * f + (Zbnd - zpre) * (Zbnd - zpre));
   } else {
     knew = p.kph + inout;
     jnew = p.jph;
@@ -2041,7 +2064,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
       jnew = p.jph;
       knew = p.kph;
       const double f = trld * swmu;
-      rnew = __builtin_sqrt(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
+      rnew = FSQRT(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
       znew = zpre + trld * wmu;
     }
     p.dcen = p.dcen - trld;
@@ -2086,6 +2109,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
   }
   /* ---- the survivors' absorption points and deposits (imctrk2d.f:382-462),
    * at the step's starting point ---- */
+  TP_MARK(pf, TP_EVENT);
   if (nabs > 0) {
     double sum_prdep = 0.0;
 #ifdef C2D_ABLATE_PROBE_ABS            /* profiling ablation only (tools/build_sweep.sh) */
@@ -2129,7 +2153,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
             sum_prdep += dabs * ((Aw + sstar) * y) * C_LIGHT;
 #else
             const double sstar = -c2d_log_pos(1.0 - x) / sigabs;
-            const double denom = __builtin_sqrt(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
+            const double denom = FSQRT(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
             sum_prdep += dabs * ((wmu * rpre + sstar) / denom) * C_LIGHT;
 #endif
           }
@@ -2141,6 +2165,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
     cell_add(P, T, TC_EDEP, cell, (double)nabs * dabs);
     cell_add(P, T, TC_PRDEP, cell, sum_prdep);
   }
+  TP_MARK(pf, TP_PTS);
 }
 
 __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(const KParams* __restrict__ Pg,

@@ -14,6 +14,7 @@
 #                  "base" = the in-tree library), SPINUP/STEPS/WARMUP
 #   profile        rocprofv3 kernel trace + PMC passes of the C3 bench (tools/gpu_profile.sh)
 #   fp             tools/fp_bench.py off the clamp: 30x9, varied zones, memo on and off
+#   fpab:<t1>,..   the fp run for each build (as ab:)
 #   fppmc          rocprofv3 kernel trace + SQ counters of that FP run (memo on)
 #   fpprof         FP section timers off the clamp (sweep build "fpprof", tools/fp_prof.py)
 #   trprof         wave section timers of the C3 run (sweep build "prof", tools/tr_prof.py)
@@ -73,6 +74,12 @@ for r in "$@"; do
       for m in 1 0; do
         C2D_FP_MEMO=$m run 300 "fp_memo$m" python tools/fp_bench.py --nz 30 --nr 9 --vary --reps 3 --cpu-zones 8
         tail -1 "$O/fp_memo$m.out"
+      done ;;
+    fpab:*)  # tools/fp_bench.py off the clamp for each build (as ab:, memo on)
+      for t in $(echo "${r#fpab:}" | tr ',' ' '); do
+        lib=""; [ "$t" = base ] || lib=$PWD/compton2d_amd/sweep/$t/libcompton2d.so
+        C2D_LIBRARY=$lib run 300 "fpab_$t" python tools/fp_bench.py --nz 30 --nr 9 --vary --reps 3 --cpu-zones 8
+        echo "fpab_$t $(tail -1 $O/fpab_$t.out | cut -c1-200)"
       done ;;
     fppmc)   # kernel trace + SQ counters of the off-clamp FP run (memo on)
       R=$PWD; F=$R/$O/fpprof; mkdir -p "$F"

@@ -20,12 +20,12 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT)]
 
-SECTIONS = ["refill", "start", "geom", "abs", "event", "post"]
+SECTIONS = ["refill", "start", "geom", "abs", "event", "post", "points"]
 COUNTS = {"got": 10, "census": 12, "leak": 14, "collide": 16, "restart": 18}
 
 
 def summarize(v, steps):
-    cyc = [float(v[i]) for i in range(6)]
+    cyc = [float(v[i]) for i in range(len(SECTIONS))]
     tot = sum(cyc) or 1.0
     it = float(v[8]) or 1.0
     out = {"packet_steps": steps, "waves": int(v[20]), "iterations": int(v[8]),
