@@ -974,6 +974,7 @@ enum : int {
   TP_EVENT = 4,     /* flight: acos, census write, escape, collision      */
   TP_POST = 5,      /* push_scat, probe restart from the source record    */
   TP_PTS = 6,       /* bundle: the survivors' absorption points           */
+  TP_CWR = 7,       /* bundle: the escape / census write of the step      */
   TP_ITER = 8,      /* loop iterations (waves)                            */
   TP_LANES = 9,     /* sum of lanes in flight over iterations             */
   TP_GOT_W = 10, TP_GOT_L = 11,       /* new items: waves, lanes        */
@@ -2083,6 +2084,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
 #endif
     p.rpre = rnew;
     p.zpre = znew;
+    TP_MARK(pf, TP_EVENT);
     if (bnd) {
       if (leaves) {
         b.alive = 0;                            /* probes leaving end (no tally) */
@@ -2106,6 +2108,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
         b.flags &= ~BF_TRACK;
       }
     }
+    TP_MARK(pf, TP_CWR);
   }
   /* ---- the survivors' absorption points and deposits (imctrk2d.f:382-462),
    * at the step's starting point ---- */

@@ -20,7 +20,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT)]
 
-SECTIONS = ["refill", "start", "geom", "abs", "event", "post", "points"]
+SECTIONS = ["refill", "start", "geom", "abs", "event", "post", "points", "write"]
 COUNTS = {"got": 10, "census": 12, "leak": 14, "collide": 16, "restart": 18}
 
 
