@@ -853,55 +853,11 @@ C2D_COLD_FN void census_item_done(const KParams& P0, long long slot) {
   atomicAdd(&c2d_cnt_lds[C2D_CNT_CREUSE_INT], 1u);
 }
 
-/* census write (src/imctrk2d.f:528-578): appended to the wave's chunk.
- * Order: the LDS reads (chunk base, the E_field bin) are issued first and
- * waited for together, then the record stores and the n_field atomic, and
- * the LDS tally atomics last -- LDS operations complete in order, so a read
- * issued after the atomics would wait for their bank conflicts
- * (C2D_CW_ORDER=0: the former order, for A/B). */
-#ifndef C2D_CW_ORDER
-#define C2D_CW_ORDER 1
-#endif
+/* census write (src/imctrk2d.f:528-578): appended to the wave's chunk */
 C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, LaneCnt& lc) {
   const KParams& P = cold(P0);
   const Geo* g = T.g;
   int cell = (p.jph - 1) * P.nr + (p.kph - 1);
-#if C2D_CW_ORDER
-  const uint64_t ckey = c2d_census_key(p.key, p.ctr, p.sub);
-  const unsigned long long slot = census_slot_chunk(P);
-#ifdef C2D_ABLATE_NFIELD                /* profiling ablation only (tools/build_sweep.sh) */
-  const bool nf = p.xnu < 0.0;
-#else
-  const bool nf = p.xnu > P.egg_min;    /* Egg_min = E_field(1)^2/E_field(2), host-computed */
-#endif
-  const int ib = grid_lookup(g->E_field, C2D_NPHFIELD, g->efl_start, g->efl_k0, p.xnu);
-  if (slot < (unsigned long long)P.cap_cout) {
-    gst(P.cout.rpre + slot, p.rpre);
-    gst(P.cout.zpre + slot, p.zpre);
-    gst(P.cout.wmu + slot, p.wmu);
-#if C2D_TABLE_COMTOT
-    gst(P.cout.phi + slot, p.eta);                   /* encoded azimuth (CensusSoA) */
-#else
-    gst(P.cout.phi + slot, p.phi);
-#endif
-    gst(P.cout.ew + slot, p.ew);
-    gst(P.cout.xnu + slot, p.xnu);
-    gst(P.cout.jk + slot, ((uint32_t)p.jph << 16) | (uint32_t)p.kph);
-    gst(P.cout.bins + slot, (p.bins & 0x00ffffffu)
-#if C2D_TABLE_COMTOT
-                                | (p.esw == -1 ? C2D_CENS_ESW : 0u)
-#endif
-    );
-    gst(P.cout.key + slot, ckey);
-  } else {
-    gor(P.err, ERR_CENSUS);
-  }
-  if (nf)
-    gadd(&P.nf_rep[(int64_t)(blockIdx.x % C2D_NF_REPL) * P.ncell * C2D_NPHFIELD +
-                   (int64_t)cell * C2D_NPHFIELD + (ib - 1)], FDIV_POS(6.25e8 * p.ew, p.xnu));
-  cell_add(P, T, TC_NPCEN, cell, 1.0);
-  cell_add(P, T, TC_ECENS, cell, p.ew);
-#else
   cell_add(P, T, TC_NPCEN, cell, 1.0);
   cell_add(P, T, TC_ECENS, cell, p.ew);
 #ifdef C2D_ABLATE_NFIELD                /* profiling ablation only (tools/build_sweep.sh) */
@@ -935,7 +891,6 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
   } else {
     gor(P.err, ERR_CENSUS);
   }
-#endif
   LC_ADD(lc, C2D_CNT_CENSUS);
 }
 
@@ -1863,10 +1818,10 @@ __device__ __forceinline__ double UB(Bundle& b) {
   return c2d_draw_s(b.p.key, C2D_SUB_BUNDLE | (uint32_t)b.g0, b.bctr++);
 }
 
-/* start (or restart) the bundle at probe g0 of source b.src, its record
- * already loaded into b.p (load_source) */
-__device__ __forceinline__ void bundle_begin_loaded(const KParams& P, const Tal& T, Bundle& b) {
+/* start (or restart) the bundle at probe g0 of source b.src */
+__device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bundle& b) {
   Pkt& p = b.p;
+  load_source(P, p, b.src);
   const double ew0 = p.ew;
   const double s_ew = FDIV_POS(ew0, (double)P.split1);   /* imctrk2d.f:106-123 */
   const int G = min(P.split1 - b.g0, BUNDLE_MAX);
@@ -1891,21 +1846,6 @@ __device__ __forceinline__ void bundle_begin_loaded(const KParams& P, const Tal&
   }
   cache_energy(P, T.g, p);          /* azimuth: set by load_source */
 }
-__device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bundle& b) {
-  load_source(P, b.p, b.src);
-  bundle_begin_loaded(P, T, b);
-}
-
-/* the survivors' absorption points of a shared step (bundle_step computes
- * them; with C2D_EARLY_REFILL the loop runs after the wave's work fetch) */
-struct PtWork {
-  int nabs;            /* survivors that deposit over the whole step (0: none) */
-  int two;             /* the absorption point is sampled (xabs > 1e-5) */
-  int cell;
-  uint32_t sub;        /* C2D_SUB_ABSPT | g0 of the bundle */
-  uint64_t key;        /* the source key (b.p is reloaded before the loop) */
-  double qabs, dabs, sig, rpre, wmu;   /* sig: the step's absorption coefficient */
-};
 
 /* probe g0 + i collides at dcol inside the shared step: its own partial
  * step to the collision point (flight(), ikind = 3), then the record */
@@ -1963,9 +1903,8 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
 }
 
 /* one shared step of the bundle (flight() for every copy on the path) */
-__device__ __forceinline__ void bundle_points(const KParams& P, const Tal& T, Bundle& b, const PtWork& w);
 __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, const GenArgs& A,
-                                            Bundle& b, ComCache& cc, LaneCnt& lc, Prof& pf, PtWork& w) {
+                                            Bundle& b, ComCache& cc, LaneCnt& lc, Prof& pf) {
 #ifdef C2D_HOT_RELOAD
   const KParams& P = cold_always(P1);
 #else
@@ -2174,41 +2113,22 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
   /* ---- the survivors' absorption points and deposits (imctrk2d.f:382-462),
    * at the step's starting point ---- */
   TP_MARK(pf, TP_EVENT);
-  w.nabs = nabs;
-  w.two = two ? 1 : 0;
-  w.cell = cell;
-  w.sub = C2D_SUB_ABSPT | (uint32_t)b.g0;
-  w.key = p.key;
-  w.qabs = qabs;
-  w.dabs = dabs;
-  w.sig = sigabs;
-  w.rpre = rpre;
-  w.wmu = wmu;
-#if !C2D_EARLY_REFILL
-  bundle_points(P, T, b, w);
-  w.nabs = 0;
-#endif
-  TP_MARK(pf, TP_PTS);
-}
-
-__device__ __forceinline__ void bundle_points(const KParams& P, const Tal& T, Bundle& b, const PtWork& w) {
-  const int nabs = w.nabs;
   if (nabs > 0) {
     double sum_prdep = 0.0;
 #ifdef C2D_ABLATE_PROBE_ABS            /* profiling ablation only (tools/build_sweep.sh) */
-    if (w.two && nabs < 0) {
+    if (two && nabs < 0) {
 #else
-    if (w.two) {
+    if (two) {
 #endif
       /* two 32-bit uniforms per output of the bundle's point stream
        * (c2d_abspt), fresh outputs per shared step */
-      const double qabs = w.qabs, dabs = w.dabs, sigabs = w.sig, rpre = w.rpre, wmu = w.wmu;
+      const uint32_t sub = C2D_SUB_ABSPT | (uint32_t)b.g0;
 #if C2D_TABLE_COMTOT
       const double isig = FDIV_POS(1.0, sigabs);
       const double Aw = wmu * rpre, Bw = rpre * rpre;
 #endif
       for (int t = 0; t < nabs; t += 2) {
-        const uint64_t wo = c2d_abspt(w.key, w.sub, b.actr++);
+        const uint64_t wo = c2d_abspt(p.key, sub, b.actr++);
 #pragma unroll
         for (int j = 0; j < 2; j++) {
           if (t + j < nabs) {
@@ -2243,11 +2163,12 @@ __device__ __forceinline__ void bundle_points(const KParams& P, const Tal& T, Bu
         }
       }
     } else {
-      sum_prdep = (double)nabs * (w.dabs * w.wmu * C_LIGHT);
+      sum_prdep = (double)nabs * (dabs * wmu * C_LIGHT);
     }
-    cell_add(P, T, TC_EDEP, w.cell, (double)nabs * w.dabs);
-    cell_add(P, T, TC_PRDEP, w.cell, sum_prdep);
+    cell_add(P, T, TC_EDEP, cell, (double)nabs * dabs);
+    cell_add(P, T, TC_PRDEP, cell, sum_prdep);
   }
+  TP_MARK(pf, TP_PTS);
 }
 
 __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(const KParams* __restrict__ Pg,
@@ -2292,119 +2213,6 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
 #endif
   census_chunk_load(P, tid >> 6, lane);
 
-#ifndef C2D_EARLY_REFILL
-#define C2D_EARLY_REFILL 1
-#endif
-#if C2D_EARLY_REFILL
-  /* The wave's work fetch and the new sources' record loads are issued
-   * between a step's writes and its survivors' point loop, so the loads
-   * arrive during that VALU-only loop instead of stalling the next
-   * iteration's bundle start.  pend: the lane's record is in flight into b.p
-   * (a new source, or a restart of the same one). */
-  bool pend = false;
-  for (;;) {
-    if (pend) {
-      bundle_begin_loaded(P, T, b);
-      busy = true;
-      pend = false;
-    }
-    TP_MARK(pf, TP_START);
-#ifdef C2D_TR_PROF
-    pf.acc[TP_ITER] += 1;
-#endif
-    if (exhausted && __ballot(busy) == 0ull) break;
-    PtWork w;
-    w.nabs = 0;
-    if (busy) {
-#ifdef C2D_TR_PROF
-      pf.acc[TP_LANES] += __popcll(__ballot(1));
-#endif
-      bundle_step(P, T, A, b, cc, lc, pf, w);
-      if (!b.alive && !(b.flags & BF_TRACK)) {
-        if ((b.flags & (BF_TKILL | BF_RERUN)) == BF_TKILL)
-          LC_ADD(lc, (b.flags & BF_TABORT) ? C2D_CNT_ABORTED : C2D_CNT_KILLED);
-        const int G = min(P.split1 - b.g0, BUNDLE_MAX);
-        busy = false;
-        if (b.g0 + G < P.split1) {
-          TP_COUNT(pf, TP_RST_W, TP_RST_L);
-          b.g0 += G;                        /* next bundle of probes */
-          pend = true;
-        } else if ((b.flags & BF_RERUN) && P.split1 - b.nscat > 0) {
-          TP_COUNT(pf, TP_RST_W, TP_RST_L);
-          b.g0 = P.split1;                  /* the recombined copy alone */
-          pend = true;
-        } else {
-          if (cold(P).clist && b.src >= 0) census_item_done(P, b.src);
-        }
-      }
-    }
-    TP_MARK(pf, TP_EVENT);
-    /* ---- refill idle lanes: chunked, wave-aggregated work fetch from the
-     * workgroup's shard of the item range, then from the following ones ---- */
-    bool got = false;
-    long long item = -1;
-    if (!exhausted) {
-      unsigned long long needm = __ballot(!busy && !pend);
-      while (needm != 0ull) {
-        if (chunk_base >= chunk_end) {
-          for (;;) {
-            if (shard_try >= C2D_WORK_SHARDS) { exhausted = true; break; }
-            /* shard bounds on work-chunk (= census-chunk) boundaries */
-            const int s = (shard0 + shard_try) % C2D_WORK_SHARDS;
-            const long long lo = (n_items * s / C2D_WORK_SHARDS) & ~(CHUNK - 1);
-            const long long hi = s + 1 == C2D_WORK_SHARDS
-                                     ? n_items : (n_items * (s + 1) / C2D_WORK_SHARDS) & ~(CHUNK - 1);
-            unsigned long long nb = 0;
-            if (lane == 0)
-              nb = atomicAdd(A.work_sh + (size_t)s * C2D_EV_SHARD_STRIDE, (unsigned long long)CHUNK);
-            nb = rfl64(nb);
-            if (lo + (long long)nb < hi) {
-              chunk_base = lo + (long long)nb;
-              chunk_end = chunk_base + CHUNK < hi ? chunk_base + CHUNK : hi;
-              chunk_slot = chunk_base;
-              if (cold(P).clist && chunk_base < cold(P).n_cens_items) {
-                const int32_t id = __builtin_amdgcn_readfirstlane(gld(cold(P).clist + (chunk_base >> C2D_CCHUNK_LOG)));
-                chunk_slot = (long long)id << C2D_CCHUNK_LOG;
-                if (lane == 0)
-                  census_track(tid >> 6, id,
-                               (uint32_t)(min(chunk_end, (long long)cold(P).n_cens_items) - chunk_base));
-              }
-              break;
-            }
-            shard_try++;
-          }
-          if (exhausted) break;
-        }
-        const long long avail = chunk_end - chunk_base;
-        const unsigned long long lt = (lane == 0) ? 0ull : (needm & ((~0ull) >> (64 - lane)));
-        const long long rank = __popcll(lt);
-        const long long nneed = __popcll(needm);
-        if (((needm >> lane) & 1ull) && rank < avail) {
-          /* the source: its census slot (this work chunk's) or packet-store entry */
-          const long long it = chunk_base + rank;
-          item = it < cold(P).n_cens_items ? chunk_slot + (it & (CHUNK - 1))
-                                           : -(it - cold(P).n_cens_items) - 1;
-          got = true;
-        }
-        chunk_base += (nneed < avail ? nneed : avail);
-        needm = __ballot(!busy && !pend && !got);
-      }
-    }
-    if (got) {
-      TP_COUNT(pf, TP_GOT_W, TP_GOT_L);
-      LC_ADD(lc, C2D_CNT_SOURCES);      /* imctrk2d(-1) entry (imctrk2d.f:91,106-123) */
-      b.src = item;
-      b.g0 = 0;
-      b.nscat = 0;
-      cc.cell0 = -1; cc.cell1 = -1;
-      pend = true;
-    }
-    if (pend) load_source(P, b.p, b.src);
-    TP_MARK(pf, TP_REFILL);
-    bundle_points(P, T, b, w);
-    TP_MARK(pf, TP_PTS);
-  }
-#else
   for (;;) {
     /* ---- refill idle lanes: chunked, wave-aggregated work fetch from the
      * workgroup's shard of the item range, then from the following ones ---- */
@@ -2477,8 +2285,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
 #ifdef C2D_TR_PROF
       pf.acc[TP_LANES] += __popcll(__ballot(1));
 #endif
-      PtWork w;
-      bundle_step(P, T, A, b, cc, lc, pf, w);
+      bundle_step(P, T, A, b, cc, lc, pf);
       TP_MARK(pf, TP_EVENT);
       if (!b.alive && !(b.flags & BF_TRACK)) {
         if ((b.flags & (BF_TKILL | BF_RERUN)) == BF_TKILL)
@@ -2500,7 +2307,6 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
     }
     TP_MARK(pf, TP_POST);
   }
-#endif
 #ifdef C2D_TR_PROF
   pf.acc[TP_NWAVE] = 1;
   if (lane == 0)
