@@ -140,6 +140,7 @@ struct c2d_ctx {
   int64_t cscan_cap = 0;
   uint32_t* ctile_cnt = nullptr;           /* [tiles][2] holes, sources per tile       */
   unsigned long long* ctile_off = nullptr; /* [tiles][2] + totals: exclusive prefixes  */
+  uint8_t* ctile_flag = nullptr;           /* [tiles] the tile holds a chunk tail        */
   int64_t ctile_cap = 0;
   int last_compact_rounds = 0;
   int64_t last_compact_moved = 0;
@@ -444,7 +445,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
                   c->Pnt, c->n_e, c->vfrac, c->ewsv, c->surf_ew, c->surf_tbb, c->tbbl,
                   c->vol_prefix, c->surf_prefix, c->surf_spec, c->spectra, c->comtab, c->comS,
                   c->ev, c->q2[0], c->q2[1], c->q3[0], c->q3[1], c->T_own, c->nf_rep, c->ctl, c->derr, c->dP,
-                  c->cscan, c->ctile_cnt, c->ctile_off, c->cstate, c->clist[0], c->clist[1],
+                  c->cscan, c->ctile_cnt, c->ctile_off, c->ctile_flag, c->cstate, c->clist[0], c->clist[1],
                   c->pool, c->out_list, c->relist, c->cflag, c->part_id, c->part_off, c->tmp_rec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -718,10 +719,17 @@ __device__ __forceinline__ void census_class(const uint32_t* bins, int64_t i, in
 }
 
 __global__ void __launch_bounds__(CT_BLOCK) c2d_census_count(const uint32_t* __restrict__ bins, int64_t R,
-                                                             int64_t W, uint32_t* __restrict__ cnt) {
+                                                             int64_t W, const uint8_t* __restrict__ flag,
+                                                             uint32_t* __restrict__ cnt) {
   __shared__ uint32_t sh[2][CT_BLOCK / 64];
   const int64_t t = blockIdx.x;
   const int64_t base = t * CT_TILE;
+  /* the only dead slots are the chunk tails (c2d_chunk_tails): a tile below
+   * W without one holds neither holes nor sources */
+  if (base + CT_TILE <= W && !flag[t]) {
+    if (threadIdx.x < 2) cnt[2 * t + threadIdx.x] = 0u;
+    return;
+  }
   uint32_t nh = 0, ns = 0;
   for (int j = 0; j < CT_TILE / CT_BLOCK; j++) {
     bool h, s;
@@ -782,6 +790,7 @@ __global__ void __launch_bounds__(CT_BLOCK) c2d_census_emit(const uint32_t* __re
   const uint32_t lane = __lane_id();
   const unsigned long long below = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
   unsigned long long rh = off[2 * t], rs = off[2 * t + 1];
+  if (off[2 * t + 2] == rh && off[2 * t + 3] == rs) return;   /* no hole, no source */
   for (int j = 0; j < CT_TILE / CT_BLOCK; j++) {
     const int64_t i = base + j * CT_BLOCK + threadIdx.x;
     bool h, s;
@@ -889,6 +898,18 @@ __global__ void __launch_bounds__(256) c2d_chunk_tails(const int64_t* __restrict
   const int64_t t1 = base + chunk < cap ? base + chunk : cap;
   for (int64_t s = base + used + threadIdx.x; s < t1; s += blockDim.x) bins[s] = C2D_CENS_DEAD;
   if (threadIdx.x == 0 && t1 > base + used) atomicAdd(dead, (unsigned long long)(t1 - base - used));
+}
+
+/* flag the compaction tiles (CT_TILE slots) that hold a chunk tail */
+__global__ void __launch_bounds__(256) c2d_tail_tiles(const int64_t* __restrict__ cstate, int64_t n_ws,
+                                                      uint32_t chunk, int64_t cap, uint8_t* __restrict__ flag) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_ws;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t base = cstate[2 * i], used = cstate[2 * i + 1];
+    if (base < 0 || used <= 0 || used >= (int64_t)chunk || base >= cap) continue;
+    const int64_t t1 = base + chunk < cap ? base + chunk : cap;
+    for (int64_t t = (base + used) / CT_TILE; t <= (t1 - 1) / CT_TILE; t++) flag[t] = 1;
+  }
 }
 
 /* chunked census after the step: the wave slots' partly filled chunks, in
@@ -1067,18 +1088,29 @@ static int census_compact(c2d_ctx* c, const DevCensus& cb, int64_t R, int64_t W)
   if (ntiles > c->ctile_cap) {
     if (c->ctile_cnt) (void)hipFree(c->ctile_cnt);
     if (c->ctile_off) (void)hipFree(c->ctile_off);
+    if (c->ctile_flag) (void)hipFree(c->ctile_flag);
     c->ctile_cnt = nullptr;
     c->ctile_off = nullptr;
+    c->ctile_flag = nullptr;
     HIPCHK(c, dalloc(&c->ctile_cnt, 2 * (size_t)ntiles));
     HIPCHK(c, dalloc(&c->ctile_off, 2 * (size_t)ntiles + 2));
+    HIPCHK(c, dalloc(&c->ctile_flag, (size_t)ntiles));
     c->ctile_cap = ntiles;
+  }
+  /* tiles that hold a chunk tail (the only dead slots, below or above W) */
+  HIPCHK(c, hipMemsetAsync(c->ctile_flag, 0, (size_t)ntiles, c->stream));
+  if (c->n_ws > 0) {
+    const int tg = (int)std::min<int64_t>((c->n_ws + 255) / 256, (int64_t)c->n_cu * 4);
+    hipLaunchKernelGGL(c2d_tail_tiles, dim3(tg), dim3(256), 0, c->stream, c->cstate, c->n_ws,
+                       c->cens_chunk, c->cens_phys, c->ctile_flag);
+    HIPCHK(c, hipGetLastError());
   }
   const CensusSoA cs = cb.soa();
   int64_t* holes = c->cscan;
   int64_t* srcs = c->cscan + c->cscan_cap;
   for (int round = 0;; round++) {
     hipLaunchKernelGGL(c2d_census_count, dim3((unsigned)ntiles), dim3(CT_BLOCK), 0, c->stream,
-                       cb.bins, R, W, c->ctile_cnt);
+                       cb.bins, R, W, c->ctile_flag, c->ctile_cnt);
     hipLaunchKernelGGL(c2d_census_scan, dim3(1), dim3(1024), 0, c->stream, c->ctile_cnt, ntiles,
                        c->ctile_off);
     hipLaunchKernelGGL(c2d_census_emit, dim3((unsigned)ntiles), dim3(CT_BLOCK), 0, c->stream,
