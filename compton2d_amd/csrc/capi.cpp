@@ -706,7 +706,10 @@ __global__ void __launch_bounds__(256) c2d_nf_reduce(const double* __restrict__ 
  * the k-th source's slot into the two work lists (slot order: the moves are
  * monotone, and no counter is contended), c2d_census_fill moves pair k.  A
  * round moves at most `cap` pairs; rounds repeat while holes remain. */
-constexpr int CT_TILE = 4096, CT_BLOCK = 256;
+#ifndef C2D_CT_TILE
+#define C2D_CT_TILE 16384
+#endif
+constexpr int CT_TILE = C2D_CT_TILE, CT_BLOCK = 256;
 
 __device__ __forceinline__ void census_class(const uint32_t* bins, int64_t i, int64_t R, int64_t W,
                                              bool& hole, bool& src) {

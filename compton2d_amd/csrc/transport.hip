@@ -115,6 +115,9 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 #ifndef C2D_PT_SERIES
 #define C2D_PT_SERIES 1
 #endif
+#ifndef C2D_PT_ADAPT
+#define C2D_PT_ADAPT 1
+#endif
 
 /* Fast build only (the exact build keeps the oracle's c2d_math and IEEE
  * division bit for bit):
@@ -137,6 +140,38 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 #endif
 #ifndef C2D_RSQ_NR
 #define C2D_RSQ_NR 2
+#endif
+/* C2D_FAST_LOG (fast build): log(x) for normal x > 0 by fdlibm's reduction
+ * and polynomial with one of its two final forms for every x (c2d_log_pos
+ * evaluates both and the |f| < 2^-20 form, then selects): < 1 ulp (host
+ * check against logl over (0,1), (0.7,1), e^[-40,40] and 1 +- 5e-7) */
+#ifndef C2D_FAST_LOG
+#define C2D_FAST_LOG 1
+#endif
+#if C2D_TABLE_COMTOT && C2D_FAST_LOG
+__device__ __forceinline__ double log_fast(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+               Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  int32_t hx = c2d_hi(x);
+  int32_t k = (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  const int32_t i = (hx + 0x95f64) & 0x100000;
+  x = c2d_with_hi(x, hx | (i ^ 0x3ff00000));
+  k += (i >> 20);
+  const double f = x - 1.0, dk = (double)k;
+  const double s = C2D_MDIV(f, 2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  const double R = t2 + t1;
+  return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+#define FLOG(x) log_fast(x)
+#else
+#define FLOG(x) c2d_log_pos(x)
 #endif
 #if C2D_TABLE_COMTOT && C2D_FAST_EXP == 1
 #define FEXP(x) exp(x)
@@ -932,7 +967,7 @@ __device__ __forceinline__ void load_rec(Pkt& p, const ScatRec& r) {
 __device__ __forceinline__ void cache_energy(const KParams& P, const Geo* g, Pkt& p) {
   p.ie = grid_lookup(g->E_ph, C2D_N_VOL, g->eph_start, g->eph_k0, p.xnu);
 #if C2D_TABLE_COMTOT
-  const double s = (c2d_log_pos(p.xnu) - C2D_COMTAB_U0) * P.comtab_du_inv;   /* = c2d_log, branch-free */
+  const double s = (FLOG(p.xnu) - C2D_COMTAB_U0) * P.comtab_du_inv;
   if (s >= 1.0 && s < (double)(C2D_COMTAB_N - 3)) {
     p.tg = (int32_t)s;
     p.tt = s - (double)p.tg;
@@ -1833,7 +1868,7 @@ __device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bun
   b.flags = 0;
   b.tsteps = 0;
   b.tau = 0.0;
-  if (G > 0) b.tau = FDIV_POS(-c2d_log_pos(UB(b)), (double)G);
+  if (G > 0) b.tau = FDIV_POS(-FLOG(UB(b)), (double)G);
   p.nflight = 0;
   p.mode = 0;
   if (b.g0 + G == P.split1 && P.split1 - b.nscat > 0) {
@@ -1870,7 +1905,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
   } else {
     /* one draw: mr < 1 <= ew / deleabs always holds (ew >= 1e-40) */
     const double mr = UB(b);
-    const double sstar = FDIV_POS(-c2d_log_pos(1.0 - FDIV_POS(mr * deleabs, b.ewp)), sigabs);
+    const double sstar = FDIV_POS(-FLOG(1.0 - FDIV_POS(mr * deleabs, b.ewp)), sigabs);
     const double denom = FSQRT(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
     wmustar = FDIV_POS(wmu * rpre + sstar, denom);
   }
@@ -2022,7 +2057,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
       probe_collide(P, T, A, b, i, dcol, sigabs, Eta, swmu, eta_switch, cell, lc);
       dpos = dcol;
       if (n == 0) break;
-      b.tau = FDIV_POS(-c2d_log_pos(UB(b)), (double)n);
+      b.tau = FDIV_POS(-FLOG(UB(b)), (double)n);
     }
     if (n > 0) {
       b.tau = b.tau - sigsc * (trld - dpos);
@@ -2127,41 +2162,57 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
       const double isig = FDIV_POS(1.0, sigabs);
       const double Aw = wmu * rpre, Bw = rpre * rpre;
 #endif
+#if C2D_TABLE_COMTOT
+      /* -log(1-x) for x = u * qabs: the series below 1e-2 (8 terms, truncation
+       * < x^8/9 relative; 1e-4 with 4 terms -3 %, 0.05 with 12 terms or
+       * 2 atanh(x/(2-x)) below 0.2: no better, r02ap-aq), else the log; a
+       * wave whose every lane has qabs < 1e-4 runs 4 terms (C2D_PT_ADAPT) */
+#define C2D_PT_LOOP(LEXPR)                                                               \
+      for (int t = 0; t < nabs; t += 2) {                                                \
+        const uint64_t wo = c2d_abspt(p.key, sub, b.actr++);                             \
+        _Pragma("unroll") for (int j = 0; j < 2; j++) {                                  \
+          if (t + j < nabs) {                                                            \
+            const double x = c2d_u01_32(j == 0 ? (uint32_t)(wo >> 32) : (uint32_t)wo) * qabs; \
+            const double L = (LEXPR);                                                    \
+            const double sstar = L * isig;                                               \
+            /* 1/sqrt(d) from v_rsq_f64 and two Newton steps (f64 accurate) */           \
+            const double d = Bw + sstar * (2.0 * Aw + sstar);                            \
+            const double h = 0.5 * d;                                                    \
+            double y = __builtin_amdgcn_rsq(d);                                          \
+            _Pragma("unroll") for (int nr = 0; nr < C2D_RSQ_NR; nr++)                    \
+              y = y * __builtin_fma(-h, y * y, 1.5);                                     \
+            sum_prdep += dabs * ((Aw + sstar) * y) * C_LIGHT;                            \
+          }                                                                              \
+        }                                                                                \
+      }
+#if C2D_PT_SERIES
+      if (C2D_PT_ADAPT && __ballot(qabs >= 1.0e-4) == 0ull) {
+        C2D_PT_LOOP(x * (1.0 + x * (0.5 + x * (0.33333333333333333 + x * 0.25))));
+      } else {
+        C2D_PT_LOOP((x < 1.0e-2)
+            ? x * C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x,
+                  C2D_MADD(x, 0.125, 0.14285714285714286), 0.16666666666666667), 0.2), 0.25),
+                  0.33333333333333333), 0.5), 1.0)
+            : -FLOG(1.0 - x));
+      }
+#else
+      C2D_PT_LOOP(-FLOG(1.0 - x));
+#endif
+#undef C2D_PT_LOOP
+#else
       for (int t = 0; t < nabs; t += 2) {
         const uint64_t wo = c2d_abspt(p.key, sub, b.actr++);
 #pragma unroll
         for (int j = 0; j < 2; j++) {
           if (t + j < nabs) {
             const double x = c2d_u01_32(j == 0 ? (uint32_t)(wo >> 32) : (uint32_t)wo) * qabs;
-#if C2D_TABLE_COMTOT
-#if C2D_PT_SERIES
-            /* -log(1-x): series below 1e-2 (8 terms, truncation < x^8/9 relative;
-             * 1e-4 with 4 terms -3 %, 0.05 with 12 terms or 2 atanh(x/(2-x))
-             * below 0.2: no better, r02ap-aq) */
-            const double L = (x < 1.0e-2)
-                ? x * C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x,
-                      C2D_MADD(x, 0.125, 0.14285714285714286), 0.16666666666666667), 0.2), 0.25),
-                      0.33333333333333333), 0.5), 1.0)
-                : -c2d_log_pos(1.0 - x);
-#else
-            const double L = -c2d_log_pos(1.0 - x);
-#endif
-            const double sstar = L * isig;
-            /* 1/sqrt(d) from v_rsq_f64 and two Newton steps (f64 accurate) */
-            const double d = Bw + sstar * (2.0 * Aw + sstar);
-            const double h = 0.5 * d;
-            double y = __builtin_amdgcn_rsq(d);
-#pragma unroll
-            for (int nr = 0; nr < C2D_RSQ_NR; nr++) y = y * __builtin_fma(-h, y * y, 1.5);
-            sum_prdep += dabs * ((Aw + sstar) * y) * C_LIGHT;
-#else
             const double sstar = -c2d_log_pos(1.0 - x) / sigabs;
             const double denom = FSQRT(rpre * rpre + 2.0 * wmu * rpre * sstar + sstar * sstar);
             sum_prdep += dabs * ((wmu * rpre + sstar) / denom) * C_LIGHT;
-#endif
           }
         }
       }
+#endif
     } else {
       sum_prdep = (double)nabs * (dabs * wmu * C_LIGHT);
     }
