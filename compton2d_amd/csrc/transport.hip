@@ -115,9 +115,6 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 #ifndef C2D_PT_SERIES
 #define C2D_PT_SERIES 1
 #endif
-#ifndef C2D_PT_ADAPT
-#define C2D_PT_ADAPT 1
-#endif
 
 /* Fast build only (the exact build keeps the oracle's c2d_math and IEEE
  * division bit for bit):
@@ -2165,8 +2162,8 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
 #if C2D_TABLE_COMTOT
       /* -log(1-x) for x = u * qabs: the series below 1e-2 (8 terms, truncation
        * < x^8/9 relative; 1e-4 with 4 terms -3 %, 0.05 with 12 terms or
-       * 2 atanh(x/(2-x)) below 0.2: no better, r02ap-aq), else the log; a
-       * wave whose every lane has qabs < 1e-4 runs 4 terms (C2D_PT_ADAPT) */
+       * 2 atanh(x/(2-x)) below 0.2: no better, r02ap-aq; 4 terms in waves
+       * whose every qabs < 1e-4: +-0, r03u), else the log */
 #define C2D_PT_LOOP(LEXPR)                                                               \
       for (int t = 0; t < nabs; t += 2) {                                                \
         const uint64_t wo = c2d_abspt(p.key, sub, b.actr++);                             \
@@ -2186,15 +2183,11 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
         }                                                                                \
       }
 #if C2D_PT_SERIES
-      if (C2D_PT_ADAPT && __ballot(qabs >= 1.0e-4) == 0ull) {
-        C2D_PT_LOOP(x * (1.0 + x * (0.5 + x * (0.33333333333333333 + x * 0.25))));
-      } else {
-        C2D_PT_LOOP((x < 1.0e-2)
-            ? x * C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x,
-                  C2D_MADD(x, 0.125, 0.14285714285714286), 0.16666666666666667), 0.2), 0.25),
-                  0.33333333333333333), 0.5), 1.0)
-            : -FLOG(1.0 - x));
-      }
+      C2D_PT_LOOP((x < 1.0e-2)
+          ? x * C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x, C2D_MADD(x,
+                C2D_MADD(x, 0.125, 0.14285714285714286), 0.16666666666666667), 0.2), 0.25),
+                0.33333333333333333), 0.5), 1.0)
+          : -FLOG(1.0 - x));
 #else
       C2D_PT_LOOP(-FLOG(1.0 - x));
 #endif
