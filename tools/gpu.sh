@@ -99,9 +99,9 @@ for r in "$@"; do
       C2D_LIBRARY=$PWD/compton2d_amd/sweep/prof/libcompton2d.so run 300 trprof python tools/tr_prof.py --steps ${STEPS}
       tail -2 "$O/trprof.out" ;;
     n2)
-      run 300 n2_w1 python -u bench.py --sources 40000000 --steps 3 --warmup 2 --no-cpu-baseline
+      run 300 n2_w1 python -u bench.py --workload c3 --sources 40000000 --steps 3 --warmup 2 --no-cpu-baseline
       C2D_ONE_GPU=1 C2D_DIST_BACKEND=gloo run 300 n2_w2 python -u -m torch.distributed.run --nnodes=1 \
-          --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 \
+          --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --workload c3 \
           --sources 20000000 --steps 3 --warmup 2 --no-cpu-baseline
       line "$O/n2_w1.out"; line "$O/n2_w2.out" ;;
     *) echo "unknown recipe $r"; exit 2 ;;
