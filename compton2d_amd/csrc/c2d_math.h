@@ -198,6 +198,51 @@ C2D_HD double c2d_exp(double x) {
   return y * twom1000;
 }
 
+/* c2d_exp without branches, bit for bit equal to it for every x (NaN and
+ * infinities included): fdlibm's reduction with its own choice of k (0, +-1
+ * or the rounded x/ln2), both final forms evaluated from one division
+ * ((x c)/(c - 2) = -((x c)/(2 - c)) exactly), and the |x| < 2^-28, subnormal
+ * and overflow/underflow results selected.  A wavefront whose lanes hold
+ * arguments of different ranges runs one path instead of several. */
+C2D_HD double c2d_exp_bf(double x) {
+  const double o_threshold = 7.09782712893383973096e+02,
+               u_threshold = -7.45133219101941108420e+02,
+               ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10,
+               invln2 = 1.44269504088896338700e+00, huge = 1.0e+300,
+               twom1000 = 9.33263618503218878990e-302,
+               P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+               P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+               P5 = 4.13813679705723846039e-08;
+  const int32_t hx0 = c2d_hi(x);
+  const int32_t xsb = (hx0 >> 31) & 1;
+  const int32_t hx = hx0 & 0x7fffffff;
+  /* the reduction on a clamped copy (the results of |x| > 800 and NaN are
+   * replaced below; the clamp keeps the int conversion in range) */
+  const double xr = (x > 800.0) ? 800.0 : ((x < -800.0) ? -800.0 : ((x == x) ? x : 0.0));
+  const int32_t kg = (int32_t)(invln2 * xr + (xsb ? -0.5 : 0.5));
+  const int32_t k = (hx > 0x3fd62e42) ? ((hx < 0x3FF0A2B2) ? (1 - xsb - xsb) : kg) : 0;
+  const double t = (double)k;
+  const double hi = xr - t * ln2HI, lo = t * ln2LO;
+  const double xx = hi - lo;
+  const double tt = xx * xx;
+  const double c = xx - tt * (P1 + tt * (P2 + tt * (P3 + tt * (P4 + tt * P5))));
+  const double q = (xx * c) / (2.0 - c);
+  const double y = (k == 0) ? 1.0 - ((-q) - xx) : 1.0 - ((lo - q) - hi);
+  const double yn = c2d_with_hi(y, (int32_t)((uint32_t)c2d_hi(y) + ((uint32_t)k << 20)));
+  const double ys = c2d_with_hi(y, (int32_t)((uint32_t)c2d_hi(y) + ((uint32_t)(k + 1000) << 20))) * twom1000;
+  double r = (k >= -1021) ? yn : ys;
+  r = (hx < 0x3e300000) ? 1.0 + x : r;
+  if (hx >= 0x40862E42) {                    /* |x| >= 709.78... (rare: a wave-uniform-ish branch) */
+    if (hx >= 0x7ff00000)
+      r = (((hx & 0xfffff) | c2d_lo(x)) != 0) ? x + x : ((xsb == 0) ? x : 0.0);
+    else if (x > o_threshold)
+      r = huge * huge;
+    else if (x < u_threshold)
+      r = twom1000 * twom1000;
+  }
+  return r;
+}
+
 /* kernels on [-pi/4, pi/4] (FreeBSD k_cos.c, k_sin.c) */
 C2D_HD double c2d_kcos(double x, double y) {
   const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,

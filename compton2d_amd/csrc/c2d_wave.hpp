@@ -155,7 +155,7 @@ __device__ __forceinline__ McdTerm mcd_term_tab(double z, int n, const double* _
   const double y = z * ts;
   double sd2 = 0.0, sd3 = 0.0;
   if (y < 2.25e2) {
-    const double ey = c2d_exp(y);
+    const double ey = c2d_exp_bf(y);
     sd2 = p2 / ey;
     sd3 = p3 / ey;
   }
@@ -236,7 +236,7 @@ __device__ inline void mcdonald23_from(double z, int lane, const double* __restr
     const double y = z * ts;
     double sd2 = 0.0, sd3 = 0.0;
     if (y < 2.25e2) {
-      const double ey = c2d_exp(y);
+      const double ey = c2d_exp_bf(y);
       sd2 = p2 / ey;
       sd3 = p3 / ey;
     }
@@ -273,8 +273,17 @@ __device__ inline void mcdonald23_from(double z, int lane, const double* __restr
 /* McDonald's normalisation (volume2d.f:623-624) of the two sums */
 __device__ __forceinline__ void mcdonald23_finish(double z, double sum2, double sum3, double& K2,
                                                   double& K3) {
-  K2 = __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, 2.0) * sum2 / c2d_exp(gammln(5.0e-1 + 2.0));
-  K3 = __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, 3.0) * sum3 / c2d_exp(gammln(5.0e-1 + 3.0));
+  K2 = __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, 2.0) * sum2 / c2d_exp_bf(gammln(5.0e-1 + 2.0));
+  K3 = __builtin_sqrt(3.14159265) * c2d_pow(5.0e-1 * z, 3.0) * sum3 / c2d_exp_bf(gammln(5.0e-1 + 3.0));
+}
+/* ... with the argument-free factors exp(gammln(2.5)), exp(gammln(3.5))
+ * given (the same values, computed once per launch) and c2d_pow's log of
+ * 0.5 z shared by both powers (c2d_pow(x, y) = c2d_exp_bf(y * c2d_log(x))) */
+__device__ __forceinline__ void mcdonald23_finish_c(double z, double sum2, double sum3, double eg2,
+                                                    double eg3, double& K2, double& K3) {
+  const double lz = c2d_log(5.0e-1 * z);
+  K2 = __builtin_sqrt(3.14159265) * c2d_exp_bf(2.0 * lz) * sum2 / eg2;
+  K3 = __builtin_sqrt(3.14159265) * c2d_exp_bf(3.0 * lz) * sum3 / eg3;
 }
 
 __device__ inline void mcdonald23_w(double z, int lane, const double* __restrict__ tab, double& K2,

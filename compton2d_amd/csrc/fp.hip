@@ -145,6 +145,10 @@ struct McdBatch {
   double bc[N], bg[N];
 };
 
+/* exp(gammln(2.5)), exp(gammln(3.5)) of McDonald's normalisation, computed
+ * once per launch (c2d_fp_kernel) instead of per series */
+__shared__ double s_eg[2];
+
 /* gamma_bar (volume2d.f:572-594) of this lane's Theta, McDonald's series
  * summed sequentially by the lane (volume2d.f:598-626): n is wave-uniform, so
  * the abscissa table reads are scalar loads; two terms per iteration give the
@@ -183,12 +187,12 @@ __device__ double gamma_bar_lane(double Theta, const double* __restrict__ tab, l
       const double ya = z * tsa, yb = z * tsb;
       double sd2a = 0.0, sd3a = 0.0, sd2b = 0.0, sd3b = 0.0;
       if (ya < 2.25e2) {
-        const double ey = c2d_exp(ya);
+        const double ey = c2d_exp_bf(ya);
         sd2a = p2a / ey;
         sd3a = p3a / ey;
       }
       if (yb < 2.25e2) {
-        const double ey = c2d_exp(yb);
+        const double ey = c2d_exp_bf(yb);
         sd2b = p2b / ey;
         sd3b = p3b / ey;
       }
@@ -219,7 +223,7 @@ __device__ double gamma_bar_lane(double Theta, const double* __restrict__ tab, l
       const double y = z * ts;
       double sd2 = 0.0, sd3 = 0.0;
       if (y < 2.25e2) {
-        const double ey = c2d_exp(y);
+        const double ey = c2d_exp_bf(y);
         sd2 = p2 / ey;
         sd3 = p3 / ey;
       }
@@ -236,7 +240,7 @@ __device__ double gamma_bar_lane(double Theta, const double* __restrict__ tab, l
       if (++guard > GUARD_MAX) break;
     }
     double K2, K3;
-    mcdonald23_finish(z, sum2, sum3, K2, K3);
+    mcdonald23_finish_c(z, sum2, sum3, s_eg[0], s_eg[1], K2, K3);
     g = K3 / K2 - Theta;
   }
   if (g < 1.0) g = 1.0;
@@ -421,7 +425,7 @@ __device__ __forceinline__ void mcdonald23_coop(McdCoop& C, double z, int lane, 
     const int n0 = npass * pass;
     mcdonald23_from(z, lane, tab, n0, tab[(size_t)n0 * 4], sum2, sum3, run2, run3, guard, scr);
   }
-  mcdonald23_finish(z, sum2, sum3, K2, K3);
+  mcdonald23_finish_c(z, sum2, sum3, s_eg[0], s_eg[1], K2, K3);
 }
 
 /* wave 0: evaluate chain members 1..NB from th0 on every wave of the zone */
@@ -455,8 +459,12 @@ __device__ __forceinline__ double gamma_bar_coop(McdCoop& C, double Theta, int l
     double K2, K3;
     if (fp_nwaves<WMAX>() > 1)
       mcdonald23_coop<WMAX>(C, 1.0 / Theta, lane, tab, K2, K3, guard, scr);
-    else
-      mcdonald23_w(1.0 / Theta, lane, tab, K2, K3, guard, scr);
+    else {
+      const double z = 1.0 / Theta;
+      double sum2 = 0.0, sum3 = 0.0;
+      mcdonald23_from(z, lane, tab, 0, 1.0, sum2, sum3, true, true, guard, scr);
+      mcdonald23_finish_c(z, sum2, sum3, s_eg[0], s_eg[1], K2, K3);
+    }
     g = K3 / K2 - Theta;
   }
   if (g < 1.0) g = 1.0;
@@ -559,7 +567,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
     const double az = (zmid - P.z_flare) / P.sigma_z;
     const double at = (P.time - P.t_flare) / P.sigma_t;
     const double y = 5.0e-1 * (ar * ar + az * az + at * at);
-    tl_flare = (y < 1.0e2) ? P.flare_amp / c2d_exp(y) : 0.0;
+    tl_flare = (y < 1.0e2) ? P.flare_amp / c2d_exp_bf(y) : 0.0;
   }
   const double tlev = zin[FZ_TURB] + tl_flare;
   const double Tp_flare = tna * (1.0 + tl_flare);
@@ -654,7 +662,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
                        (c2d_pow(sT, 1.5) * (1.0 + 1.875 * Th_e + .8203 * (Th_e * Th_e)));
     const double hr_th_Coul = f_th * 1.7386e-26 * n_p * LNL * h_T * (Tp_flare - Te_new);
     const double yR = gamma_R / g_av;
-    const double hr_th_sy = (yR < 100.0) ? -Eloss_sy / (P.dt * c2d_exp(yR)) : 0.0;
+    const double hr_th_sy = (yR < 100.0) ? -Eloss_sy / (P.dt * c2d_exp_bf(yR)) : 0.0;
     double hr_th_A = tlev * hr_th_Coul;
     if (hr_th_A < 1.0e-20) hr_th_A = 1.0e-20;
     const double hr_th_total = hr_th_sy + hr_th_c + hr_th_A;
@@ -667,7 +675,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
     for (int i = lane + 1; i <= NT; i += FPB) {
       const double gi = s_gam[i];
       const double y = gamma_R / gi;
-      const double dg_sy = (y < 100.0) ? -(f_sy * (gi * gi - 1.0) / c2d_exp(y)) : -1.0e-50;
+      const double dg_sy = (y < 100.0) ? -(f_sy * (gi * gi - 1.0) / c2d_exp_bf(y)) : -1.0e-50;
       const double dg_A = gi / t_acc;
       s_disp[i] = gi * gi / t_acc / 2.0;
       s_dgdt[i] = dg_sy + s_dgic[i] + dg_A;
@@ -725,7 +733,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
     if (P.pick_sw == 1) {
       for (int i = lane + 1; i <= NT - 1; i += FPB) {
         const double x = s_gam[i] - P.inj_gg;
-        s_inj[i] = 1.0e2 * c2d_exp(-((x * x) / 2.0 / (P.inj_sigma * P.inj_sigma))) /
+        s_inj[i] = 1.0e2 * c2d_exp_bf(-((x * x) / 2.0 / (P.inj_sigma * P.inj_sigma))) /
                    (P.inj_sigma * __builtin_sqrt(2.0 * PI_REF));
       }
       fp_sync<WMAX>();
@@ -754,14 +762,14 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
           double v;
           if (P.inj_dis == 1) {
             const double x = gi - P.inj_gg;
-            v = 1.0e2 * c2d_exp(-((x * x) / 2.0 / (P.inj_sigma * P.inj_sigma))) /
+            v = 1.0e2 * c2d_exp_bf(-((x * x) / 2.0 / (P.inj_sigma * P.inj_sigma))) /
                 (P.inj_sigma * __builtin_sqrt(2.0 * PI_REF));
           } else {
             const double inj_g2var =
                 P.inj_g2 * c2d_pow(10.0, (P.time + t_fp - P.inj_t) * P.inj_v / zmax);
             if (gi > P.inj_g1) {
               const double inj_y = (P.g2var_switch == 1) ? gi / inj_g2var : gi / P.inj_g2;
-              v = (inj_y < 1.0e2) ? 1.0e2 / (c2d_pow(gi, P.inj_p) * c2d_exp(inj_y)) : 0.0;
+              v = (inj_y < 1.0e2) ? 1.0e2 / (c2d_pow(gi, P.inj_p) * c2d_exp_bf(inj_y)) : 0.0;
             } else {
               v = 0.0;
             }
@@ -808,8 +816,8 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
       const double bigC = (s_disp[i] + s_disp[i + 1]) / 2.0;
       const double smw = Dg * bigB / bigC;
       s_smw[i] = smw;
-      s_bigW[i] = smw / (c2d_exp(smw) - 1.0);
-      s_em[i] = bigC * smw / (1.0 - c2d_exp(-smw));   /* bigC*smw/(1-exp(-smw)) */
+      s_bigW[i] = smw / (c2d_exp_bf(smw) - 1.0);
+      s_em[i] = bigC * smw / (1.0 - c2d_exp_bf(-smw));   /* bigC*smw/(1-exp(-smw)) */
       s_bigC[i] = bigC;
     }
     fp_sync<WMAX>();
@@ -1017,7 +1025,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
         const int q = c0 + lane;
         double v1 = 0.0, v2 = 0.0;
         if (q < i_end) {
-          const double f_pl = N_nt / (c2d_pow(s_gam[q], p_nth) * c2d_exp(s_gam[q] / gmax));
+          const double f_pl = N_nt / (c2d_pow(s_gam[q], p_nth) * c2d_exp_bf(s_gam[q] / gmax));
           v1 = f_pl * s_gam[q] * (s_gnt[q + 1] - s_gnt[q]);
           v2 = f_pl * (s_gnt[q + 1] - s_gnt[q]);
         }
@@ -1072,6 +1080,11 @@ template <int WMAX>
 __global__ void __launch_bounds__(WMAX * FPB) c2d_fp_kernel(const FpParams P) {
   /* wave-uniform by construction (readfirstlane): a scalar branch, so no
    * wave ever steps through the other role's barriers with EXEC = 0 */
+  if (threadIdx.x == 0) {
+    s_eg[0] = c2d_exp_bf(gammln(5.0e-1 + 2.0));
+    s_eg[1] = c2d_exp_bf(gammln(5.0e-1 + 3.0));
+  }
+  __syncthreads();
   if (WMAX > 1) {
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x) / FPB;
     if (wave != 0) {

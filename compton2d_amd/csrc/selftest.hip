@@ -27,6 +27,7 @@ __global__ void c2d_selftest_math_kernel(int fn, const double* x, double* y, int
     case 5: r = __builtin_sqrt(v); break;
     case 6: r = v / 3.0; break;
     case 8: r = c2d_log_pos(v); break;
+    case 9: r = c2d_exp_bf(v); break;
     default: r = c2d_draw((uint64_t)(int64_t)v, (uint32_t)i); break;
   }
   y[i] = r;

@@ -46,7 +46,7 @@ __device__ __forceinline__ double expk13(double t) {
     z3 = z3 * z3;
     const double f1 = 1.0 + z3 / 6.0 * (1.0 + z3 / 30.0 * (1.0 + z3 / 56.0));
     const double f2 = z * (1.0 + z3 / 12.0 * (1.0 + z3 / 42.0 * (1.0 + z3 / 90.0)));
-    return c2d_exp(t) * PI_REF * 1.7320508 / zs * (c1 * f1 - c2 * f2);
+    return c2d_exp_bf(t) * PI_REF * 1.7320508 / zs * (c1 * f1 - c2 * f2);
   }
   const double z = 1.0 / (72.0 * t);
   const double poly = 1.0 - 5.0 * z * (1.0 - 38.5 * z);
@@ -108,7 +108,7 @@ __global__ void __launch_bounds__(VEM_BLOCK) c2d_vem_kernel(const VemParams P) {
     if (Theta < 2.0e-1)                                 /* volume2d.f:56-65 */
       K2 = 1.2533 * __builtin_sqrt(Theta) *
            (1. + 1.875 * Theta + 8.2031e-1 * (Theta * Theta) - 2.03e-1 * (Theta * Theta * Theta)) /
-           c2d_exp(Theta);
+           c2d_exp_bf(Theta);
     else
       K2 = K2m;
     double g_av;                                        /* gamma_bar (volume2d.f:572-594) */
@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(VEM_BLOCK) c2d_vem_kernel(const VemParams P) {
     if (g_av < 1.0) g_av = 1.0;
     const double gamma_R = 2.1e-3 * __builtin_sqrt(ne) / (B * __builtin_sqrt(g_av));
     const double y = gamma_R / g_av;
-    const double f_rz = (y < 1.0e2) ? c2d_exp(-y) : 0.;
+    const double f_rz = (y < 1.0e2) ? c2d_exp_bf(-y) : 0.;
     /* Eloss_sy's sum (imcgen2d.f:169-172), in order */
     const double s1 = seq_sum(0.0, 0, NT - 2, lane, [&](int i) {
       const double g1 = s_gnt[i] + 1.0;
@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(VEM_BLOCK) c2d_vem_kernel(const VemParams P) {
         if (tt < 1.0e4) {
           const double eq43 = expk43(tt), eq13 = expk13(tt);
           const double ff = tt * tt * (eq43 * eq13 - F32(0.6) * tt * (eq43 - eq13) * (eq43 + eq13));
-          es = face * ff * c2d_exp(-2.0 * tt);
+          es = face * ff * c2d_exp_bf(-2.0 * tt);
         }
         const double sd = s_f[i2] * es;
         const double sd_k = s_gamp[i2] * es;
@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(VEM_BLOCK) c2d_vem_kernel(const VemParams P) {
         const double q = (E - E_m) / D_m;
         const double x = q * q;
         if (x < 50.) {
-          const double f_cy = f_rz * c2d_exp(-x) * ne * (B * B) * c2d_pow(Theta, mm - 1.5) *
+          const double f_cy = f_rz * c2d_exp_bf(-x) * ne * (B * B) * c2d_pow(Theta, mm - 1.5) *
                               (mm + 1.0) * f_m * c2d_pow(mm, 2.0 * mm + 1.0);
           j_cy = j_cy + 8.46e-14 * f_cy * (E * E) / (E_m * E_m * E_m);
         }
@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(VEM_BLOCK) c2d_vem_kernel(const VemParams P) {
         const double y = 4.5 * v;
         if (y < 1.0e6)
           j_cy = j_cy + 4.652e-12 * ne * nu /
-                            (K2 * c2d_pow(v, 1.6666667e-1) * c2d_exp(c2d_pow(y, 3.33333e-1)));
+                            (K2 * c2d_pow(v, 1.6666667e-1) * c2d_exp_bf(c2d_pow(y, 3.33333e-1)));
       }
     }
     P.kappa[(int64_t)cell * NV + i] = kappa_sy;           /* :347 */
@@ -208,8 +208,8 @@ __global__ void __launch_bounds__(VEM_BLOCK) c2d_vem_kernel(const VemParams P) {
     } else {
       const double x = E / tea;
       const double tau_tot = kappa_sy * lm;
-      double j_th = (x < 1.0e2) ? 1.47e-47 * (nu * nu * nu) / (c2d_exp(x) - 1.0) : 1.0e-50;
-      if (tau_tot < 5.0e1) j_th = j_th * (1.0 - c2d_exp(-tau_tot));
+      double j_th = (x < 1.0e2) ? 1.47e-47 * (nu * nu * nu) / (c2d_exp_bf(x) - 1.0) : 1.0e-50;
+      if (tau_tot < 5.0e1) j_th = j_th * (1.0 - c2d_exp_bf(-tau_tot));
       cT = j_th * E * (dE - 1.0);
     }
     s_cP[i] = cP; s_cC[i] = cC; s_cT[i] = cT;

@@ -1728,8 +1728,10 @@ void c2o_unit_math(int fn, const double* x, double* y, int64_t n) {
       case 3: y[i] = ACOS(x[i]); break;
 #ifdef C2O_DETMATH
       case 5: y[i] = c2d_log_pos(x[i]); break;   /* the GPU's branch-free log */
+      case 6: y[i] = c2d_exp_bf(x[i]); break;    /* the GPU's branch-free exp */
 #else
       case 5: y[i] = LOG(x[i]); break;
+      case 6: y[i] = EXP(x[i]); break;
 #endif
       default: y[i] = POW(x[i], 1.0 / 3.0); break;
     }

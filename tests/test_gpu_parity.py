@@ -182,6 +182,15 @@ def test_device_branch_free_log_equals_host():
     np.testing.assert_array_equal(yd.view(np.uint64), y.view(np.uint64))
 
 
+def test_device_branch_free_exp_equals_host():
+    from test_math_rng import exp_inputs
+    x = exp_inputs()
+    y = np.zeros_like(x)
+    OL.load("det").c2o_unit_math(1, x.ctypes.data_as(abi.PD), y.ctypes.data_as(abi.PD), x.size)
+    yd = device_math(9, x)
+    np.testing.assert_array_equal(yd.view(np.uint64), y.view(np.uint64))
+
+
 def test_device_draws_equal_host():
     """Lineage draws (c2d_rng.h c2d_draw): device = host bit for bit."""
     keys = np.array([0, 1, 0x5EEDC2D, 2 ** 53 - 1], np.float64)

@@ -65,6 +65,30 @@ def test_branch_free_log_bitwise_equals_log():
     np.testing.assert_array_equal(y5.view(np.uint64), y0.view(np.uint64))
 
 
+def exp_inputs():
+    rng = np.random.default_rng(6)
+    parts = [rng.uniform(-750.0, 750.0, 200000), rng.uniform(-1.5, 1.5, 100000),
+             rng.uniform(-1e-7, 1e-7, 50000), rng.uniform(-746.0, -700.0, 50000),
+             rng.uniform(700.0, 710.0, 50000),
+             np.ldexp(rng.uniform(-0.5, 0.5, 50000), rng.integers(-60, 20, 50000)),
+             np.array([0.0, -0.0, 3.7252902984e-09, -3.7252902984e-09, 0.34657359027997264,
+                       -0.3465735902799727, 1.0397207708399179, -1.0397207708399179,
+                       709.782712893384, 709.79, -745.1332191019411, -745.2, 1000.0, -1000.0,
+                       np.inf, -np.inf, np.nan, 5e-324, -5e-324])]
+    return np.concatenate(parts)
+
+
+def test_branch_free_exp_bitwise_equals_exp():
+    """c2d_exp_bf (the FP and table kernels' exp, no branches) == c2d_exp bit
+    for bit, NaN/inf/overflow/subnormal results included."""
+    x = exp_inputs()
+    y1, y6 = np.zeros_like(x), np.zeros_like(x)
+    lib = OL.load("det")
+    lib.c2o_unit_math(1, x.ctypes.data_as(abi.PD), y1.ctypes.data_as(abi.PD), x.size)
+    lib.c2o_unit_math(6, x.ctypes.data_as(abi.PD), y6.ctypes.data_as(abi.PD), x.size)
+    np.testing.assert_array_equal(y6.view(np.uint64), y1.view(np.uint64))
+
+
 def test_rng_known_answers():
     lib = OL.load("det")
     # Random123 kat_vectors, philox4x32-10: (ctr, key) -> out
