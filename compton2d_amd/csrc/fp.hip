@@ -590,7 +590,7 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
   /* gamma_bar is a pure function and label 200 evaluates it at the Th_e the
    * previous sub-step's temperature search ended on, whose value that search
    * computed last: reuse it (one McDonald pair per sub-step saved, exact) */
-  double g_av_next = 0.0;
+  double g_av_next = 0.0, hr_th_c_next = 0.0;
   /* The temperature search steps Theta by x1.005 or /1.005 from the last
    * sub-step's value, so successive sub-steps keep re-evaluating the same few
    * arguments (T oscillating across the crossing). gamma_bar is a pure
@@ -649,9 +649,13 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
     /* label 200 (:577) */
     double g_av = (fp_steps == 0) ? gamma_bar_m(Th_e) : g_av_next;
     /* hr_th_c = hr_th_c - x_i, i.e. + (-x_i) bit for bit */
-    const double hr_th_c = seq_sum_lds(0.0, 1, NT - 1, lane, s_seq, [&](int i) {
-      return -(8.176e-7 * s_dgic[i] * s_fold[i] * (s_gnt[i + 1] - s_gnt[i]) * volume * n_lept);
-    });
+    /* after the first sub-step this sum was formed beside the previous
+     * sub-step's gbar (same f_old, n_lept and order: the same value) */
+    const double hr_th_c = (fp_steps == 0)
+        ? seq_sum_lds(0.0, 1, NT - 1, lane, s_seq, [&](int i) {
+            return -(8.176e-7 * s_dgic[i] * s_fold[i] * (s_gnt[i + 1] - s_gnt[i]) * volume * n_lept);
+          })
+        : hr_th_c_next;
     if (fp_steps > MAX_FP_STEPS) {
       if (lane == 0) atomicOr(P.err, FPERR_STEPS);
       return;
@@ -934,9 +938,16 @@ __device__ __forceinline__ void fp_zone_body(const FpParams& P, const int lane) 
     }
     fp_sync<WMAX>();
     /* new temperature (:1440-1468) */
-    const double gbar = seq_sum_lds(0.0, 1, NT - 1, lane, s_seq, [&](int i) {
-      return s_gam[i] * s_fnew[i] * (s_gnt[i + 1] - s_gnt[i]);
-    });
+    /* gbar, and the next sub-step's hr_th_c over the same bins (s_fold = s_fnew
+     * now; n_lept and volume do not change before label 200): two in-order
+     * chains in one pass */
+    double gbar = 0.0;
+    hr_th_c_next = 0.0;
+    seq_sum2_lds(gbar, hr_th_c_next, 1, NT - 1, lane, s_seq,
+                 [&](int i) { return s_gam[i] * s_fnew[i] * (s_gnt[i + 1] - s_gnt[i]); },
+                 [&](int i) {
+                   return -(8.176e-7 * s_dgic[i] * s_fold[i] * (s_gnt[i + 1] - s_gnt[i]) * volume * n_lept);
+                 });
     double The_new = Th_e;
     PF_BEGIN();
     if (gbar > g_av) {
