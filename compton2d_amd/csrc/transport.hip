@@ -1634,26 +1634,49 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
  * sampled volume/surface packet from the packet store.  src >= 0: the census
  * slot (the fetch resolved the chunk list once per work chunk); src < 0:
  * packet-store entry -src - 1 */
+/* a census record's columns as loaded (the census branch of load_source):
+ * issued by pf_issue, turned into the packet by pf_apply */
+struct CensRec {
+  double rpre, zpre, wmu, cphi, ew, xnu;
+  uint32_t jk, bn;
+  uint64_t key;
+};
+
+__device__ __forceinline__ void pf_issue(const KParams& P0, CensRec& r, long long i) {
+  const KParams& P = cold(P0);
+  r.rpre = gld(P.cin.rpre + i); r.zpre = gld(P.cin.zpre + i);
+  r.wmu = gld(P.cin.wmu + i);
+  r.ew = gld(P.cin.ew + i); r.xnu = gld(P.cin.xnu + i);
+  r.jk = gld(P.cin.jk + i); r.bn = gld(P.cin.bins + i);
+  r.cphi = gld(P.cin.phi + i);
+  r.key = gld(P.cin.key + i);
+}
+
+__device__ __forceinline__ void pf_apply(const KParams& P0, Pkt& p, const CensRec& r) {
+  const KParams& P = cold(P0);
+  p.rpre = r.rpre; p.zpre = r.zpre;
+  p.wmu = clampd(r.wmu, 0.99999999);
+  p.ew = r.ew; p.xnu = r.xnu;
+#if C2D_TABLE_COMTOT
+  p.eta = r.cphi;                                    /* encoded azimuth (CensusSoA) */
+  p.esw = (r.bn & C2D_CENS_ESW) ? -1 : 1;
+  p.phi = 0.0;
+#else
+  p.phi = r.cphi;
+#endif
+  p.jph = (int32_t)(r.jk >> 16); p.kph = (int32_t)(r.jk & 0xffffu);
+  p.bins = r.bn & 0x00ffffffu;                       /* kap = 0 (census phase, H3) */
+  p.key = r.key;
+  p.sub = 0;
+  p.dcen = P.cdt;                                    /* imcfield2d.f:117 */
+}
+
 __device__ __forceinline__ void load_source(const KParams& P0, Pkt& p, long long src) {
   const KParams& P = cold(P0);
   if (src >= 0) {
-    const int64_t i = src;
-    p.rpre = gld(P.cin.rpre + i); p.zpre = gld(P.cin.zpre + i);
-    p.wmu = clampd(gld(P.cin.wmu + i), 0.99999999);
-    p.ew = gld(P.cin.ew + i); p.xnu = gld(P.cin.xnu + i);
-    const uint32_t jk = gld(P.cin.jk + i), bn = gld(P.cin.bins + i);
-#if C2D_TABLE_COMTOT
-    p.eta = gld(P.cin.phi + i);                        /* encoded azimuth (CensusSoA) */
-    p.esw = (bn & C2D_CENS_ESW) ? -1 : 1;
-    p.phi = 0.0;
-#else
-    p.phi = gld(P.cin.phi + i);
-#endif
-    p.jph = (int32_t)(jk >> 16); p.kph = (int32_t)(jk & 0xffffu);
-    p.bins = bn & 0x00ffffffu;                     /* kap = 0 (census phase, H3) */
-    p.key = gld(P.cin.key + i);
-    p.sub = 0;
-    p.dcen = P.cdt;                                    /* imcfield2d.f:117 */
+    CensRec r;
+    pf_issue(P, r, src);
+    pf_apply(P, p, r);
   } else {
     load_pk(p, P.pk, -src - 1);
     set_phi(p, p.phi);
@@ -1824,6 +1847,13 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
  * deposits, records and counters are the per-copy tracker's; the cell
  * tallies are summed in another order. */
 constexpr int BUNDLE_MAX = 32;
+/* C2D_PF_SRC: each lane claims its next census source while it runs the
+ * current one and issues that record's loads after the step's table loads
+ * have been waited for, so they complete under the rest of the step instead
+ * of stalling the next bundle_begin (packet-store sources load as before) */
+#ifndef C2D_PF_SRC
+#define C2D_PF_SRC 1
+#endif
 enum : int32_t {
   BF_TRACK = 1,     /* the recombined copy is on the path               */
   BF_SPEC = 2,      /* ... with a weight that assumes no more collisions */
@@ -1851,9 +1881,11 @@ __device__ __forceinline__ double UB(Bundle& b) {
 }
 
 /* start (or restart) the bundle at probe g0 of source b.src */
-__device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bundle& b) {
+__device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bundle& b,
+                                             bool from_pf = false, const CensRec* pr = nullptr) {
   Pkt& p = b.p;
-  load_source(P, p, b.src);
+  if (from_pf) pf_apply(P, p, *pr);   /* the census record prefetched into pr */
+  else load_source(P, p, b.src);
   const double ew0 = p.ew;
   const double s_ew = FDIV_POS(ew0, (double)P.split1);   /* imctrk2d.f:106-123 */
   const int G = min(P.split1 - b.g0, BUNDLE_MAX);
@@ -1936,7 +1968,8 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
 
 /* one shared step of the bundle (flight() for every copy on the path) */
 __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, const GenArgs& A,
-                                            Bundle& b, ComCache& cc, LaneCnt& lc, Prof& pf) {
+                                            Bundle& b, ComCache& cc, LaneCnt& lc, Prof& pf,
+                                            CensRec& nr, long long nitem, int& nst) {
 #ifdef C2D_HOT_RELOAD
   const KParams& P = cold_always(P1);
 #else
@@ -2145,6 +2178,17 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
   /* ---- the survivors' absorption points and deposits (imctrk2d.f:382-462),
    * at the step's starting point ---- */
   TP_MARK(pf, TP_EVENT);
+#if C2D_PF_SRC
+  /* the step's own loads have been waited for and its records stored: the
+   * next source's record loads issue here and complete under the VALU-only
+   * point loop and the refill */
+  if (nst == 1 && nitem >= 0) {
+    pf_issue(P, nr, nitem);
+    nst = 2;
+  }
+#else
+  (void)nr; (void)nitem; (void)nst;
+#endif
   if (nabs > 0) {
     double sum_prdep = 0.0;
 #ifdef C2D_ABLATE_PROBE_ABS            /* profiling ablation only (tools/build_sweep.sh) */
@@ -2256,59 +2300,89 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
   pf.t = clock64();
 #endif
   census_chunk_load(P, tid >> 6, lane);
+  /* the lane's next source (C2D_PF_SRC): nst 0 none, 1 claimed, 2 record loaded */
+  CensRec nr = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0u, 0u, 0ull};
+  long long nitem = 0;
+  int nst = 0;
+
+  /* chunked, wave-aggregated work fetch from the workgroup's shard of the
+   * item range, then from the following ones: every lane with `want` gets
+   * the next item (its census slot or packet-store entry) while items last */
+  auto claim = [&](bool want, long long& it_out) -> bool {
+    bool ok = false;
+    unsigned long long needm = __ballot(want);
+    while (needm != 0ull) {
+      if (chunk_base >= chunk_end) {
+        for (;;) {
+          if (shard_try >= C2D_WORK_SHARDS) { exhausted = true; break; }
+          /* shard bounds on work-chunk (= census-chunk) boundaries */
+          const int s = (shard0 + shard_try) % C2D_WORK_SHARDS;
+          const long long lo = (n_items * s / C2D_WORK_SHARDS) & ~(CHUNK - 1);
+          const long long hi = s + 1 == C2D_WORK_SHARDS
+                                   ? n_items : (n_items * (s + 1) / C2D_WORK_SHARDS) & ~(CHUNK - 1);
+          unsigned long long nb = 0;
+          if (lane == 0)
+            nb = atomicAdd(A.work_sh + (size_t)s * C2D_EV_SHARD_STRIDE, (unsigned long long)CHUNK);
+          nb = rfl64(nb);
+          if (lo + (long long)nb < hi) {
+            chunk_base = lo + (long long)nb;
+            chunk_end = chunk_base + CHUNK < hi ? chunk_base + CHUNK : hi;
+            chunk_slot = chunk_base;
+            if (cold(P).clist && chunk_base < cold(P).n_cens_items) {
+              const int32_t id = __builtin_amdgcn_readfirstlane(gld(cold(P).clist + (chunk_base >> C2D_CCHUNK_LOG)));
+              chunk_slot = (long long)id << C2D_CCHUNK_LOG;
+              if (lane == 0)
+                census_track(tid >> 6, id,
+                             (uint32_t)(min(chunk_end, (long long)cold(P).n_cens_items) - chunk_base));
+            }
+            break;
+          }
+          shard_try++;
+        }
+        if (exhausted) break;
+      }
+      const long long avail = chunk_end - chunk_base;
+      const unsigned long long lt = (lane == 0) ? 0ull : (needm & ((~0ull) >> (64 - lane)));
+      const long long rank = __popcll(lt);
+      const long long nneed = __popcll(needm);
+      if (((needm >> lane) & 1ull) && rank < avail) {
+        const long long it = chunk_base + rank;
+        it_out = it < cold(P).n_cens_items ? chunk_slot + (it & (CHUNK - 1))
+                                           : -(it - cold(P).n_cens_items) - 1;
+        ok = true;
+      }
+      chunk_base += (nneed < avail ? nneed : avail);
+      needm = __ballot(want && !ok);
+    }
+    return ok;
+  };
 
   for (;;) {
-    /* ---- refill idle lanes: chunked, wave-aggregated work fetch from the
-     * workgroup's shard of the item range, then from the following ones ---- */
-    bool got = false;
+    /* ---- refill idle lanes: the prefetched source, else a fetched one;
+     * then claim the next source of every lane that has none ---- */
+    bool got = false, from_pf = false;
     long long item = -1;
+#if C2D_PF_SRC
+    if (!busy && nst != 0) {
+      got = true;
+      item = nitem;
+      from_pf = nst == 2;
+      nst = 0;
+    }
+#endif
     if (!exhausted) {
-      unsigned long long needm = __ballot(!busy);
-      while (needm != 0ull) {
-        if (chunk_base >= chunk_end) {
-          for (;;) {
-            if (shard_try >= C2D_WORK_SHARDS) { exhausted = true; break; }
-            /* shard bounds on work-chunk (= census-chunk) boundaries */
-            const int s = (shard0 + shard_try) % C2D_WORK_SHARDS;
-            const long long lo = (n_items * s / C2D_WORK_SHARDS) & ~(CHUNK - 1);
-            const long long hi = s + 1 == C2D_WORK_SHARDS
-                                     ? n_items : (n_items * (s + 1) / C2D_WORK_SHARDS) & ~(CHUNK - 1);
-            unsigned long long nb = 0;
-            if (lane == 0)
-              nb = atomicAdd(A.work_sh + (size_t)s * C2D_EV_SHARD_STRIDE, (unsigned long long)CHUNK);
-            nb = rfl64(nb);
-            if (lo + (long long)nb < hi) {
-              chunk_base = lo + (long long)nb;
-              chunk_end = chunk_base + CHUNK < hi ? chunk_base + CHUNK : hi;
-              chunk_slot = chunk_base;
-              if (cold(P).clist && chunk_base < cold(P).n_cens_items) {
-                const int32_t id = __builtin_amdgcn_readfirstlane(gld(cold(P).clist + (chunk_base >> C2D_CCHUNK_LOG)));
-                chunk_slot = (long long)id << C2D_CCHUNK_LOG;
-                if (lane == 0)
-                  census_track(tid >> 6, id,
-                               (uint32_t)(min(chunk_end, (long long)cold(P).n_cens_items) - chunk_base));
-              }
-              break;
-            }
-            shard_try++;
-          }
-          if (exhausted) break;
-        }
-        const long long avail = chunk_end - chunk_base;
-        const unsigned long long lt = (lane == 0) ? 0ull : (needm & ((~0ull) >> (64 - lane)));
-        const long long rank = __popcll(lt);
-        const long long nneed = __popcll(needm);
-        if (((needm >> lane) & 1ull) && rank < avail) {
-          /* the source: its census slot (this work chunk's) or packet-store entry */
-          const long long it = chunk_base + rank;
-          item = it < cold(P).n_cens_items ? chunk_slot + (it & (CHUNK - 1))
-                                           : -(it - cold(P).n_cens_items) - 1;
-          got = true;
-        }
-        chunk_base += (nneed < avail ? nneed : avail);
-        needm = __ballot(!busy && !got);
+      const bool g2 = claim(!busy && !got, item);
+      got = got || g2;
+    }
+#if C2D_PF_SRC
+    if (!exhausted) {
+      long long ni = 0;
+      if (claim((busy || got) && nst == 0, ni)) {
+        nitem = ni;
+        nst = 1;
       }
     }
+#endif
     TP_MARK(pf, TP_REFILL);
 #ifdef C2D_TR_PROF
     pf.acc[TP_ITER] += 1;
@@ -2320,7 +2394,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
       b.g0 = 0;
       b.nscat = 0;
       cc.cell0 = -1; cc.cell1 = -1;
-      bundle_begin(P, T, b);
+      bundle_begin(P, T, b, from_pf, &nr);
       busy = true;
     }
     if (exhausted && __ballot(busy) == 0ull) break;
@@ -2329,7 +2403,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
 #ifdef C2D_TR_PROF
       pf.acc[TP_LANES] += __popcll(__ballot(1));
 #endif
-      bundle_step(P, T, A, b, cc, lc, pf);
+      bundle_step(P, T, A, b, cc, lc, pf, nr, nitem, nst);
       TP_MARK(pf, TP_EVENT);
       if (!b.alive && !(b.flags & BF_TRACK)) {
         if ((b.flags & (BF_TKILL | BF_RERUN)) == BF_TKILL)

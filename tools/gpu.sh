@@ -17,7 +17,7 @@
 #   fpab:<t1>,..   the fp run for each build (as ab:)
 #   fppmc          rocprofv3 kernel trace + SQ counters of that FP run (memo on)
 #   fpprof         FP section timers off the clamp (sweep build "fpprof", tools/fp_prof.py)
-#   trprof         wave section timers of the C3 run (sweep build "prof", tools/tr_prof.py)
+#   trprof[:t,..]  wave section timers of the C3 run (sweep builds, default "prof"; tools/tr_prof.py)
 #   n2             rehearse bench.py's N>1 path: 2 gloo ranks on device 0 vs 1 rank
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -95,9 +95,12 @@ for r in "$@"; do
     fpprof)  # FP section timers of the -DC2D_FP_PROF build (make FP_FLAGS=-DC2D_FP_PROF OUT=sweep/fpprof/...)
       C2D_LIBRARY=$PWD/compton2d_amd/sweep/fpprof/libcompton2d.so run 300 fpprof python tools/fp_prof.py --nz 30 --nr 9 --vary
       tail -1 "$O/fpprof.out" ;;
-    trprof)  # section timers of the -DC2D_TR_PROF build (tools/build_sweep.sh prof:3:off:...,-DC2D_TR_PROF)
-      C2D_LIBRARY=$PWD/compton2d_amd/sweep/prof/libcompton2d.so run 300 trprof python tools/tr_prof.py --steps ${STEPS}
-      tail -2 "$O/trprof.out" ;;
+    trprof|trprof:*)  # section timers of -DC2D_TR_PROF builds (tools/build_sweep.sh prof:3:off:...,-DC2D_TR_PROF)
+      tags=prof; [ "$r" = trprof ] || tags=$(echo "${r#trprof:}" | tr ',' ' ')
+      for t in $tags; do
+        C2D_LIBRARY=$PWD/compton2d_amd/sweep/$t/libcompton2d.so run 300 "trprof_$t" python tools/tr_prof.py --steps ${STEPS}
+        tail -2 "$O/trprof_$t.out"
+      done ;;
     n2)
       run 300 n2_w1 python -u bench.py --workload c3 --sources 40000000 --steps 3 --warmup 2 --no-cpu-baseline
       C2D_ONE_GPU=1 C2D_DIST_BACKEND=gloo run 300 n2_w2 python -u -m torch.distributed.run --nnodes=1 \
