@@ -32,6 +32,8 @@ extern "C" int c2d_launch_scatter_exact(const KParams* P, const GenArgs* A, int 
 extern "C" int c2d_launch_scatter_fast(const KParams* P, const GenArgs* A, int grid, hipStream_t s);
 extern "C" int c2d_transport_occupancy_exact(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds);
+extern "C" int c2d_aux_occupancy_exact(int which, int* blocks_per_cu);
+extern "C" int c2d_aux_occupancy_fast(int which, int* blocks_per_cu);
 extern "C" int c2d_launch_bundle_exact(const KParams* P, const GenArgs* A, int grid, size_t lds,
                                        hipStream_t s);
 extern "C" int c2d_launch_bundle_fast(const KParams* P, const GenArgs* A, int grid, size_t lds,
@@ -112,6 +114,7 @@ struct c2d_ctx {
   size_t lds_bytes = 0;
   /* generation 0 as probe bundles (c2d_bundle_kernel): its LDS and grid */
   int bundle = 1, bundle_grid = 0;
+  int src_grid = 0, sc_grid = 0;   /* CUs x resident blocks of the source / scatter kernels */
   size_t bundle_lds = 0;
   /* census SoA(s) of cens_phys records each.  Double-buffered:
    * census_capacity + one append chunk per wave slot; the compaction's work
@@ -386,6 +389,15 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
     if (orc) return fail(c, C2D_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)orc));
     c->bundle_lds = c->lds_bytes;
     c->bundle_grid = c->n_cu * std::max(1, b0);
+  }
+  {
+    auto aocc = cfg->comtot_mode == C2D_COMTOT_TABLE ? c2d_aux_occupancy_fast : c2d_aux_occupancy_exact;
+    int bs = 0, bc = 0;
+    orc = aocc(0, &bs);
+    if (!orc) orc = aocc(1, &bc);
+    if (orc) return fail(c, C2D_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)orc));
+    c->src_grid = c->n_cu * std::max(1, bs);
+    c->sc_grid = c->n_cu * std::max(1, bc);
   }
   {
     /* the census.  A wave slot keeps one partly filled append chunk over
@@ -1243,9 +1255,9 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   auto launch_tr = fast ? c2d_launch_transport_fast : c2d_launch_transport_exact;
   auto launch_src = fast ? c2d_launch_source_fast : c2d_launch_source_exact;
   auto launch_sc = fast ? c2d_launch_scatter_fast : c2d_launch_scatter_exact;
-  const int aux_grid_max = c->n_cu * 8;
-  auto aux_grid = [&](int64_t n) {
-    return (int)std::max<int64_t>(1, std::min<int64_t>(aux_grid_max, (n + 255) / 256));
+  /* grid-stride kernels: one round of resident blocks at most */
+  auto aux_grid = [&](int64_t n, int gmax) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(gmax, (n + 255) / 256));
   };
   auto tr_grid = [&](int64_t n) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(c->max_grid, (n + C2D_TR_BLOCK - 1) / C2D_TR_BLOCK));
@@ -1258,7 +1270,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   {
     HIPCHK(c, hipEventRecord(c->ev_g0a, c->stream));
     if (n_src > 0) {
-      int rc = launch_src(c->dP, aux_grid(n_src), c->stream);
+      int rc = launch_src(c->dP, aux_grid(n_src, c->src_grid), c->stream);
       if (rc) return fail(c, C2D_E_HIP, "source launch: %s", hipGetErrorString((hipError_t)rc));
       launches++;
     }
@@ -1314,7 +1326,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
       A.work_counter = c->ctl + CTL_WORK;
       A.item_begin = b; A.item_end = e;
       A.n2_in = n2; A.n3_in = n3;
-      int rc = launch_sc(c->dP, &A, aux_grid(e - b), c->stream);
+      int rc = launch_sc(c->dP, &A, aux_grid(e - b, c->sc_grid), c->stream);
       if (rc) return fail(c, C2D_E_HIP, "scatter launch (gen %d): %s", gen, hipGetErrorString((hipError_t)rc));
       rc = launch_tr(c->dP, &A, tr_grid(e - b), c->lds_bytes, c->stream);
       if (rc) return fail(c, C2D_E_HIP, "transport launch (gen %d): %s", gen, hipGetErrorString((hipError_t)rc));

@@ -2554,6 +2554,16 @@ extern "C" int C2D_SFX(c2d_launch_scatter)(const c2d::KParams* P_dev, const c2d:
   return (int)hipGetLastError();
 }
 
+/* resident blocks per CU of the source (which = 0) and scatter (1) kernels:
+ * their static LDS (Geo image, prefix) limits them below the 8 per CU a
+ * plain CUs x 8 grid would assume, leaving a second partial round */
+extern "C" int C2D_SFX(c2d_aux_occupancy)(int which, int* blocks_per_cu) {
+  hipError_t e = which == 0
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, C2D_SFX(c2d::c2d_source_kernel), c2d::SBLOCK, 0)
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, C2D_SFX(c2d::c2d_scatter_kernel), c2d::SBLOCK, 0);
+  return (int)e;
+}
+
 extern "C" int C2D_SFX(c2d_transport_occupancy)(int* blocks_per_cu, size_t lds_bytes) {
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
       blocks_per_cu, C2D_SFX(c2d::c2d_transport_kernel), c2d::BLOCK, lds_bytes);
