@@ -257,12 +257,20 @@ def build_c3(args, rank, world, local, dev, sources, ccap, ecap, mode):
     eng.use_tally_tensor(T)
     ex, ex_desc = tally_exchange(eng, T, rank, world, dev)
     run = CoupledRun(eng, wl, device_resident=not args.host_tables, allreduce=ex)
+    # C3's named output: the step's escapes binned into the observer-frame SED
+    # of postprocessing/mrk421_sed.input (pspt.c:245-294) on the device, from
+    # the event buffer the transport just wrote (no event text, no download)
+    from compton2d_amd import observer
+    eng.obs_begin(observer.mrk421_sed_binning())
 
     def one_step():
         r = dict(run.step())
+        eng.obs_accumulate(None)
         r["census_records"] = float(eng.census_count())
+        r["escape_events"] = float(eng.last_event_count())
         return r
-    return eng, run, one_step, wl, wl.description, ex_desc
+    return eng, run, one_step, wl, wl.description + "; every step's escapes binned on the device " \
+        "into the mrk421_sed.input SED (pspt.c)", ex_desc
 
 
 def build_c2(args, rank, world, local, dev, sources, ccap, ecap, mode):
@@ -424,6 +432,8 @@ def main():
         one_step()
     distributed.barrier(dev)
     torch.cuda.synchronize()
+    if wk == "c3":
+        eng.obs_begin(eng._obs)            # the timed steps' SED alone (zeroes sums and kernel ms)
     t0 = time.perf_counter()
     rows = []
     for _ in range(args.steps):
@@ -435,6 +445,7 @@ def main():
     # packet-steps of all ranks: the counters were all-reduced with the tallies
     steps_global = sum(r["packet_steps"] for r in rows)
     census_timed_start = rows[0]["census_records"] if rows else census_start
+    all_paths = distributed.allreduce_sum(float(sum(r["all_paths"] for r in rows)), dev)
     if rank != 0:
         eng.close()
         return
@@ -488,6 +499,13 @@ def main():
                          "valu_issue_frac": pmc.get("fp_valu_issue_frac"),
                          "wait_frac": pmc.get("fp_wait_frac")}
         kernels["volume_em"] = {"ms_avg": per_step.get("vem_kernel_ms", 0.0), "zones": ncell}
+        _, _, sed_cnt, sed_ms = eng.obs_result()
+        kernels["sed_binning"] = {
+            "ms_avg": sed_ms / args.steps, "events_per_step": per_step.get("escape_events"),
+            "binned_per_step": float(sed_cnt.sum()) / args.steps,
+            "deck": "postprocessing/mrk421_sed.input (30 time bins 1.6e4-6e4 s, mu 0.99944-0.99964, "
+                    "100 log channels 1e-7-1e10 keV)",
+            "bound": "hbm: 56 B per escape event read once"}
     rounds, moved, phys = eng.last_compaction()
     chunks, recycled, unrecycled, held = eng.last_census_chunks()
     out = {
@@ -501,6 +519,11 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
+        # the hardware rate beside the metric: lane path-steps (one pass of a
+        # GPU lane through the geometry block, whatever the copies on it) of
+        # all ranks and generations per second, and the copies a path carries
+        "path_steps_per_s": all_paths / elapsed,
+        "packet_steps_per_path": steps_global / all_paths if all_paths else None,
         "dtype": "f64",
         "data": {"c3": "synthetic: the reference's P_nontherm electrons of the inputm.dat medium in "
                        "every zone, tables recomputed on the device every step from the evolving "
@@ -558,6 +581,12 @@ def main():
             "steps_per_launch_avg": steps_per_launch,
             "paths_per_launch_avg": paths_per_launch,
             "survey_formula_frac": survey_frac,
+            # what binds the kernel: VALU issue (PMC SQ_INSTS_VALU per path-step
+            # at the achieved rate) against one wave64 VALU op / 4 cycles / SIMD
+            "issue_roof": {"bound": "valu_issue", "frac": valu_frac,
+                           "valu_wave_insts_per_path": vpp,
+                           "peak": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU op",
+                           "source": pmc.get("source")},
         },
         "kernels": kernels,
         "cpu_baseline": None,

@@ -130,6 +130,8 @@ struct c2d_ctx {
   int32_t* clist[2] = {nullptr, nullptr};
   int ccur = 0;
   int64_t n_clist = 0;
+  bool g0_launched = false;      /* this step's generation 0 has rewritten the chunked census */
+  bool census_lost = false;      /* a failed in-place step overwrote the census (c2d_run_step) */
   int32_t* pool = nullptr;       /* [nchunks] free chunks at the step's start */
   int32_t* out_list = nullptr;   /* [nchunks] chunks the step took            */
   int32_t* relist = nullptr;     /* [nchunks] chunks freed and handed on      */
@@ -412,8 +414,14 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
        * ones, and 1/16 of the capacity for chunks whose sources are still
        * in flight when the waves need new ones (c2d_device.hpp) */
       c->cens_chunk = C2D_CCHUNK;
-      c->nchunks = (ccap + C2D_CCHUNK - 1) / C2D_CCHUNK + (ccap / 16 + C2D_CCHUNK - 1) / C2D_CCHUNK +
-                   4 * c->n_ws + 64;
+      /* additive slack: per wave slot one partly filled chunk, the 2-3 chunks
+       * whose sources are in flight and the free stack's turnover; test knob
+       * C2D_CHUNK_SLACK replaces it by a fixed number of chunks, so a test
+       * can pin that the usable capacity is census_capacity with only the
+       * chunks its waves need beside the capacity/16 term */
+      int64_t slack = 4 * c->n_ws + 64;
+      if (const char* e = getenv("C2D_CHUNK_SLACK")) slack = std::max<long long>(0, atoll(e));
+      c->nchunks = (ccap + C2D_CCHUNK - 1) / C2D_CCHUNK + (ccap / 16 + C2D_CCHUNK - 1) / C2D_CCHUNK + slack;
       c->cens_phys = c->nchunks * C2D_CCHUNK;
       for (int b = 0; b < 2; b++) HIPCHK(c, dalloc(&c->clist[b], (size_t)c->nchunks));
       HIPCHK(c, dalloc(&c->pool, (size_t)c->nchunks));
@@ -1149,8 +1157,34 @@ static int census_compact(c2d_ctx* c, const DevCensus& cb, int64_t R, int64_t W)
   return C2D_OK;
 }
 
+static int run_step_body(c2d_ctx* c);
+
+/* A failed step leaves the double-buffered census as it was (the step wrote
+ * the other buffer).  The chunked census is rewritten in place from the
+ * generation-0 launch on, so a failure after that launch loses it: the
+ * context then holds no census and every census read, and the next step,
+ * fail with C2D_E_STATE until c2d_census_import or c2d_census_truncate
+ * (ADVICE r03). */
 extern "C" int c2d_run_step(c2d_ctx* c) {
   if (!c) return C2D_E_ARG;
+  if (c->census_lost)
+    return fail(c, C2D_E_STATE, "the census was lost by a failed in-place step: c2d_census_import or "
+                "c2d_census_truncate first");
+  c->g0_launched = false;
+  const int rc = run_step_body(c);
+  if (rc && c->chunked && c->g0_launched) {
+    c->n_census = 0;
+    c->n_clist = 0;
+    c->census_lost = true;
+  }
+  return rc;
+}
+
+static int census_lost(c2d_ctx* c, const char* who) {
+  return fail(c, C2D_E_STATE, "%s: the census was lost by a failed in-place step", who);
+}
+
+static int run_step_body(c2d_ctx* c) {
   if (!c->have_step) return fail(c, C2D_E_STATE, "c2d_set_step must precede c2d_run_step");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const c2d_config& cfg = c->cfg;
@@ -1291,6 +1325,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
       if (const char* e = getenv("C2D_BUNDLE_GRID")) gmax = std::max<int64_t>(1, std::min<int64_t>(gmax, atoll(e)));
       const int grid = (int)std::max<int64_t>(
           1, std::min<int64_t>(gmax, (A.n_items + C2D_TR_BLOCK - 1) / C2D_TR_BLOCK));
+      c->g0_launched = true;
       int rc = launch_b(c->dP, &A, grid, c->bundle_lds, c->stream);
       if (rc) return fail(c, C2D_E_HIP, "bundle launch (gen 0): %s", hipGetErrorString((hipError_t)rc));
       launches++;
@@ -1436,6 +1471,7 @@ extern "C" int c2d_run_step(c2d_ctx* c) {
   }
   c->n_census = cens_live;
   c->cur = out_buf;
+  c->g0_launched = false;        /* the new census is complete: later failures keep it */
   if (herr & ERR_EVENT) {
     unsigned long long fill = 0;
     for (int sh = 0; sh < C2D_EV_SHARDS; sh++)
@@ -1584,6 +1620,7 @@ static int census_download(c2d_ctx* c, int64_t first, int64_t stride, int64_t m,
 extern "C" int c2d_census_export_range(c2d_ctx* c, int64_t first, int64_t stride, double* d6,
                                        int32_t* i5, uint64_t* keys, int64_t cap, int64_t* n) {
   if (!c || !n || first < 0 || stride < 1) return C2D_E_ARG;
+  if (c->census_lost) return census_lost(c, "c2d_census_export_range");
   const int64_t avail = first < c->n_census ? (c->n_census - first + stride - 1) / stride : 0;
   *n = avail;
   const int64_t m = std::min(cap, avail);
@@ -1595,6 +1632,7 @@ extern "C" int c2d_census_export_range(c2d_ctx* c, int64_t first, int64_t stride
 extern "C" int c2d_census_export(c2d_ctx* c, double* d6, int32_t* i5, uint64_t* keys, int64_t cap,
                                  int64_t* n) {
   if (!c || !n) return C2D_E_ARG;
+  if (c->census_lost) return census_lost(c, "c2d_census_export");
   *n = c->n_census;
   const int64_t m = std::min(cap, c->n_census);
   if (m <= 0) return C2D_OK;
@@ -1646,11 +1684,13 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
     c->n_clist = k;
   }
   c->n_census = n;
+  c->census_lost = false;
   return C2D_OK;
 }
 
 extern "C" int c2d_census_pack(c2d_ctx* c, int64_t first, int64_t n, uint64_t* d_rec) {
   if (!c || first < 0 || n < 0 || (n > 0 && !d_rec)) return C2D_E_ARG;
+  if (c->census_lost) return census_lost(c, "c2d_census_pack");
   if (first + n > c->n_census)
     return fail(c, C2D_E_ARG, "c2d_census_pack: records [%lld, %lld) beyond the census (%lld)",
                 (long long)first, (long long)(first + n), (long long)c->n_census);
@@ -1666,6 +1706,7 @@ extern "C" int c2d_census_pack(c2d_ctx* c, int64_t first, int64_t n, uint64_t* d
 
 extern "C" int c2d_census_append(c2d_ctx* c, const uint64_t* d_rec, int64_t n) {
   if (!c || n < 0 || (n > 0 && !d_rec)) return C2D_E_ARG;
+  if (c->census_lost) return census_lost(c, "c2d_census_append");
   if (c->n_census + n > c->cfg.census_capacity)
     return fail(c, C2D_E_CENSUS_OVERFLOW, "c2d_census_append: %lld + %lld > capacity %lld",
                 (long long)c->n_census, (long long)n, (long long)c->cfg.census_capacity);
@@ -1697,6 +1738,7 @@ extern "C" int c2d_census_append(c2d_ctx* c, const uint64_t* d_rec, int64_t n) {
 
 extern "C" int c2d_census_truncate(c2d_ctx* c, int64_t n) {
   if (!c || n < 0 || n > c->n_census) return C2D_E_ARG;
+  c->census_lost = false;
   c->n_census = n;
   if (c->chunked) c->n_clist = (n + C2D_CCHUNK - 1) / C2D_CCHUNK;
   return C2D_OK;
@@ -2196,14 +2238,21 @@ extern "C" int c2d_obs_begin(c2d_ctx* c, const c2d_obs_bins* b) {
   return C2D_OK;
 }
 
-static int obs_launch(c2d_ctx* c, const double* ev, int64_t m) {
-  if (m == 0) return C2D_OK;
+/* Bin `nseg` event segments (device pointer, count) back to back on the
+ * context's stream; one event pair and one synchronisation around them all. */
+static int obs_launch_segments(c2d_ctx* c, const double* const* ev, const int64_t* m, int nseg) {
+  int64_t tot = 0;
+  for (int s = 0; s < nseg; s++) tot += m[s];
+  if (tot == 0) return C2D_OK;
   /* enough blocks to fill the chip, each privatising its own histogram */
   const int64_t bs = c2d_obs_block();
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * c->obs_wg_per_cu, (m + bs - 1) / bs));
   HIPCHK(c, hipEventRecord(c->ev_g0a, c->stream));
-  int rc = c2d_launch_obs(&c->obs, ev, m, grid, c->stream);
-  if (rc) return fail(c, C2D_E_HIP, "obs launch: %s", hipGetErrorString((hipError_t)rc));
+  for (int s = 0; s < nseg; s++) {
+    if (m[s] == 0) continue;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * c->obs_wg_per_cu, (m[s] + bs - 1) / bs));
+    int rc = c2d_launch_obs(&c->obs, ev[s], m[s], grid, c->stream);
+    if (rc) return fail(c, C2D_E_HIP, "obs launch: %s", hipGetErrorString((hipError_t)rc));
+  }
   HIPCHK(c, hipEventRecord(c->ev_g0b, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   float ms = 0.f;
@@ -2212,16 +2261,22 @@ static int obs_launch(c2d_ctx* c, const double* ev, int64_t m) {
   return C2D_OK;
 }
 
+static int obs_launch(c2d_ctx* c, const double* ev, int64_t m) {
+  return obs_launch_segments(c, &ev, &m, 1);
+}
+
 extern "C" int c2d_obs_accumulate(c2d_ctx* c, const double* events, int64_t n) {
   if (!c) return C2D_E_ARG;
   if (!c->obs_ready) return fail(c, C2D_E_STATE, "c2d_obs_begin must precede c2d_obs_accumulate");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (!events) {
+    const double* seg[C2D_EV_SHARDS];
+    int64_t cnt[C2D_EV_SHARDS];
     for (int sh = 0; sh < C2D_EV_SHARDS; sh++) {
-      const int rc = obs_launch(c, c->ev + (size_t)sh * c->ev_cap_sh * C2D_EVENT_WORDS, c->ev_cnt[sh]);
-      if (rc) return rc;
+      seg[sh] = c->ev + (size_t)sh * c->ev_cap_sh * C2D_EVENT_WORDS;
+      cnt[sh] = c->ev_cnt[sh];
     }
-    return C2D_OK;
+    return obs_launch_segments(c, seg, cnt, C2D_EV_SHARDS);
   }
   if (n < 0) return C2D_E_ARG;
   if (n > c->obs_ev_cap) {

@@ -75,6 +75,16 @@ def allreduce_max(value: float, device=None) -> float:
     return float(t.item())
 
 
+def allreduce_sum(value: float, device=None) -> float:
+    if not is_dist():
+        return value
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
 def barrier(device=None) -> None:
     if is_dist():
         import torch.distributed as dist

@@ -216,6 +216,12 @@ class Engine:
     def tallies(self) -> dict:
         return abi.split_tallies(self.tallies_raw(), self.nz, self.nr, self.nmu)
 
+    def last_event_count(self) -> int:
+        """Escape events the last transport step wrote (c2d_events with no buffer)."""
+        n = C.c_int64()
+        self._check(self.lib.c2d_events(self.ctx, None, 0, C.byref(n)))
+        return n.value
+
     def events(self) -> np.ndarray:
         n = C.c_int64()
         self._check(self.lib.c2d_events(self.ctx, None, 0, C.byref(n)))

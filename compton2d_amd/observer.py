@@ -41,6 +41,11 @@ PSPT_T_MAX, PSPT_CH_MAX = 90, 200            # pspt.c:8-10 (t_max, ch_max)
 PLCM_ST_MAX, PLCM_MU_MAX, PLCM_CH_MAX = 1024, 10, 20   # plcm.c:6-8
 # plcm.c:251-266: default energy regions [keV]
 PLCM_REGIONS = ((1e-3, 3e-3), (2., 4.), (9., 15.), (15., 20.), (20., 60.), (5e5, 5e7), (1e9, 1e10))
+# postprocessing/mrk421_sed.input, the pspt deck of BASELINE configs[2] (C3): input
+# series, Gamma, r_max, output file, n_t, t_start, t_end, mu window, 1 log region
+# of 100 channels over 1e-7 .. 1e10 keV (an input deck: data, one value a line)
+MRK421_SED_DECK = "\n".join(["p001_evb.dat", "33", "1e16", "sed30.dat", "30", "1.6e4", "6e4", "0.99944", "0.99964",
+                             "1", "1e-7", "1e10", "100", "0", "n", ""])
 
 
 # ---------------------------------------------------------------------------
@@ -213,6 +218,12 @@ def parse_pspt_deck(text: str) -> Binning:
     b = sed_binning(gam_bulk, rmax, n_t, t_start, t_end, mu0, mu1, regs)
     b.infile, b.outfiles = infile, [outfile]
     return b
+
+
+def mrk421_sed_binning() -> Binning:
+    """The SED binning of C3's named output (postprocessing/mrk421_sed.input
+    through pspt.c:105-205)."""
+    return parse_pspt_deck(MRK421_SED_DECK)
 
 
 def parse_plcm_deck(text: str) -> Binning:

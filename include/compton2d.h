@@ -349,7 +349,13 @@ int  c2d_transport_step(c2d_ctx* ctx, const c2d_step_in* in);
 int  c2d_set_step(c2d_ctx* ctx, const c2d_step_in* in);
 /* Advance the clock only (tables unchanged, e.g. T_const=1 runs). */
 int  c2d_set_clock(c2d_ctx* ctx, int32_t ncycle, double time, double dt);
-/* Transport with the tables of the last c2d_set_step. */
+/* Transport with the tables of the last c2d_set_step.
+ * On failure the double-buffered census (census_inplace = 0) is left as it
+ * was.  The chunked census (census_inplace = 1) is rewritten in place once
+ * generation 0 runs, so a failure after that LOSES it: c2d_census_count
+ * then reports 0, and the census export/pack/append calls and the next
+ * c2d_run_step return C2D_E_STATE until c2d_census_import or
+ * c2d_census_truncate starts a new census. */
 int  c2d_run_step(c2d_ctx* ctx);
 /* Use caller-owned device memory (>= layout.total doubles on the context's
  * device) as the fused tally buffer, e.g. a torch tensor that is then

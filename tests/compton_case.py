@@ -45,6 +45,11 @@ def fib_seed(k: int) -> int:
     return FIB_SEED0 + 7919 * k
 
 
+def lin_seed(k: int) -> int:
+    """Lineage seed of the k-th lineage-stream run (tests/golden/compton_lin.npz)."""
+    return LINEAGE_SEED + 104729 * (k + 1)
+
+
 def workload(mode=abi.COMTOT_EXACT, seed=LINEAGE_SEED, rank=0, world=1, n=IDENT_SOURCES, device=0,
              queue_capacity=None):
     grid, si = S.workload(mode=mode, seed=seed, rank=rank, world=world, n=n, device=device)

@@ -114,6 +114,59 @@ def make_fib(runs, procs, work):
                                           m, sd / np.where(m > 0, m, 1)))
 
 
+def _lin_run_job(args):
+    """One lineage-stream run of FIB_SOURCES sources (own seed), as a fib run:
+    probe bundles (the GPU's algorithm) or per-copy probes (C2O_PROBE_BUNDLES=0)."""
+    import os
+    k, seed, n, bundles, work = args
+    out = Path(work) / ("lin%d_%05d.npy" % (bundles, k))
+    if out.exists():
+        return k, np.load(out)
+    os.environ["C2O_PROBE_BUNDLES"] = str(bundles)
+    import compton_case as CC
+    t0 = time.time()
+    T = CC.oracle_run(("lineage", seed, n, 0, 1, "ref"))
+    F, E, cnt = CC.summary(T)
+    rec = np.concatenate([F, E, cnt, [time.time() - t0]])
+    np.save(out, rec)
+    return k, rec
+
+
+def make_lin(runs, procs, work):
+    """compton_lin.npz: `runs` lineage-stream runs per probe mode (bundles and
+    per-copy), each FIB_SOURCES sources with seed lin_seed(k), per-run F(E),
+    light curves and counters -- the lineage side of the Compton-component
+    comparison with run-to-run (not shard) variances, and the bundles vs
+    per-copy split on identical run sizes (tests/test_compton_oracle.py)."""
+    import compton_case as CC
+    import oracle_lib as OL
+    OL.build()
+    work = Path(work)
+    work.mkdir(parents=True, exist_ok=True)
+    out = {}
+    t0 = time.time()
+    with get_context("spawn").Pool(procs) as pool:
+        for bundles in (1, 0):
+            jobs = [(k, CC.lin_seed(k), CC.FIB_SOURCES, bundles, str(work)) for k in range(runs)]
+            recs = [None] * runs
+            for i, (k, rec) in enumerate(pool.imap_unordered(_lin_run_job, jobs)):
+                recs[k] = rec
+                if i % 20 == 0:
+                    print("lin%d run %d/%d (%.0f s)" % (bundles, i + 1, runs, time.time() - t0), flush=True)
+            R = np.array(recs)
+            nb = 128
+            tag = "bundle" if bundles else "copy"
+            out[tag + "_F"] = R[:, :nb]
+            out[tag + "_edout"] = R[:, nb:nb + 5]
+            out[tag + "_counters"] = R[:, nb + 5:nb + 5 + 16]
+            out[tag + "_cpu_seconds"] = R[:, -1]
+    np.savez_compressed(HERE / "compton_lin.npz", seeds=np.array([CC.lin_seed(k) for k in range(runs)]),
+                        sources=CC.FIB_SOURCES, n_e_factor=CC.N_E_FACTOR, **out)
+    for tag in ("bundle", "copy"):
+        c = out[tag + "_counters"]
+        print("lin %s: %d runs, %.4g collisions per run" % (tag, runs, c[:, 3].mean()))
+
+
 def _fib_check(seed):
     import compton_case as CC
     return CC.oracle_run(("fib", seed, CC.FIB_CHECK_SOURCES))
@@ -124,12 +177,15 @@ def main():
     ap.add_argument("--runs", type=int, default=1200)
     ap.add_argument("--procs", type=int, default=8)
     ap.add_argument("--work", default="/tmp/c2d_compton_fib")
-    ap.add_argument("--only", choices=("ident", "fib"), default=None)
+    ap.add_argument("--lin-runs", type=int, default=256)
+    ap.add_argument("--only", choices=("ident", "fib", "lin"), default=None)
     a = ap.parse_args()
     if a.only in (None, "ident"):
         make_ident(a.procs)
     if a.only in (None, "fib"):
         make_fib(a.runs, a.procs, a.work)
+    if a.only in (None, "lin"):
+        make_lin(a.lin_runs, a.procs, a.work)
 
 
 if __name__ == "__main__":

@@ -124,3 +124,34 @@ def test_gpu_c3_device_resident_loop_equals_host_loop():
     np.testing.assert_array_equal(sa["tea"], sb["tea"])
     assert rb[-1]["aborted"] == 0 and ra[-1]["aborted"] == 0
     assert ra[-1]["mean_Te"] > 1.0e3          # FP_calc heats past the clamp, as the reference
+
+
+@pytest.mark.parametrize("mode", [abi.COMTOT_EXACT, abi.COMTOT_TABLE])
+def test_gpu_c3_sed_binned_on_device_equals_oracle_binning(mode):
+    """C3's named output (postprocessing/mrk421_sed.input through pspt.c:245-294):
+    the step's escapes binned on the device straight from the event buffer
+    (c2d_obs_accumulate(ctx, NULL, 0), as bench.py's C3 step does) equal the
+    oracle's binning of the same events downloaded (counts exact, ew sums to
+    atomic order), for the deck's own binning and for a wide window that every
+    event of the golden's first steps falls into (the deck's window opens at
+    t_obs = 1.6e4 s, later than these steps' escapes reach)."""
+    from compton2d_amd import observer
+    gc = case()
+    eng = Engine(gc.grid(comtot_mode=mode, device=0))
+    wide = observer.sed_binning(n_t=4, t_start=0.0, t_end=4.0e5, mu_min=-1.0, mu_max=1.0)
+    eng.transport_step(gc.step_inputs(0))        # step 0 only fills the census
+    for n in (1, 2):
+        eng.transport_step(gc.step_inputs(n))
+        ev = eng.events()
+        assert len(ev) > 100
+        for b in (observer.mrk421_sed_binning(), wide):
+            eng.obs_begin(b)
+            eng.obs_accumulate(None)
+            F, F2, cnt, ms = eng.obs_result()
+            oF, oF2, ocnt = OL.obs_bin(b, ev, "det")
+            np.testing.assert_array_equal(cnt, ocnt)
+            np.testing.assert_allclose(F, oF, rtol=1e-12, atol=0)
+            np.testing.assert_allclose(F2, oF2, rtol=1e-12, atol=0)
+            assert ms > 0
+        assert cnt.sum() > 0.5 * len(ev)       # the wide window holds the step's escapes
+    eng.close()

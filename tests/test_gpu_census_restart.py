@@ -242,7 +242,80 @@ def test_chunked_census_recycles_chunks():
         np.testing.assert_array_equal(i5g[og], i5o[oo])
         chunks, rec, lost, held = eng.last_census_chunks()
         reused.append((rec, lost, chunks))
-    # the census of step n-1 is step n's first items: its chunks come back
+    # the census of step n-1 is step n's first items: its chunks come back,
+    # every one of them (the open-addressed count-down table tracks them all)
     assert any(r > 0 for r, _, _ in reused[1:]), reused
+    assert all(lost == 0 for _, lost, _ in reused), reused
+    for n in range(1, len(reused)):
+        assert reused[n][0] == reused[n - 1][2], reused
     eng.close()
     orc.close()
+
+
+def test_chunked_census_at_capacity_on_few_waves(monkeypatch):
+    """the chunked census's usable capacity is census_capacity.
+    Two workgroups (C2D_BUNDLE_GRID: every wave runs many census chunks) and
+    the additive slack cut to 48 chunks (C2D_CHUNK_SLACK: ~6 per wave, for its
+    partly filled chunk, the chunks whose sources are in flight and its free
+    stack) beside capacity/16: a capacity equal to the census the run needs
+    suffices, no census chunk goes untracked and every input chunk is
+    recycled within its step; records stay the oracle's."""
+    gc = GoldenCase("c3_mrk421")
+    probe = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, census_inplace=1))
+    need = []
+    for n in range(gc.nsteps):
+        probe.transport_step(gc.step_inputs(n))
+        need.append(probe.census_count())
+    probe.close()
+    monkeypatch.setenv("C2D_BUNDLE_GRID", "2")
+    monkeypatch.setenv("C2D_CHUNK_SLACK", "48")
+    eng = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, census_inplace=1, census_capacity=max(need)))
+    orc = OL.Oracle(gc.grid(), OL.RNG_LINEAGE, "det")
+    prev = 0
+    for n in range(gc.nsteps):
+        si = gc.step_inputs(n)
+        eng.transport_step(si)
+        assert orc.step(si) == 0
+        assert eng.census_count() == need[n]
+        chunks, rec, lost, held = eng.last_census_chunks()
+        assert lost == 0 and rec == prev, (n, chunks, rec, lost, held)
+        prev = chunks
+        kg, ko = eng.census()[2], orc.census()[2]
+        np.testing.assert_array_equal(np.sort(kg), np.sort(ko))
+    eng.close()
+    orc.close()
+
+
+def test_chunked_census_lost_after_failed_step():
+    """a chunked step that fails after generation 0 has
+    rewritten the census in place leaves no stale census behind: the count
+    is 0 and census reads and the next step fail with C2D_E_STATE until a
+    census is imported (include/compton2d.h c2d_run_step).  The failure here
+    is a scatter-queue overflow found after generation 0 (ssc_tau collides;
+    queue_capacity 1).  A double-buffered context keeps its census."""
+    from compton2d_amd.engine import C2DError
+    gc = GoldenCase("ssc_tau")
+    for inplace in (1, 0):
+        eng = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, census_inplace=inplace))
+        eng.transport_step(gc.step_inputs(0))
+        d6, i5, keys = eng.census()
+        n0 = eng.census_count()
+        assert n0 > 0
+        eng.close()
+        eng = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT, census_inplace=inplace, queue_capacity=1))
+        eng.import_census(d6, i5, keys)
+        with pytest.raises(C2DError) as e:
+            eng.transport_step(gc.step_inputs(1))
+        assert e.value.code == -5                          # C2D_E_QUEUE_OVERFLOW
+        if inplace:
+            assert eng.census_count() == 0
+            for call in (lambda: eng.census(), lambda: eng.run_step()):
+                with pytest.raises(C2DError) as e:
+                    call()
+                assert e.value.code == -7                  # C2D_E_STATE
+            eng.import_census(d6, i5, keys)                # a new census: the context runs again
+        else:
+            assert eng.census_count() == n0
+            np.testing.assert_array_equal(np.sort(eng.census()[2]), np.sort(keys))
+        assert eng.census_count() == n0
+        eng.close()

@@ -92,3 +92,12 @@ def test_binning_edges():
     assert lc.mode == abi.OBS_LC and lc.n_t == 1024 and lc.n_mu == 1 and lc.n_e == 7
     assert lc.outfiles == ["lc07_ev0.dat"] and lc.dt == 7e2 and lc.t_stop == 7e4
     assert np.array_equal(lc.t1[:-1], lc.t0[1:])
+
+
+def test_mrk421_sed_deck_is_the_reference_deck():
+    """bench.py's C3 step bins its escapes with observer.mrk421_sed_binning():
+    the deck text is the reference's postprocessing/mrk421_sed.input as the
+    golden generator read it (tests/golden/obs.npz deck_sed_mrk421)."""
+    assert observer.MRK421_SED_DECK == str(G["deck_sed_mrk421"])
+    b = observer.mrk421_sed_binning()
+    assert (b.n_t, b.n_mu, b.n_e) == (30, 1, 100) and b.outfiles == ["sed30.dat"]

@@ -77,9 +77,18 @@ def main(root):
         for n, v in sorted(names.items(), key=lambda kv: -sum(kv[1])):
             print("  %-60s n=%4d total=%9.3f ms mean=%8.3f ms" % (n[:60], len(v), sum(v), mean(v)))
         r0 = by[g0[-1]] if g0 else rows[0]
-        print("transport: VGPR=%s SGPR=%s scratch=%s LDS=%s grid=%s wg=%s" % (
-            r0.get("VGPR_Count"), r0.get("SGPR_Count"), r0.get("Scratch_Size"),
-            r0.get("LDS_Block_Size"), r0.get("Grid_Size_X"), r0.get("Workgroup_Size_X")))
+        print("transport launch: grid=%s wg=%s LDS=%s (rocprofv3 fields; its VGPR_Count=%s is a "
+              "granule field, the code object's counts follow)" % (
+            r0.get("Grid_Size_X"), r0.get("Workgroup_Size_X"), r0.get("LDS_Block_Size"),
+            r0.get("VGPR_Count")))
+        try:
+            sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+            import code_object
+            print(code_object.describe(code_object.Path(os.environ.get(
+                "C2D_LIBRARY") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                               "compton2d_amd", "libcompton2d.so")), "bundle_kernel"))
+        except Exception as e:  # the summary stays useful without the code object
+            print("code object registers unavailable: %s" % e)
     for sub in ("fetch", "write", "sq"):
         d = os.path.join(root, sub)
         f = find(d, "kernel_trace.csv")

@@ -23,7 +23,8 @@ def main(path, timed_last=None):
         print("mean of the last %d generation-0 launches (bench timed steps): %.3f ms"
               % (len(sel), mean(sel)))
     r0 = tk[0]
-    print("VGPR=%s SGPR=%s LDS=%s scratch=%s workgroup=%s grid=%s" % (
+    print("rocprofv3 fields (VGPR_Count is granule-encoded; tools/code_object.py prints the code "
+          "object's register counts): VGPR=%s SGPR=%s LDS=%s scratch=%s workgroup=%s grid=%s" % (
         r0["VGPR_Count"], r0["SGPR_Count"], r0["LDS_Block_Size"], r0["Scratch_Size"],
         r0["Workgroup_Size_X"], r0["Grid_Size_X"]))
 
