@@ -32,6 +32,8 @@ CNT_STEPS, CNT_ESCAPES, CNT_CENSUS, CNT_COLLIDE, CNT_KILLED, CNT_SOURCES, \
     CNT_COMPB, CNT_EVENTS, CNT_GENS, CNT_ABORTED = range(10)
 CNT_ESC_SCAT = 11          # escapes of Compton-scattered packets (imctrk2d(1) copies)
 
+FP_EXACT, FP_FAST = 0, 1   # c2d_fp_set_mode
+
 ERRORS = {
     0: "C2D_OK", -1: "C2D_E_ARG", -2: "C2D_E_HIP", -3: "C2D_E_CENSUS_OVERFLOW",
     -4: "C2D_E_EVENT_OVERFLOW", -5: "C2D_E_QUEUE_OVERFLOW", -6: "C2D_E_NOMEM",

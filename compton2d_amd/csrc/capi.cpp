@@ -44,6 +44,8 @@ extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
                                       double* tab, int ncell, hipStream_t s);
 extern "C" int c2d_launch_fp(const FpParams* P, int ncell, int waves, hipStream_t s);
+extern "C" int c2d_launch_fp_fast(const FpParams* dP, int ncell, int block, hipStream_t s);
+extern "C" int c2d_fp_fast_block(int ncell, int n_simd);
 extern "C" int c2d_fp_waves(int ncell, int n_simd);
 extern "C" int c2d_launch_vem(const VemParams* P, int ncell, hipStream_t s);
 extern "C" int c2d_launch_obs(const ObsDev* O, const double* ev, int64_t n, int grid,
@@ -204,6 +206,10 @@ struct c2d_ctx {
   int32_t* fp_err = nullptr;
   unsigned long long* fp_gb_key = nullptr;   /* gamma_bar memo (fp.hip GbMemo) */
   double* fp_gb_val = nullptr;
+  int32_t fp_mode = C2D_FP_EXACT;             /* c2d_fp_set_mode */
+  unsigned long long* fpf_gb_key = nullptr;  /* the fast kernel's own gamma_bar memo */
+  double* fpf_gb_val = nullptr;
+  FpParams* fp_dP = nullptr;                 /* FpParams in device memory (fast kernel) */
   float last_fp_ms = 0.f;
   int last_fp_waves = 0;
   /* emission / absorption tables (c2d_volume_em) */
@@ -484,7 +490,8 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
   for (void* q : vptrs)
     if (q) (void)hipFree(q);
   void* fptrs[] = {c->fp_FT, c->fp_mcd, c->fp_zin, c->fp_fin, c->fp_Pin, c->fp_nf, c->fp_fout, c->fp_Pout,
-                   c->fp_zout, c->fp_err, c->fp_gb_key, c->fp_gb_val};
+                   c->fp_zout, c->fp_err, c->fp_gb_key, c->fp_gb_val, c->fpf_gb_key, c->fpf_gb_val,
+                   c->fp_dP};
   for (void* p : fptrs)
     if (p) (void)hipFree(p);
   c->pk.release();
@@ -1845,7 +1852,12 @@ static int ensure_mcd(c2d_ctx* c) {
     HIPCHK(c, dalloc(&c->fp_gb_val, C2D_FP_MEMO_SLOTS));
     HIPCHK(c, hipMemset(c->fp_gb_key, 0, sizeof(unsigned long long) * C2D_FP_MEMO_SLOTS));
     HIPCHK(c, hipMemset(c->fp_gb_val, 0, sizeof(double) * C2D_FP_MEMO_SLOTS));
+    HIPCHK(c, dalloc(&c->fpf_gb_key, C2D_FP_MEMO_SLOTS));
+    HIPCHK(c, dalloc(&c->fpf_gb_val, C2D_FP_MEMO_SLOTS));
+    HIPCHK(c, hipMemset(c->fpf_gb_key, 0, sizeof(unsigned long long) * C2D_FP_MEMO_SLOTS));
+    HIPCHK(c, hipMemset(c->fpf_gb_val, 0, sizeof(double) * C2D_FP_MEMO_SLOTS));
   }
+  HIPCHK(c, dalloc(&c->fp_dP, 1));
   return C2D_OK;
 }
 
@@ -1878,6 +1890,14 @@ extern "C" int c2d_fp_set_config(c2d_ctx* c, const c2d_fp_config* fc) {
   c->fpc = *fc;
   c->fpc.F_IC = nullptr;
   c->fp_ready = true;
+  return C2D_OK;
+}
+
+extern "C" int c2d_fp_set_mode(c2d_ctx* c, int32_t mode) {
+  if (!c) return C2D_E_ARG;
+  if (mode != C2D_FP_EXACT && mode != C2D_FP_FAST)
+    return fail(c, C2D_E_ARG, "c2d_fp_set_mode: mode %d is neither C2D_FP_EXACT nor C2D_FP_FAST", mode);
+  c->fp_mode = mode;
   return C2D_OK;
 }
 
@@ -1971,8 +1991,17 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   P.zout = c->fp_zout; P.err = c->fp_err;
   P.gb_key = c->fp_gb_key; P.gb_val = c->fp_gb_val; P.gb_mask = C2D_FP_MEMO_SLOTS - 1u;
   HIPCHK(c, hipEventRecord(c->ev_g0a, st));
-  c->last_fp_waves = c2d_fp_waves(nc, 4 * c->n_cu);
-  int rc = c2d_launch_fp(&P, nc, c->last_fp_waves, st);
+  int rc;
+  if (c->fp_mode == C2D_FP_FAST) {
+    P.gb_key = c->fpf_gb_key; P.gb_val = c->fpf_gb_val;
+    HIPCHK(c, hipMemcpyAsync(c->fp_dP, &P, sizeof P, hipMemcpyHostToDevice, st));
+    const int bs = c2d_fp_fast_block(nc, 4 * c->n_cu);
+    c->last_fp_waves = bs / 64;
+    rc = c2d_launch_fp_fast(c->fp_dP, nc, bs, st);
+  } else {
+    c->last_fp_waves = c2d_fp_waves(nc, 4 * c->n_cu);
+    rc = c2d_launch_fp(&P, nc, c->last_fp_waves, st);
+  }
   if (rc) return fail(c, C2D_E_HIP, "fp launch: %s", hipGetErrorString((hipError_t)rc));
   HIPCHK(c, hipEventRecord(c->ev_g0b, st));
   std::vector<double> zout((size_t)nc * FO_N), fout(nnt), pout(nnt);

@@ -1,0 +1,713 @@
+/*
+ * fp_fast.hip — the Fokker-Planck electron update (FP_calc,
+ * src/update2d.f:337-1739) as a block-parallel kernel: C2D_FP_FAST.
+ *
+ * fp.hip's c2d_fp_kernel reproduces FP_calc bit for bit, so every sum,
+ * the Thomas solve (tridag, update2d.f:2476-2518) and McDonald's series
+ * (volume2d.f:598-626) run in the reference's order: one in-order latency
+ * chain per zone per implicit sub-step.  Off the tea clamp a zone takes
+ * thousands of sub-steps and the update is that chain's length.
+ * This kernel keeps the same arithmetic per bin and per series term and
+ * changes only the ORDER of the additions and the tridiagonal algorithm, so
+ * its results differ from the exact kernel's by rounding (the stated
+ * tolerance, DESIGN §4b and tests/test_gpu_fp.py):
+ *   - one zone per workgroup of BS threads (BS/64 waves); thread t owns
+ *     energy bin t+1 for every element-wise stage;
+ *   - the reference's sequential sums are block reductions (wave butterfly,
+ *     then the waves' partials in wave order: every thread gets the same
+ *     bits, so all scalar control flow stays uniform across the block);
+ *   - the cumulative Pnt is a block inclusive scan;
+ *   - the 200-row Chang-Cooper system is solved by parallel cyclic reduction
+ *     (8 levels, one row per thread, double-buffered in LDS, one barrier per
+ *     level) instead of the Thomas recurrence;
+ *   - McDonald's K2/K3 terms are evaluated BS at a time; each series' first
+ *     stopping term is found by a block minimum, so the terms added are
+ *     exactly the reference's (same stopping index); their sum is a tree.
+ *     exp(-y) multiplies instead of exp(y) dividing (one exp, no divide);
+ *   - gamma_bar keeps the exact kernel's memos (4 entries per zone, and a
+ *     table shared by all zones and steps -- a separate one, since the
+ *     values differ from the exact kernel's in the last bits).
+ * The temperature search walks the same lattice Theta*1.005^k and stops at
+ * the same crossing unless gbar and gamma_bar agree to within rounding.
+ * Line numbers: src/update2d.f unless stated.
+ */
+#include <hip/hip_runtime.h>
+#include <limits.h>
+#include <stdint.h>
+
+#include "c2d_device.hpp"
+#include "c2d_math.h"
+#include "c2d_wave.hpp"
+
+namespace c2d {
+namespace {
+
+using namespace wave;
+constexpr int NT = C2D_NUM_NT;
+constexpr int NPH = C2D_NPHFIELD;
+constexpr double PI_REF = 3.1415926536;       /* general.pa:24 */
+constexpr double C_LIGHT = 2.9979245620e10;   /* general.pa:25 */
+constexpr double LNL = 20.0;                  /* update2d.f:143 */
+constexpr int MAX_FP_STEPS = 1000000;         /* update2d.f:585-599 */
+constexpr int WMAXF = 8;                      /* waves per zone at most (BS = 512) */
+
+/* zone state in LDS (namespace scope: ds_* accesses) */
+__shared__ double f_gnt[NT + 2], f_gam[NT + 2], f_fold[NT + 2], f_fnew[NT + 2];
+__shared__ double f_dgic[NT + 2], f_dgdt[NT + 2], f_disp[NT + 2], f_inj[NT + 2];
+__shared__ double f_bigW[NT + 2], f_bigC[NT + 2], f_em[NT + 2], f_Pnt[NT + 2], f_nf[NPH];
+__shared__ double f_pcr[2][4][256];          /* PCR rows a, b, c, d (double-buffered) */
+__shared__ double f_red[2][2][WMAXF];        /* block reductions: [slot][value][wave] */
+__shared__ int f_ired[2][2][WMAXF];          /* block integer min/max                 */
+__shared__ double f_eg[2];                   /* exp(gammln(2.5)), exp(gammln(3.5))    */
+
+/* one block of BS threads; `slot` alternates so each reduction needs one barrier */
+template <int BS>
+struct Blk {
+  static constexpr int W = BS / FPB;
+  int tid, lane, wave;
+  int slot = 0, islot = 0;
+
+  __device__ __forceinline__ static double wsum(double v) {
+#pragma unroll
+    for (int o = FPB / 2; o > 0; o >>= 1) v = v + __shfl_xor(v, o, FPB);
+    return v;
+  }
+  /* two sums at once; identical bits in every thread */
+  __device__ __forceinline__ void sum2(double& a, double& b) {
+    a = wsum(a);
+    b = wsum(b);
+    if (lane == 0) {
+      f_red[slot][0][wave] = a;
+      f_red[slot][1][wave] = b;
+    }
+    __syncthreads();
+    double x = 0.0, y = 0.0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      x = x + f_red[slot][0][w];
+      y = y + f_red[slot][1][w];
+    }
+    a = x;
+    b = y;
+    slot ^= 1;
+  }
+  __device__ __forceinline__ double sum(double a) {
+    double b = 0.0;
+    sum2(a, b);
+    return a;
+  }
+  /* block minimum and maximum of two ints (same in every thread) */
+  __device__ __forceinline__ void minmax(int& mn, int& mx) {
+#pragma unroll
+    for (int o = FPB / 2; o > 0; o >>= 1) {
+      const int a = __shfl_xor(mn, o, FPB), b = __shfl_xor(mx, o, FPB);
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+    }
+    if (lane == 0) {
+      f_ired[islot][0][wave] = mn;
+      f_ired[islot][1][wave] = mx;
+    }
+    __syncthreads();
+    mn = INT_MAX;
+    mx = INT_MIN;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      mn = f_ired[islot][0][w] < mn ? f_ired[islot][0][w] : mn;
+      mx = f_ired[islot][1][w] > mx ? f_ired[islot][1][w] : mx;
+    }
+    islot ^= 1;
+  }
+  /* block minima of two ints */
+  __device__ __forceinline__ void min2(int& a, int& b) {
+#pragma unroll
+    for (int o = FPB / 2; o > 0; o >>= 1) {
+      const int x = __shfl_xor(a, o, FPB), y = __shfl_xor(b, o, FPB);
+      a = x < a ? x : a;
+      b = y < b ? y : b;
+    }
+    if (lane == 0) {
+      f_ired[islot][0][wave] = a;
+      f_ired[islot][1][wave] = b;
+    }
+    __syncthreads();
+    a = INT_MAX;
+    b = INT_MAX;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      a = f_ired[islot][0][w] < a ? f_ired[islot][0][w] : a;
+      b = f_ired[islot][1][w] < b ? f_ired[islot][1][w] : b;
+    }
+    islot ^= 1;
+  }
+  /* inclusive prefix sum of v over the threads in tid order, and the total */
+  __device__ __forceinline__ double scan(double v, double& total) {
+#pragma unroll
+    for (int o = 1; o < FPB; o <<= 1) {
+      const double u = __shfl_up(v, o, FPB);
+      if (lane >= o) v = v + u;
+    }
+    if (lane == FPB - 1) f_red[slot][0][wave] = v;
+    __syncthreads();
+    double before = 0.0, all = 0.0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const double x = f_red[slot][0][w];
+      if (w < wave) before = before + x;
+      all = all + x;
+    }
+    slot ^= 1;
+    total = all;
+    return before + v;
+  }
+};
+
+/* gamma_bar memo shared by every zone and step (the fast kernel's own
+ * table: see fp.hip GbMemo for the protocol) */
+constexpr int GB_PROBES = 8;
+__device__ __forceinline__ uint32_t gb_hash(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  return (uint32_t)k;
+}
+__device__ __forceinline__ bool gb_lookup(const FpParams& P, double th, double& g) {
+  if (!P.gb_key) return false;
+  const unsigned long long k = c2d_bits(th);
+  uint32_t h = gb_hash(k) & P.gb_mask;
+  for (int i = 0; i < GB_PROBES; i++) {
+    const unsigned long long kk = __hip_atomic_load(P.gb_key + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (kk == k) {
+      const double v = __hip_atomic_load(P.gb_val + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v != 0.0) { g = v; return true; }
+      return false;
+    }
+    if (kk == 0ull) return false;
+    h = (h + 1u) & P.gb_mask;
+  }
+  return false;
+}
+__device__ __forceinline__ void gb_insert(const FpParams& P, double th, double g) {
+  if (!P.gb_key) return;
+  const unsigned long long k = c2d_bits(th);
+  uint32_t h = gb_hash(k) & P.gb_mask;
+  for (int i = 0; i < GB_PROBES; i++) {
+    const unsigned long long prev = atomicCAS(P.gb_key + h, 0ull, k);
+    if (prev == 0ull) {
+      __hip_atomic_store(P.gb_val + h, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (prev == k) return;
+    h = (h + 1u) & P.gb_mask;
+  }
+}
+
+/* McDonald K2, K3 (volume2d.f:598-626) by the whole block: terms n0 + tid of
+ * each pass, the first stopping term of each series by a block minimum (so
+ * exactly the reference's terms enter), per-thread partial sums, one tree
+ * sum at the end.  Beyond the abscissa table wave 0 finishes the series with
+ * c2d_wave's replayed chain (never reached on the reference's decks). */
+template <int BS>
+__device__ void mcdonald23_fast(Blk<BS>& B, double z, const double* __restrict__ tab, double& K2, double& K3,
+                                long long& guard) {
+  const double dt = 1.001, d = dt - 1.0, sm = 5.0e-1 * (1.0 + dt);
+  /* past the table (never reached on the reference's decks) the abscissae
+   * continue from the table's last t by a power of dt instead of the
+   * reference's repeated product: the same values to rounding */
+  const double t_last = tab[(size_t)(C2D_FP_MCD_N - 1) * 4], ldt = c2d_log(dt);
+  double s2 = 0.0, s3 = 0.0;
+  bool run2 = true, run3 = true;
+  for (int n0 = 0;; n0 += BS) {
+    const int n = n0 + B.tid;
+    double t, ts, p2, p3;
+    if (n < C2D_FP_MCD_N) {
+      const double4 e = *(const double4*)(tab + (size_t)n * 4);
+      t = e.x; ts = e.y; p2 = e.z; p3 = e.w;
+    } else {
+      t = t_last * c2d_exp_bf((double)(n - C2D_FP_MCD_N + 1) * ldt);
+      ts = t * sm;
+      const double q = ts * ts - 1.0, rq = __builtin_sqrt(q);
+      p2 = q * rq;
+      p3 = q * q * rq;
+    }
+    const double y = z * ts;
+    double sd2 = 0.0, sd3 = 0.0;
+    if (y < 2.25e2) {
+      const double em = c2d_exp_bf(-y);
+      sd2 = p2 * em;
+      sd3 = p3 * em;
+    }
+    const double tn = t * dt;
+    const bool st2 = !(tn < 2.0 || sd2 > 1.0e-8), st3 = !(tn < 2.0 || sd3 > 1.0e-8);
+    /* first stopping term of each series in this pass */
+    int stop2 = st2 ? n : INT_MAX, stop3 = st3 ? n : INT_MAX;
+    B.min2(stop2, stop3);
+    if (run2 && n <= stop2) s2 = s2 + d * t * sd2;
+    if (run3 && n <= stop3) s3 = s3 + d * t * sd3;
+    if (stop2 != INT_MAX) run2 = false;
+    if (stop3 != INT_MAX) run3 = false;
+    guard += BS;
+    if (!run2 && !run3) break;
+    if (guard > GUARD_MAX) break;
+  }
+  B.sum2(s2, s3);
+  mcdonald23_finish_c(z, s2, s3, f_eg[0], f_eg[1], K2, K3);
+}
+
+template <int BS>
+__device__ double gamma_bar_fast(Blk<BS>& B, double Theta, const double* tab, long long& guard) {
+  double g;
+  if (Theta < F32(0.2)) {
+    g = (1. + F32(4.375) * Theta + F32(7.383) * (Theta * Theta) + F32(3.384) * (Theta * Theta * Theta)) /
+            (1. + F32(1.875) * Theta + F32(.8203) * (Theta * Theta)) -
+        Theta;
+  } else {
+    double K2, K3;
+    mcdonald23_fast<BS>(B, 1.0 / Theta, tab, K2, K3, guard);
+    g = K3 / K2 - Theta;
+  }
+  if (g < 1.0) g = 1.0;
+  return g;
+}
+
+/* PCR on rows 1..NT (row i in thread i-1): a x_{i-1} + b x_i + c x_{i+1} = d.
+ * Rows outside 1..NT act as the identity (a = c = d = 0, b = 1). */
+template <int BS>
+__device__ double pcr_solve(Blk<BS>& B, double a, double b, double c, double dd) {
+  const int i = B.tid + 1;
+  const bool own = i <= NT;
+  int buf = 0;
+  for (int s = 1; s < NT; s <<= 1) {
+    if (own) {
+      f_pcr[buf][0][i] = a;
+      f_pcr[buf][1][i] = b;
+      f_pcr[buf][2][i] = c;
+      f_pcr[buf][3][i] = dd;
+    }
+    __syncthreads();
+    if (own) {
+      double am = 0.0, bm = 1.0, cm = 0.0, dm = 0.0, ap = 0.0, bp = 1.0, cp = 0.0, dp = 0.0;
+      if (i - s >= 1) {
+        am = f_pcr[buf][0][i - s]; bm = f_pcr[buf][1][i - s];
+        cm = f_pcr[buf][2][i - s]; dm = f_pcr[buf][3][i - s];
+      }
+      if (i + s <= NT) {
+        ap = f_pcr[buf][0][i + s]; bp = f_pcr[buf][1][i + s];
+        cp = f_pcr[buf][2][i + s]; dp = f_pcr[buf][3][i + s];
+      }
+      const double k1 = a / bm, k2 = c / bp;
+      const double na = -am * k1, nc = -cp * k2;
+      const double nb = b - cm * k1 - ap * k2;
+      const double nd = dd - dm * k1 - dp * k2;
+      a = na; b = nb; c = nc; dd = nd;
+    }
+    buf ^= 1;
+  }
+  return own ? dd / b : 0.0;
+}
+
+/* FP_calc of one zone (blockIdx.x) by the whole block */
+template <int BS>
+__device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
+  const int tid = B.tid;
+  const int cell = blockIdx.x;
+  const int j = cell / P.nr + 1, k = cell % P.nr + 1;
+  const Geo* G = P.geo;
+  const double* zin = P.zin + (size_t)cell * FZ_N;
+  double* zo = P.zout + (size_t)cell * FO_N;
+  long long guard = 0;
+  const int i = tid + 1;                   /* this thread's energy bin */
+  const bool own = i <= NT;
+
+  const double volume = zin[FZ_VOL], tea = zin[FZ_TEA], tna = zin[FZ_TNA];
+  const double Bf = zin[FZ_B], Eloss_sy = zin[FZ_ELSY], f_pair = zin[FZ_FPAIR];
+  const double ecens = P.ecens ? P.ecens[cell] : zin[FZ_ECENS];
+  const double zmax = G->z[P.nz], rmax = G->r[P.nr];
+  const double t_esc = P.r_esc * zmax / C_LIGHT;   /* :460-461 */
+  const double t_acc = P.r_acc * zmax / C_LIGHT;
+  double Te_new = tea;
+  double n_p = zin[FZ_NE];
+  double ne = n_p * (1. + f_pair);
+  double n_positron = n_p * f_pair;
+  double n_lept = ne + n_positron;
+  if (n_lept < 1.0e-11) {                           /* :478 */
+    if (tid == 0) {
+      zo[FO_TE] = Te_new;
+      for (int q = 0; q < C2D_FP_NDIAG; q++) zo[FO_DIAG + q] = 0.0;
+      zo[FO_DIAG + C2D_FP_SKIPPED] = 1.0;
+    }
+    return;
+  }
+  if (own) {
+    f_gnt[i] = P.gnt[i - 1];
+    f_gam[i] = P.gnt[i - 1] + 1.0;
+    f_fold[i] = P.f_in[(size_t)cell * NT + i - 1];
+    f_Pnt[i] = P.P_in[(size_t)cell * NT + i - 1];
+  }
+  for (int q = tid; q < NPH; q += BS) f_nf[q] = P.nf[(size_t)cell * NPH + q];
+  __syncthreads();
+  /* this thread's bin widths (used by most sums) */
+  const double dgp = (i <= NT - 1) ? f_gnt[i + 1] - f_gnt[i] : 0.0;    /* gnt(i+1)-gnt(i) */
+  const double dgm = (i >= 2 && own) ? f_gnt[i] - f_gnt[i - 1] : 0.0;  /* gnt(i)-gnt(i-1) */
+  const double gi = own ? f_gam[i] : 0.0;
+
+  /* E_el, normalisation (:482-509) */
+  double E_el = B.sum((i >= 2 && own) ? dgm * gi * f_fold[i] : 0.0);
+  double E_pos = 0.0;
+  E_el = E_el * ne * 8.176e-7 * volume;
+  double e_old = 0.0 + E_el + E_pos + zin[FZ_ECOLD];
+  double e_new = 0.0 + ecens;
+  double sum_p = B.sum((i <= NT - 1) ? dgp * f_fold[i] : 0.0);
+  if (own) f_fold[i] = (i == NT) ? 0.0 : f_fold[i] / sum_p;
+
+  /* flare (:532-562) */
+  const double rmid = 5.0e-1 * (G->r[k] + G->r[k - 1]);
+  const double zmid = 5.0e-1 * (G->z[j] + G->z[j - 1]);
+  double tl_flare = 0.0;
+  if (P.cf_sentinel == 1) {
+    const double ar = (rmid - P.r_flare) / P.sigma_r;
+    const double az = (zmid - P.z_flare) / P.sigma_z;
+    const double at = (P.time - P.t_flare) / P.sigma_t;
+    const double y = 5.0e-1 * (ar * ar + az * az + at * at);
+    tl_flare = (y < 1.0e2) ? P.flare_amp / c2d_exp_bf(y) : 0.0;
+  }
+  const double tlev = zin[FZ_TURB] + tl_flare;
+  const double Tp_flare = tna * (1.0 + tl_flare);
+  const double Th_p = Tp_flare / 9.382e5;
+  double Th_e = tea / 5.11e2;
+  const double f_th = 1.5 * volume * n_lept;
+  /* dg_ic(i) = -sum_ph n_field(ph) F_IC(i,ph) / volume (:568-574) */
+  if (i <= NT - 1) {
+    double s = 0.0;
+    const double* ft = P.FT + (i - 1);
+    for (int ph = 0; ph < NPH; ph++) s = s - f_nf[ph] * ft[(size_t)ph * NT] / volume;
+    f_dgic[i] = s;
+  }
+  if (i == NT) f_dgic[NT] = 0.0;     /* hazard H10 */
+  const double dz = G->z[j] - G->z[j - 1];          /* :628-632 */
+  __syncthreads();
+
+  double hr = 0.0, hr_st = 0.0, sum_E = 0.0, t_fp = 0.0;
+  int fp_steps = 0;
+  double g_av_next = 0.0, hr_th_c_next = 0.0;
+  double memo_th[4] = {-1.0, -1.0, -1.0, -1.0}, memo_g[4] = {0.0, 0.0, 0.0, 0.0};
+  int memo_next = 0;
+  auto gamma_bar_m = [&](double th) -> double {
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (memo_th[q] == th) return memo_g[q];
+    double g = 0.0;
+    /* the global memo, read by thread 0 and broadcast, so every thread takes the same branch */
+    if (tid == 0) {
+      double gm = 0.0;
+      f_red[B.slot][0][0] = gb_lookup(P, th, gm) ? gm : 0.0;
+    }
+    __syncthreads();
+    g = f_red[B.slot][0][0];
+    B.slot ^= 1;
+    if (g == 0.0) {
+      g = gamma_bar_fast<BS>(B, th, P.mcd, guard);
+      if (tid == 0) gb_insert(P, th, g);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (q == memo_next) { memo_th[q] = th; memo_g[q] = g; }
+    memo_next = (memo_next + 1) & 3;
+    return g;
+  };
+  const double vn = 8.176e-7;
+  for (;;) {
+    /* label 200 (:577) */
+    const double g_av0 = (fp_steps == 0) ? gamma_bar_m(Th_e) : g_av_next;
+    double g_av = g_av0;
+    const double hr_th_c = (fp_steps == 0)
+        ? B.sum((i <= NT - 1) ? -(vn * f_dgic[i] * f_fold[i] * dgp * volume * n_lept) : 0.0)
+        : hr_th_c_next;
+    if (fp_steps > MAX_FP_STEPS) {
+      if (tid == 0) atomicOr(P.err, FPERR_STEPS);
+      return;
+    }
+    const double gamma_R = 2.1e-3 * __builtin_sqrt(n_lept) / (Bf * __builtin_sqrt(g_av));
+    const double sT = Th_e + Th_p;
+    const double h_T = F32(.79788) * (2. * (sT * sT) + 2.0 * sT + 1.0) /
+                       (c2d_pow(sT, 1.5) * (1.0 + 1.875 * Th_e + .8203 * (Th_e * Th_e)));
+    const double hr_th_Coul = f_th * 1.7386e-26 * n_p * LNL * h_T * (Tp_flare - Te_new);
+    const double yR = gamma_R / g_av;
+    const double hr_th_sy = (yR < 100.0) ? -Eloss_sy / (P.dt * c2d_exp_bf(yR)) : 0.0;
+    double hr_th_A = tlev * hr_th_Coul;
+    if (hr_th_A < 1.0e-20) hr_th_A = 1.0e-20;
+    const double hr_th_total = hr_th_sy + hr_th_c + hr_th_A;
+    const double dT_total = 6.25e8 * P.dt * hr_th_total / f_th;
+    double f_t_implicit = P.df_implicit * Te_new / fabs(dT_total);
+    if (f_t_implicit > P.df_T) f_t_implicit = P.df_T;
+    const double f_sy = 1.058e-15 * (Bf * Bf) / 8.176e-7;
+    const double g_thr = 1.0 + 4.0 * Th_e;
+    /* dgdt, disp (:880-889, :1035-1049) */
+    if (own) {
+      const double y = gamma_R / gi;
+      const double dg_sy = (y < 100.0) ? -(f_sy * (gi * gi - 1.0) / c2d_exp_bf(y)) : -1.0e-50;
+      const double dg_A = gi / t_acc;
+      f_disp[i] = gi * gi / t_acc / 2.0;
+      f_dgdt[i] = dg_sy + f_dgic[i] + dg_A;
+    }
+    /* loop 350 sums */
+    double hr_nt_A = 0.0, hr_st_A = 0.0;
+    if (i <= NT - 1) {
+      const double v = gi / t_acc * f_fold[i] * (f_gam[i + 1] - gi);
+      hr_nt_A = v;
+      hr_st_A = gi > g_thr ? v : 0.0;
+    }
+    B.sum2(hr_nt_A, hr_st_A);                          /* also publishes dgdt/disp */
+    hr_st_A = hr_st_A * vn * n_lept * volume;
+    hr_nt_A = hr_nt_A * vn * n_lept * volume;
+    const double heat_total = hr_th_Coul + hr_nt_A;
+    e_old = e_old + heat_total * f_t_implicit * P.dt;
+    if (fp_steps == 0) {
+      hr = hr + heat_total;
+      hr_st = hr_st + hr_st_A;
+    }
+    double d_t = f_t_implicit * P.dt;                  /* :1142-1146 */
+    if (d_t > (P.dt - t_fp)) d_t = 1.00001 * (P.dt - t_fp);
+    if (P.pair_sw == 1 && i <= NT - 1) {               /* H6: inert positrons, loop 460 clip */
+      double v = f_fold[i] + 0.0 / ne;
+      if (v < 1.0e-50) v = 0.0;
+      f_fold[i] = v;
+    }
+    n_positron = 0.0;                                  /* :1164-1167 / :1218 */
+    ne = n_p + n_positron;
+    /* injection (:1226-1306) */
+    double n_inject = 0.0;
+    if (P.pick_sw == 1) {
+      double sv = 0.0;
+      if (i <= NT - 1) {
+        const double x = gi - P.inj_gg;
+        const double v = 1.0e2 * c2d_exp_bf(-((x * x) / 2.0 / (P.inj_sigma * P.inj_sigma))) /
+                         (P.inj_sigma * __builtin_sqrt(2.0 * PI_REF));
+        f_inj[i] = v;
+        sv = v * dgp;
+      }
+      const double inj_sum = B.sum(sv);
+      const double inj_rho = P.pick_rate * d_t;
+      double nv = 0.0;
+      if (i <= NT - 1) {
+        const double v = inj_rho * f_inj[i] / inj_sum;
+        f_fold[i] = f_fold[i] + v / ne;
+        nv = v * dgp;
+      }
+      n_inject = n_inject + B.sum(nv);
+    }
+    if (P.inj_switch != 0) {
+      const double tt = P.time + t_fp - P.inj_t;
+      if (tt > dz / P.inj_v * (double)(j - 1) && tt < dz / P.inj_v * (double)j && k <= P.nr) {
+        double v = 0.0;
+        if (i <= NT - 1) {
+          if (P.inj_dis == 1) {
+            const double x = gi - P.inj_gg;
+            v = 1.0e2 * c2d_exp_bf(-((x * x) / 2.0 / (P.inj_sigma * P.inj_sigma))) /
+                (P.inj_sigma * __builtin_sqrt(2.0 * PI_REF));
+          } else {
+            const double inj_g2var = P.inj_g2 * c2d_pow(10.0, (P.time + t_fp - P.inj_t) * P.inj_v / zmax);
+            if (gi > P.inj_g1) {
+              const double inj_y = (P.g2var_switch == 1) ? gi / inj_g2var : gi / P.inj_g2;
+              v = (inj_y < 1.0e2) ? 1.0e2 / (c2d_pow(gi, P.inj_p) * c2d_exp_bf(inj_y)) : 0.0;
+            }
+          }
+        }
+        double isum = v * dgp, inj_E = v * dgp * gi;
+        B.sum2(isum, inj_E);
+        inj_E = inj_E / isum;
+        const double inj_rate = P.inj_L / 8.186e-7 / inj_E / (PI_REF * (rmax * rmax) * dz);
+        const double rho = inj_rate * d_t;
+        double nv = 0.0;
+        if (i <= NT - 1) {
+          const double w = rho * v / isum;
+          f_fold[i] = f_fold[i] + w / ne;
+          nv = w * dgp;
+        }
+        n_inject = n_inject + B.sum(nv);
+      }
+    }
+    ne = ne + n_inject;
+    n_p = n_p + n_inject;
+    n_lept = n_lept + n_inject;
+    ne = ne * t_esc / (t_esc + d_t);                  /* escape (:1309-1313) */
+    n_p = n_p * t_esc / (t_esc + d_t);
+    n_lept = n_lept * t_esc / (t_esc + d_t);
+    /* Chang-Cooper coefficients (:1363-1390) */
+    if (i <= NT - 1) {
+      double bigB, Dg;
+      if (i == 1) {
+        bigB = -(f_dgdt[1] + f_dgdt[2]);
+        Dg = f_gnt[2] - f_gnt[1];
+      } else {
+        bigB = -(f_dgdt[i] + f_dgdt[i + 1]) / 2.0;
+        Dg = dgp;
+      }
+      const double bigC = (f_disp[i] + f_disp[i + 1]) / 2.0;
+      const double smw = Dg * bigB / bigC;
+      f_bigW[i] = smw / (c2d_exp_bf(smw) - 1.0);
+      f_em[i] = bigC * smw / (1.0 - c2d_exp_bf(-smw));
+      f_bigC[i] = bigC;
+    }
+    __syncthreads();
+    double ta = 0.0, tb = 1.0, tc = 0.0;
+    if (i >= 2 && i <= NT - 1) {
+      const double D_gminus = dgm, D_gplus = dgp;
+      const double Delta_g = __builtin_sqrt(f_gnt[i] / f_gnt[i - 1]) * D_gminus;
+      tc = -d_t * (f_em[i] / Delta_g / D_gplus);
+      tb = 1.0 + d_t / Delta_g * (f_bigC[i] * f_bigW[i] / D_gplus + f_em[i - 1] / D_gminus) + d_t / t_esc;
+      ta = -d_t / Delta_g * f_bigC[i - 1] * f_bigW[i - 1] / D_gminus;
+    }
+    /* tridag (:2476-2518) by cyclic reduction; clip u(2..num_nt) (:2512) */
+    double u = pcr_solve<BS>(B, ta, tb, tc, own ? f_fold[i] : 0.0);
+    if (i >= 2 && u < 0.0) u = 0.0;
+    if (i == NT || i == 1) u = 0.0;
+    /* Pnt prefix, sum_p, sum_E (:1415-1419) */
+    double tot = 0.0;
+    const double pv = (i <= NT - 1) ? dgp * u : 0.0;
+    const double pref = B.scan(pv, tot);
+    sum_p = tot;
+    const double sE = B.sum((i <= NT - 1) ? dgp * gi * u : 0.0);
+    if (i <= NT - 1) f_Pnt[i] = pref;
+    sum_E = sE / sum_p;
+    t_fp = t_fp + d_t;
+    fp_steps = fp_steps + 1;
+    const double fn = own ? u / sum_p : 0.0;
+    if (own) {
+      f_fnew[i] = fn;
+      f_fold[i] = fn;
+    }
+    /* gbar and the next sub-step's hr_th_c (:1440, label 200) */
+    double gbar = (i <= NT - 1) ? gi * fn * dgp : 0.0;
+    hr_th_c_next = (i <= NT - 1) ? -(vn * f_dgic[i] * fn * dgp * volume * n_lept) : 0.0;
+    B.sum2(gbar, hr_th_c_next);
+    /* new temperature (:1440-1468) */
+    double The_new = Th_e;
+    if (gbar > g_av) {
+      while (gbar > g_av) {
+        The_new = The_new * F32(1.005);
+        g_av = gamma_bar_m(The_new);
+        if (guard > GUARD_MAX) break;
+      }
+    } else {
+      while (gbar < g_av) {
+        The_new = The_new / F32(1.005);
+        g_av = gamma_bar_m(The_new);
+        if (The_new < 1.0e-2) break;
+        if (guard > GUARD_MAX) break;
+      }
+    }
+    if (guard > GUARD_MAX) {
+      if (tid == 0) atomicOr(P.err, FPERR_GUARD);
+      return;
+    }
+    Te_new = 5.11e2 * The_new;
+    Th_e = The_new;
+    g_av_next = g_av;
+    if (!(t_fp < P.dt)) break;                         /* :1473 */
+  }
+  __syncthreads();
+
+  /* outputs (:1481-1500) */
+  const double fo = own ? f_fnew[i] : 0.0;
+  E_el = B.sum((i >= 2 && own) ? fo * gi * dgm : 0.0);
+  E_pos = 0.0;
+  E_el = E_el * ne * 8.176e-7 * volume;
+  e_new = e_new + E_el + E_pos;
+  if (own) {
+    P.f_out[(size_t)cell * NT + i - 1] = fo;
+    P.P_out[(size_t)cell * NT + i - 1] = f_Pnt[i] / sum_p;
+  }
+  /* nonthermal parameters (:1654-1736) */
+  int lo = (own && i >= 5 && i <= NT - 5 && fo > 1.0e-10) ? i : INT_MAX;
+  int hi = (own && i >= 5 && i <= NT - 5 && fo > 1.0e-15) ? i : INT_MIN;
+  B.minmax(lo, hi);
+  const int i_nt = lo == INT_MAX ? NT - 4 : lo;
+  const int i_mx = hi == INT_MIN ? 4 : hi;
+  const double gmin = f_gam[i_nt];
+  const double gmax = f_gam[i_mx];
+  const double dfn = (i <= NT - 1) ? (f_gam[i + 1] - gi) * fo : 0.0;
+  double sum_th = (i <= i_nt - 1) ? dfn : 0.0, sum_nt = (i >= i_nt && i <= NT - 1) ? dfn : 0.0;
+  B.sum2(sum_th, sum_nt);
+  double amxwl = sum_th / (sum_nt + sum_th);
+  double p_nth = zin[FZ_PNTH];
+  if (amxwl > 9.999e-1) {
+    amxwl = 1.0;
+  } else {
+    p_nth = F32(0.1);
+    double sum_g = 1.0e50, sumg_old;
+    /* first bin with gamma/gmax >= 100 ends the fit sum (:1707-1717) */
+    int e0 = (i >= i_nt && i <= NT - 2 && !(gi / gmax < 100.0)) ? i : INT_MAX, e1 = INT_MIN;
+    B.minmax(e0, e1);
+    const int i_end = e0 == INT_MAX ? NT - 1 : e0;
+    for (;;) {
+      sumg_old = sum_g;
+      const double p_1 = 1.0 - p_nth;
+      double N_nt;
+      if (fabs(p_1) > 1.0e-4)
+        N_nt = (1. - amxwl) * p_1 / (c2d_pow(gmax, p_1) - c2d_pow(gmin, p_1));
+      else
+        N_nt = (1.0 - amxwl) / c2d_log(gmax / gmin);
+      double v1 = 0.0, v2 = 0.0;
+      if (i >= i_nt && i < i_end) {
+        const double f_pl = N_nt / (c2d_pow(gi, p_nth) * c2d_exp_bf(gi / gmax));
+        v1 = f_pl * gi * dgp;
+        v2 = f_pl * dgp;
+      }
+      B.sum2(v1, v2);
+      sum_g = v1 / v2;
+      sum_g = fabs(sum_g - sum_E);
+      if (sum_g < sumg_old && p_nth < 10.) {
+        p_nth = p_nth + 0.5e-1;
+        continue;
+      }
+      break;
+    }
+  }
+  if (tid == 0) {
+    zo[FO_TE] = Te_new;
+    zo[FO_NE] = n_p;
+    zo[FO_GMIN] = gmin;
+    zo[FO_GMAX] = gmax;
+    zo[FO_AMXWL] = amxwl;
+    zo[FO_PNTH] = p_nth;
+    zo[FO_DIAG + C2D_FP_E_OLD] = e_old;
+    zo[FO_DIAG + C2D_FP_E_NEW] = e_new;
+    zo[FO_DIAG + C2D_FP_HR] = hr;
+    zo[FO_DIAG + C2D_FP_HR_ST] = hr_st;
+    zo[FO_DIAG + C2D_FP_DELTA_T] = fabs(Te_new - tea) / Te_new;
+    zo[FO_DIAG + C2D_FP_STEPS] = (double)fp_steps;
+    zo[FO_DIAG + C2D_FP_SKIPPED] = 0.0;
+    zo[FO_DIAG + 7] = 0.0;
+  }
+}
+
+template <int BS>
+__global__ void __launch_bounds__(BS) c2d_fp_fast_kernel(const FpParams* __restrict__ Pp) {
+  const FpParams& P = *Pp;
+  Blk<BS> B;
+  B.tid = threadIdx.x;
+  B.lane = B.tid & (FPB - 1);
+  B.wave = B.tid / FPB;
+  if (B.tid == 0) {
+    f_eg[0] = c2d_exp_bf(gammln(5.0e-1 + 2.0));
+    f_eg[1] = c2d_exp_bf(gammln(5.0e-1 + 3.0));
+  }
+  __syncthreads();
+  fp_zone_fast<BS>(P, B);
+}
+
+}  // namespace
+}  // namespace c2d
+
+/* threads per zone (one workgroup per zone): 4 waves, one per SIMD of the
+ * zone's CU; with <= 256 VGPRs two zones share a CU */
+extern "C" int c2d_fp_fast_block(int, int) { return 256; }
+
+/* dP: the parameters in device memory (uploaded by the caller on `stream`) */
+extern "C" int c2d_launch_fp_fast(const c2d::FpParams* dP, int ncell, int block, hipStream_t stream) {
+  if (ncell <= 0) return 0;
+  if (block != 256) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(c2d::c2d_fp_fast_kernel<256>, dim3(ncell), dim3(256), 0, stream, dP);
+  return (int)hipGetLastError();
+}

@@ -113,6 +113,8 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_fp_set_config.argtypes = [vp, C.POINTER(abi.FpConfig)]
     lib.c2d_fp_step.restype = C.c_int
     lib.c2d_fp_step.argtypes = [vp, C.POINTER(abi.FpStepIn), C.POINTER(abi.FpStepOut)]
+    lib.c2d_fp_set_mode.restype = C.c_int
+    lib.c2d_fp_set_mode.argtypes = [vp, C.c_int32]
     lib.c2d_last_fp_ms.restype = C.c_int
     lib.c2d_last_fp_ms.argtypes = [vp, C.POINTER(C.c_double)]
     lib.c2d_volume_em.restype = C.c_int
@@ -344,6 +346,12 @@ class Engine:
         """FP_calc run constants + F_IC (replaces setup_bcast / FP_bcast)."""
         self._fpc = const.to_ctypes()
         self._check(self.lib.c2d_fp_set_config(self.ctx, C.byref(self._fpc)))
+
+    def fp_set_mode(self, mode: int) -> None:
+        """abi.FP_EXACT (bit for bit the reference order, default) or
+        abi.FP_FAST (block-parallel sums, PCR tridag, tree-summed McDonald
+        series: equal within rounding; include/compton2d.h c2d_fp_set_mode)."""
+        self._check(self.lib.c2d_fp_set_mode(self.ctx, int(mode)))
 
     def fp_step(self, ncycle: int, time: float, dt: float, inputs: dict, state: dict) -> dict:
         """One `update` (src/update2d.f:7-327) on the GPU; returns the new state.

@@ -408,6 +408,18 @@ int  c2d_fp_set_config(c2d_ctx* ctx, const c2d_fp_config* cfg);
  * Replaces FP_send_job / FP_calc / FP_send_result / E_add_up /
  * FP_end_bcast.  Synchronous. */
 int  c2d_fp_step(c2d_ctx* ctx, const c2d_fp_step_in* in, c2d_fp_step_out* out);
+/* FP_calc arithmetic of the following c2d_fp_step calls:
+ *   C2D_FP_EXACT (default): every sum, tridag's Thomas recurrence and
+ *     McDonald's series in the reference's order -- bit for bit the det-math
+ *     oracle (one in-order latency chain per zone);
+ *   C2D_FP_FAST: the same per-bin and per-term arithmetic, the sums as block
+ *     reductions/scans, tridag by parallel cyclic reduction, McDonald's terms
+ *     summed as a tree (the same terms: the reference's stopping index) --
+ *     equal to the exact mode within rounding (DESIGN.md §4b states the
+ *     tolerance: f_nt 1e-10 relative, Te_new on the same 1.005 lattice). */
+#define C2D_FP_EXACT 0
+#define C2D_FP_FAST  1
+int  c2d_fp_set_mode(c2d_ctx* ctx, int32_t mode);
 
 /* Device timing of the last step's dominant kernel (transport generation 0):
  * milliseconds and launches, measured with HIP events on the library's

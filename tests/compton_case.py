@@ -95,3 +95,37 @@ def summary(tallies, nz=2, nr=2, nmu=1):
     """(F(E), edout, counters) of a tally vector."""
     t = abi.split_tallies(np.asarray(tallies), nz, nr, nmu)
     return S.f_of_e(t["fout"]), np.asarray(t["edout"]).ravel()[:5].copy(), np.asarray(t["counters"])
+
+
+def compare_runs(FA, EA, FB, EB):
+    """Two sets of independent runs of the Compton workload (per-run F(E)
+    [runs, bins] and light-curve bands [runs, 5]; each side's runs i.i.d.),
+    compared with run-to-run variances (not shard estimates): per Compton bin
+    z = (mean_A - mean_B) / sqrt(s_A^2/n_A + s_B^2/n_B), its chi^2 and p-value,
+    the bands' z, and the rel L2 of the mean F(E) over the Compton bins beside
+    the rel L2 two unbiased estimates of these sizes are expected to show."""
+    from scipy import stats
+    FA, FB, EA, EB = (np.asarray(x, float) for x in (FA, FB, EA, EB))
+    cb = compton_bins()
+    mA, mB = FA.mean(axis=0), FB.mean(axis=0)
+    vA = FA.var(axis=0, ddof=1) / len(FA)
+    vB = FB.var(axis=0, ddof=1) / len(FB)
+    s = np.sqrt(vA + vB)
+    live = cb[(mB[cb] > 0) & (s[cb] > 0)]
+    z = (mA[live] - mB[live]) / s[live]
+    chi2 = float(np.sum(z ** 2))
+    eA, eB = EA.mean(axis=0), EB.mean(axis=0)
+    se = np.sqrt(EA.var(axis=0, ddof=1) / len(EA) + EB.var(axis=0, ddof=1) / len(EB))
+    zb = np.where(se > 0, (eA - eB) / np.where(se > 0, se, 1.0), 0.0)
+    rel = float(np.linalg.norm(mA[cb] - mB[cb]) / np.linalg.norm(mB[cb]))
+    v = vA[cb] + vB[cb]
+    rel_exp = float(np.sqrt(np.sum(v)) / np.linalg.norm(mB[cb]))
+    # rel^2 is a variance-weighted sum of squared normals: ~ chi^2 with nu
+    # effective degrees of freedom (a few bins carry most of the variance)
+    nu = float(np.sum(v) ** 2 / np.sum(v ** 2))
+    return {"rel_l2_bound_999": rel_exp * float(np.sqrt(stats.chi2.ppf(0.999, nu) / nu)), "nu": nu,
+            "bins": int(len(live)), "rms_z": float(np.sqrt(np.mean(z ** 2))),
+            "max_abs_z": float(np.abs(z).max()), "chi2": chi2,
+            "p_value": float(stats.chi2.sf(chi2, len(live))),
+            "bins_over_4sigma": [int(b) for b in live[np.abs(z) > 4.0]],
+            "band_z": [float(x) for x in zb], "rel_l2": rel, "rel_l2_expected": rel_exp}

@@ -155,3 +155,31 @@ def test_gpu_c3_sed_binned_on_device_equals_oracle_binning(mode):
             assert ms > 0
         assert cnt.sum() > 0.5 * len(ev)       # the wide window holds the step's escapes
     eng.close()
+
+
+def test_gpu_c3_fp_fast_within_tolerance():
+    """C2D_FP_FAST on the reference's C3 FP inputs (all 270 zones on the GPU,
+    sampled zones against the det oracle): the tolerance of
+    tests/test_gpu_fp.py, and Te_new equal to the reference's."""
+    from test_gpu_fp import fast_vs_oracle
+    gc = case()
+    eng = Engine(gc.grid(device=0))
+    eng.fp_set_config(gc.constants())
+    eng.fp_set_mode(abi.FP_FAST)
+    for n in gc.fp_steps:
+        fi = gc.fp_in(n)
+        g = eng.fp_step(fi["ncycle"], fi["time"], fi["dt"], fi, fi)
+        o = OL.fp_step(gc.grid(), gc.constants(), fi["ncycle"], fi["time"], fi["dt"], fi, fi,
+                       flavor="det", cells=SAMPLE)
+        js, ks = np.divmod(np.array(SAMPLE), gc.nr)
+        gs = {k: (np.asarray(v)[js, ks] if np.ndim(v) >= 2 else v) for k, v in g.items()}
+        os_ = {k: (np.asarray(v)[js, ks] if np.ndim(v) >= 2 else v) for k, v in o.items()}
+        for k in ("E_tot_old", "E_tot_new", "hr_total"):      # whole-grid sums: only sampled zones in o
+            gs.pop(k), os_.pop(k)
+        for k in ("Te_new", "tea", "gmin", "gmax", "p_nth"):
+            np.testing.assert_array_equal(gs[k], os_[k], err_msg=k)
+        for k in ("f_nt", "Pnt"):
+            d = np.max(np.abs(gs[k] - os_[k])) / np.max(np.abs(os_[k]))
+            assert d <= 1e-10, (n, k, d)
+        np.testing.assert_array_equal(g["Te_new"], gc.fp_out(n)["Te_new"])
+    eng.close()

@@ -77,3 +77,50 @@ def test_gpu_fp_rejects_positrons_and_requires_config():
     with pytest.raises(Exception, match="C2D_E_ARG"):
         eng.fp_set_config(c)
     eng.close()
+
+
+# C2D_FP_FAST tolerance: the same per-bin and per-term
+# arithmetic as the exact kernel, only the order of the additions and the
+# tridiagonal algorithm (PCR) differ, so the zone outputs equal the det-math
+# oracle's to rounding carried through the zone's implicit sub-steps
+FAST_TOL = {"f_nt": 1e-10, "Pnt": 1e-10, "n_e": 1e-12, "amxwl": 1e-9}
+
+
+def fast_vs_oracle(g, o, label):
+    """Deviations of a C2D_FP_FAST result from the det oracle; asserts the
+    stated tolerance and returns the measured figures."""
+    dev = {}
+    for k in ("Te_new", "tea", "gmin", "gmax", "p_nth"):
+        np.testing.assert_array_equal(g[k], o[k], err_msg="%s %s" % (label, k))
+    for k, tol in FAST_TOL.items():
+        d = np.max(np.abs(np.asarray(g[k]) - np.asarray(o[k]))) / max(np.max(np.abs(o[k])), 1e-300)
+        dev[k] = float(d)
+        assert d <= tol, (label, k, d)
+    np.testing.assert_array_equal(g["zone_diag"][..., 5], o["zone_diag"][..., 5])   # sub-steps
+    for k in ("E_tot_old", "E_tot_new", "hr_total"):
+        d = abs(g[k] - o[k]) / max(abs(o[k]), 1e-300)
+        dev[k] = float(d)
+        assert d <= 1e-10, (label, k, g[k], o[k])
+    return dev
+
+
+@pytest.mark.parametrize("name", FP_CASES)
+def test_gpu_fp_fast_within_tolerance(name, capsys):
+    """C2D_FP_FAST (fp_fast.hip) vs the det oracle on the reference's FP inputs:
+    temperatures (Te_new, tea), gmin/gmax, p_nth and the sub-step count equal;
+    f_nt, Pnt within 1e-10 of the spectrum's maximum; n_e 1e-12; energies 1e-10."""
+    case = FpGoldenCase(name)
+    eng = Engine(case.grid(device=0))
+    eng.fp_set_config(case.constants())
+    eng.fp_set_mode(abi.FP_FAST)
+    for n in case.steps:
+        fi = case.fp_in(n)
+        g = eng.fp_step(fi["ncycle"], fi["time"], fi["dt"], fi, fi)
+        o = OL.fp_step(case.grid(), case.constants(), fi["ncycle"], fi["time"], fi["dt"], fi, fi,
+                       flavor="det")
+        dev = fast_vs_oracle(g, o, "%s step %d" % (name, n))
+        with capsys.disabled():
+            print("\nC2D_FP_FAST %s step %d: %s" % (name, n, {k: "%.1e" % v for k, v in dev.items()}))
+    with pytest.raises(Exception, match="C2D_E_ARG"):
+        eng.fp_set_mode(7)
+    eng.close()

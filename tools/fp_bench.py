@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--vary", action="store_true", help="perturb n_e, tea per zone")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu-zones", type=int, default=16)
+    ap.add_argument("--mode", choices=("exact", "fast"), default="exact",
+                    help="c2d_fp_set_mode: exact (bit for bit) or fast (block-parallel, fp_fast.hip)")
     args = ap.parse_args()
     from compton2d_amd.engine import Engine
     nz = args.nz or args.grid
@@ -90,6 +92,8 @@ def main():
     g.device = 0
     eng = Engine(g)
     eng.fp_set_config(c.constants())
+    from compton2d_amd import abi
+    eng.fp_set_mode(abi.FP_FAST if args.mode == "fast" else abi.FP_EXACT)
     r = eng.fp_step(tile["ncycle"], tile["time"], tile["dt"], tile, tile)   # warm-up
     walls, kms = [], []
     for _ in range(args.reps):
@@ -117,9 +121,14 @@ def main():
     f_cpu = np.concatenate([x[1][0] for x in res], axis=0)
     te_cpu = np.concatenate([x[2][0] for x in res], axis=0)
     same = bool(np.array_equal(f_cpu, r["f_nt"][0, :m]) and np.array_equal(te_cpu, r["Te_new"][0, :m]))
+    fg = r["f_nt"][0, :m]
+    f_dev = float(np.max(np.abs(fg - f_cpu)) / max(np.max(np.abs(f_cpu)), 1e-300))
+    te_same = bool(np.array_equal(te_cpu, r["Te_new"][0, :m]))
     ms = float(np.median(kms))
     out = {
-        "kernel": "c2d_fp_kernel (one wavefront per zone)",
+        "kernel": ("c2d_fp_fast_kernel<256> (one 4-wave workgroup per zone, C2D_FP_FAST)"
+                   if args.mode == "fast" else "c2d_fp_kernel (C2D_FP_EXACT)"),
+        "mode": args.mode,
         "zones": nz * nr,
         "implicit_substeps": substeps,
         "kernel_ms": ms,
@@ -130,6 +139,8 @@ def main():
                          "sample": "%d zones of row 0 on %d processes (oracle, det math), "
                                    "%.1f s (pool wall %.1f s)" % (m, len(jobs), cpu_t, cpu_wall)},
         "gpu_equals_oracle_on_sample": same,
+        "f_nt_max_dev_vs_oracle_on_sample": f_dev,
+        "Te_new_equal_on_sample": te_same,
         "workload": "%s fixture zones (reference FP inputs after one transport step) "
                     "tiled over %dx%d%s" % (args.case, nz, nr, ", n_e/tea varied per zone" if args.vary else ""),
         "memo": os.environ.get("C2D_FP_MEMO", "1"),
