@@ -59,6 +59,8 @@ __shared__ double f_pcr[2][4][256];          /* PCR rows a, b, c, d (double-buff
 __shared__ double f_red[2][2][WMAXF];        /* block reductions: [slot][value][wave] */
 __shared__ int f_ired[2][2][WMAXF];          /* block integer min/max                 */
 __shared__ double f_eg[2];                   /* exp(gammln(2.5)), exp(gammln(3.5))    */
+constexpr int ZMEMO = 64;                    /* the zone's gamma_bar memo (direct-mapped) */
+__shared__ double f_mth[ZMEMO], f_mgv[ZMEMO];
 
 /* one block of BS threads; `slot` alternates so each reduction needs one barrier */
 template <int BS>
@@ -67,10 +69,26 @@ struct Blk {
   int tid, lane, wave;
   int slot = 0, islot = 0;
 
+  /* DPP move of a double within 16-lane rows (both halves, same control) */
+  template <int CTRL>
+  __device__ __forceinline__ static double dpp(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+  }
+  /* the wave's sum: within each 16-lane row by DPP (xor 1, xor 2, rotate 4,
+   * rotate 8), then the four rows' sums (lanes 0, 16, 32, 48) read as
+   * uniform values and added in row order, so every lane holds the same bits */
   __device__ __forceinline__ static double wsum(double v) {
-#pragma unroll
-    for (int o = FPB / 2; o > 0; o >>= 1) v = v + __shfl_xor(v, o, FPB);
-    return v;
+    v = v + dpp<0xB1>(v);          /* quad_perm [1,0,3,2] */
+    v = v + dpp<0x4E>(v);          /* quad_perm [2,3,0,1] */
+    v = v + dpp<0x124>(v);         /* row_ror:4           */
+    v = v + dpp<0x128>(v);         /* row_ror:8           */
+    double r = rl(v, 0);
+    r = r + rl(v, 16);
+    r = r + rl(v, 32);
+    r = r + rl(v, 48);
+    return r;
   }
   /* two sums at once; identical bits in every thread */
   __device__ __forceinline__ void sum2(double& a, double& b) {
@@ -118,6 +136,36 @@ struct Blk {
     }
     islot ^= 1;
   }
+  /* first set flag of each of two series over a pass of T*BS terms (term
+   * k*BS + tid is flag [k] of thread tid): a wave's first by ballot, then the
+   * waves' minimum through LDS; INT_MAX if none is set */
+  __device__ __forceinline__ static int first_lane(unsigned long long m) {
+    return m ? __ffsll((long long)m) - 1 : INT_MAX;
+  }
+  template <int T>
+  __device__ __forceinline__ void firsts(const bool (&fa)[T], const bool (&fb)[T], int& f2, int& f3) {
+    int w2 = INT_MAX, w3 = INT_MAX;
+#pragma unroll
+    for (int k = T - 1; k >= 0; k--) {           /* the lowest k with a flag wins */
+      const int la = first_lane(__ballot(fa[k])), lb = first_lane(__ballot(fb[k]));
+      if (la != INT_MAX) w2 = k * BS + wave * FPB + la;
+      if (lb != INT_MAX) w3 = k * BS + wave * FPB + lb;
+    }
+    if (lane == 0) {
+      f_ired[islot][0][wave] = w2;
+      f_ired[islot][1][wave] = w3;
+    }
+    __syncthreads();
+    f2 = INT_MAX;
+    f3 = INT_MAX;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int x = f_ired[islot][0][w], y = f_ired[islot][1][w];
+      f2 = x < f2 ? x : f2;
+      f3 = y < f3 ? y : f3;
+    }
+    islot ^= 1;
+  }
   /* block minima of two ints */
   __device__ __forceinline__ void min2(int& a, int& b) {
 #pragma unroll
@@ -142,11 +190,17 @@ struct Blk {
   }
   /* inclusive prefix sum of v over the threads in tid order, and the total */
   __device__ __forceinline__ double scan(double v, double& total) {
-#pragma unroll
-    for (int o = 1; o < FPB; o <<= 1) {
-      const double u = __shfl_up(v, o, FPB);
-      if (lane >= o) v = v + u;
-    }
+    /* within 16-lane rows by DPP row shifts (lanes shifted in from outside
+     * the row read 0), then the preceding rows' totals */
+    v = v + dpp<0x111>(v);         /* row_shr:1 */
+    v = v + dpp<0x112>(v);         /* row_shr:2 */
+    v = v + dpp<0x114>(v);         /* row_shr:4 */
+    v = v + dpp<0x118>(v);         /* row_shr:8 */
+    const double r0 = rl(v, 15), r1 = rl(v, 31), r2 = rl(v, 47);
+    const int row = lane >> 4;
+    if (row == 1) v = v + r0;
+    if (row == 2) v = v + (r0 + r1);
+    if (row == 3) v = v + ((r0 + r1) + r2);
     if (lane == FPB - 1) f_red[slot][0][wave] = v;
     __syncthreads();
     double before = 0.0, all = 0.0;
@@ -207,51 +261,148 @@ __device__ __forceinline__ void gb_insert(const FpParams& P, double th, double g
  * exactly the reference's terms enter), per-thread partial sums, one tree
  * sum at the end.  Beyond the abscissa table wave 0 finishes the series with
  * c2d_wave's replayed chain (never reached on the reference's decks). */
+#ifdef C2D_FP_PROF
+__shared__ long long f_pf[4];   /* McDonald passes, cycles in the pass loop, in the finish */
+#endif
+/* exp(x) for -745 < x <= 0 (McDonald's terms, y < 225): x = k ln2 + r with
+ * |r| <= ln2/2, e^r by its Taylor polynomial to degree 13 (truncation
+ * < 5e-18) in FMAs, 2^k by v_ldexp -- ~17 dependent operations where
+ * fdlibm's form (c2d_exp_bf) has a division in its chain; within 2 ulp */
+__device__ __forceinline__ double exp_nonpos(double x) {
+  const double kd = __builtin_rint(x * 1.4426950408889634);
+  double r = __builtin_fma(-kd, 6.93147180369123816490e-01, x);
+  r = __builtin_fma(-kd, 1.90821492927058770002e-10, r);
+  double p = 1.6059043836821613e-10;                 /* 1/13! */
+  p = __builtin_fma(p, r, 2.0876756987868100e-09);  /* 1/12! */
+  p = __builtin_fma(p, r, 2.5052108385441720e-08);  /* 1/11! */
+  p = __builtin_fma(p, r, 2.7557319223985893e-07);  /* 1/10! */
+  p = __builtin_fma(p, r, 2.7557319223985888e-06);  /* 1/9!  */
+  p = __builtin_fma(p, r, 2.4801587301587302e-05);  /* 1/8!  */
+  p = __builtin_fma(p, r, 1.9841269841269841e-04);  /* 1/7!  */
+  p = __builtin_fma(p, r, 1.3888888888888889e-03);  /* 1/6!  */
+  p = __builtin_fma(p, r, 8.3333333333333332e-03);  /* 1/5!  */
+  p = __builtin_fma(p, r, 4.1666666666666664e-02);  /* 1/4!  */
+  p = __builtin_fma(p, r, 1.6666666666666666e-01);  /* 1/3!  */
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  p = __builtin_fma(p, r, 1.0);
+  return __builtin_ldexp(p, (int)kd);
+}
+
+/* one abscissa row through a global (not flat) pointer */
+__device__ __forceinline__ double4 gld4(const double* p) {
+  const C2D_GLOBAL double* q = (const C2D_GLOBAL double*)p;
+  return make_double4(q[0], q[1], q[2], q[3]);
+}
+
+/* the abscissa row of term n: the table's, or past it (never reached on the
+ * reference's decks: the table covers Theta up to ~1e5) the chain continued
+ * from the table's last t by a power of dt instead of the reference's
+ * repeated product: the same values to rounding */
+__device__ __forceinline__ double4 mcd_row(const double* __restrict__ tab, int n) {
+  if (n < C2D_FP_MCD_N) return gld4((tab + (size_t)n * 4));
+  const double dt = 1.001, sm = 5.0e-1 * (1.0 + dt);
+  const double t = tab[(size_t)(C2D_FP_MCD_N - 1) * 4] * c2d_exp_bf((double)(n - C2D_FP_MCD_N + 1) * c2d_log(dt));
+  const double ts = t * sm;
+  const double q = ts * ts - 1.0, rq = __builtin_sqrt(q);
+  return make_double4(t, ts, q * rq, q * q * rq);
+}
+
+/* McDonald terms per thread per pass (C2D_FPF_TPT: 2 or 4) */
+#ifndef C2D_FPF_TPT
+#define C2D_FPF_TPT 2
+#endif
+constexpr int TPT = C2D_FPF_TPT;
+
+/* one pass of TPT*BS terms (row x[k]: term n0 + k*BS + tid) */
+template <int BS>
+__device__ __forceinline__ void mcd_pass(Blk<BS>& B, double z, const double4 (&x)[TPT], double& s2, double& s3,
+                                         bool& run2, bool& run3) {
+  const double dt = 1.001, d = dt - 1.0;
+  double v2[TPT], v3[TPT];
+  bool st2[TPT], st3[TPT];
+#pragma unroll
+  for (int k = 0; k < TPT; k++) {
+    const double y = z * x[k].y;
+    v2[k] = 0.0;
+    v3[k] = 0.0;
+    if (y < 2.25e2) {
+      const double em = exp_nonpos(-y);
+      v2[k] = x[k].z * em;
+      v3[k] = x[k].w * em;
+    }
+    const double tn = x[k].x * dt;
+    st2[k] = !(tn < 2.0 || v2[k] > 1.0e-8);
+    st3[k] = !(tn < 2.0 || v3[k] > 1.0e-8);
+  }
+  int f2, f3;
+  B.template firsts<TPT>(st2, st3, f2, f3);
+  /* terms up to and including each series' first stopping term */
+#pragma unroll
+  for (int k = 0; k < TPT; k++) {
+    const int n = k * BS + B.tid;
+    if (run2 && n <= f2) s2 = s2 + d * x[k].x * v2[k];
+    if (run3 && n <= f3) s3 = s3 + d * x[k].x * v3[k];
+  }
+  if (f2 != INT_MAX) run2 = false;
+  if (f3 != INT_MAX) run3 = false;
+}
+
+/* McDonald K2, K3 (volume2d.f:598-626) by the whole block: TPT*BS terms per
+ * pass (TPT per thread, the next pass's abscissa rows loaded ahead), each
+ * series' first stopping term by ballot + a block minimum (so exactly the
+ * reference's terms enter), per-thread partial sums, one tree sum at the end. */
 template <int BS>
 __device__ void mcdonald23_fast(Blk<BS>& B, double z, const double* __restrict__ tab, double& K2, double& K3,
                                 long long& guard) {
-  const double dt = 1.001, d = dt - 1.0, sm = 5.0e-1 * (1.0 + dt);
-  /* past the table (never reached on the reference's decks) the abscissae
-   * continue from the table's last t by a power of dt instead of the
-   * reference's repeated product: the same values to rounding */
-  const double t_last = tab[(size_t)(C2D_FP_MCD_N - 1) * 4], ldt = c2d_log(dt);
+  constexpr int PASS = TPT * BS;
+  static_assert(C2D_FP_MCD_N % PASS == 0, "table passes");
   double s2 = 0.0, s3 = 0.0;
   bool run2 = true, run3 = true;
-  for (int n0 = 0;; n0 += BS) {
-    const int n = n0 + B.tid;
-    double t, ts, p2, p3;
-    if (n < C2D_FP_MCD_N) {
-      const double4 e = *(const double4*)(tab + (size_t)n * 4);
-      t = e.x; ts = e.y; p2 = e.z; p3 = e.w;
-    } else {
-      t = t_last * c2d_exp_bf((double)(n - C2D_FP_MCD_N + 1) * ldt);
-      ts = t * sm;
-      const double q = ts * ts - 1.0, rq = __builtin_sqrt(q);
-      p2 = q * rq;
-      p3 = q * q * rq;
+#ifdef C2D_FP_PROF
+  const long long pt0 = clock64();
+#endif
+  const double* row = tab + (size_t)B.tid * 4;
+  double4 e[TPT];
+#pragma unroll
+  for (int k = 0; k < TPT; k++) e[k] = gld4((row + (size_t)k * BS * 4));
+  int n0 = 0;
+  for (; n0 < C2D_FP_MCD_N; n0 += PASS) {
+#ifdef C2D_FP_PROF
+    if (B.tid == 0) f_pf[0]++;
+#endif
+    double4 x[TPT];
+#pragma unroll
+    for (int k = 0; k < TPT; k++) x[k] = e[k];
+    /* next pass's rows, ahead: global (not flat) loads, so the LDS waits
+     * of the pass (lgkmcnt) do not wait for them too */
+    if (n0 + PASS < C2D_FP_MCD_N) {
+#pragma unroll
+      for (int k = 0; k < TPT; k++) e[k] = gld4((row + (size_t)(n0 + PASS + k * BS) * 4));
     }
-    const double y = z * ts;
-    double sd2 = 0.0, sd3 = 0.0;
-    if (y < 2.25e2) {
-      const double em = c2d_exp_bf(-y);
-      sd2 = p2 * em;
-      sd3 = p3 * em;
-    }
-    const double tn = t * dt;
-    const bool st2 = !(tn < 2.0 || sd2 > 1.0e-8), st3 = !(tn < 2.0 || sd3 > 1.0e-8);
-    /* first stopping term of each series in this pass */
-    int stop2 = st2 ? n : INT_MAX, stop3 = st3 ? n : INT_MAX;
-    B.min2(stop2, stop3);
-    if (run2 && n <= stop2) s2 = s2 + d * t * sd2;
-    if (run3 && n <= stop3) s3 = s3 + d * t * sd3;
-    if (stop2 != INT_MAX) run2 = false;
-    if (stop3 != INT_MAX) run3 = false;
-    guard += BS;
+    mcd_pass<BS>(B, z, x, s2, s3, run2, run3);
+    guard += PASS;
     if (!run2 && !run3) break;
-    if (guard > GUARD_MAX) break;
   }
+  /* past the table (never reached on the reference's decks) */
+  for (; (run2 || run3) && guard <= GUARD_MAX; n0 += PASS) {
+    double4 x[TPT];
+#pragma unroll
+    for (int k = 0; k < TPT; k++) x[k] = mcd_row(tab, n0 + k * BS + B.tid);
+    mcd_pass<BS>(B, z, x, s2, s3, run2, run3);
+    guard += PASS;
+  }
+#ifdef C2D_FP_PROF
+  const long long pt1 = clock64();
+#endif
   B.sum2(s2, s3);
   mcdonald23_finish_c(z, s2, s3, f_eg[0], f_eg[1], K2, K3);
+#ifdef C2D_FP_PROF
+  if (B.tid == 0) {
+    f_pf[1] += pt1 - pt0;
+    f_pf[2] += clock64() - pt1;
+  }
+#endif
 }
 
 template <int BS>
@@ -390,35 +541,64 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
   double hr = 0.0, hr_st = 0.0, sum_E = 0.0, t_fp = 0.0;
   int fp_steps = 0;
   double g_av_next = 0.0, hr_th_c_next = 0.0;
-  double memo_th[4] = {-1.0, -1.0, -1.0, -1.0}, memo_g[4] = {0.0, 0.0, 0.0, 0.0};
-  int memo_next = 0;
-  auto gamma_bar_m = [&](double th) -> double {
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-      if (memo_th[q] == th) return memo_g[q];
+#ifdef C2D_FP_PROF
+  /* section timers (tools/fp_prof.py): zone_diag 0 = gamma_bar incl. memo,
+   * 1 = PCR solve, 2 = whole sub-step loop, 3 = McDonald pairs computed */
+  long long pf_gb = 0, pf_tri = 0, pf_loop0 = clock64(), pf_t0 = 0, pf_mcd = 0;
+#define PF_BEGIN() pf_t0 = clock64()
+#define PF_END(acc) acc += clock64() - pf_t0
+#else
+#define PF_BEGIN()
+#define PF_END(acc)
+#endif
+  /* gamma_bar is a pure function of Theta, and a zone's search revisits the
+   * lattice values around its temperature sub-step after sub-step: a
+   * 64-entry direct-mapped memo in LDS keyed on Theta's bits answers those.
+   * glob: also consult and fill the table shared by all zones, which pays
+   * where zones walk the same chain (C3: every zone from the tea clamp, many
+   * lattice steps per search): used for a zone's first value and from a
+   * search's third step on; a zone tracking its own temperature stays off it */
+  for (int q = tid; q < ZMEMO; q += BS) f_mth[q] = -1.0;
+  __syncthreads();
+  auto gamma_bar_m = [&](double th, bool glob) -> double {
+    const uint64_t hb = c2d_bits(th);
+    const int slot = (int)((hb ^ (hb >> 17) ^ (hb >> 31)) & (ZMEMO - 1));
+    if (f_mth[slot] == th) return f_mgv[slot];
     double g = 0.0;
-    /* the global memo, read by thread 0 and broadcast, so every thread takes the same branch */
-    if (tid == 0) {
-      double gm = 0.0;
-      f_red[B.slot][0][0] = gb_lookup(P, th, gm) ? gm : 0.0;
+    if (glob) {
+      /* read by thread 0 and broadcast, so every thread takes the same branch */
+      if (tid == 0) {
+        double gm = 0.0;
+        f_red[B.slot][0][0] = gb_lookup(P, th, gm) ? gm : 0.0;
+      }
+      __syncthreads();
+      g = f_red[B.slot][0][0];
+      B.slot ^= 1;
     }
-    __syncthreads();
-    g = f_red[B.slot][0][0];
-    B.slot ^= 1;
     if (g == 0.0) {
       g = gamma_bar_fast<BS>(B, th, P.mcd, guard);
-      if (tid == 0) gb_insert(P, th, g);
+#ifdef C2D_FP_PROF
+      if (th >= F32(0.2)) pf_mcd++;
+#endif
+      if (glob && tid == 0) gb_insert(P, th, g);
     }
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-      if (q == memo_next) { memo_th[q] = th; memo_g[q] = g; }
-    memo_next = (memo_next + 1) & 3;
+    /* the slot is rewritten only once every thread has looked it up, and
+     * read again only once the rewrite is visible to all: the memo stays
+     * uniform across the block, so every thread takes the same branches */
+    __syncthreads();
+    if (tid == 0) {
+      f_mth[slot] = th;
+      f_mgv[slot] = g;
+    }
+    __syncthreads();
     return g;
   };
   const double vn = 8.176e-7;
   for (;;) {
     /* label 200 (:577) */
-    const double g_av0 = (fp_steps == 0) ? gamma_bar_m(Th_e) : g_av_next;
+    PF_BEGIN();
+    const double g_av0 = (fp_steps == 0) ? gamma_bar_m(Th_e, true) : g_av_next;
+    PF_END(pf_gb);
     double g_av = g_av0;
     const double hr_th_c = (fp_steps == 0)
         ? B.sum((i <= NT - 1) ? -(vn * f_dgic[i] * f_fold[i] * dgp * volume * n_lept) : 0.0)
@@ -559,7 +739,9 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
       ta = -d_t / Delta_g * f_bigC[i - 1] * f_bigW[i - 1] / D_gminus;
     }
     /* tridag (:2476-2518) by cyclic reduction; clip u(2..num_nt) (:2512) */
+    PF_BEGIN();
     double u = pcr_solve<BS>(B, ta, tb, tc, own ? f_fold[i] : 0.0);
+    PF_END(pf_tri);
     if (i >= 2 && u < 0.0) u = 0.0;
     if (i == NT || i == 1) u = 0.0;
     /* Pnt prefix, sum_p, sum_E (:1415-1419) */
@@ -583,20 +765,17 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
     B.sum2(gbar, hr_th_c_next);
     /* new temperature (:1440-1468) */
     double The_new = Th_e;
-    if (gbar > g_av) {
-      while (gbar > g_av) {
-        The_new = The_new * F32(1.005);
-        g_av = gamma_bar_m(The_new);
-        if (guard > GUARD_MAX) break;
-      }
-    } else {
-      while (gbar < g_av) {
-        The_new = The_new / F32(1.005);
-        g_av = gamma_bar_m(The_new);
-        if (The_new < 1.0e-2) break;
-        if (guard > GUARD_MAX) break;
-      }
+    PF_BEGIN();
+    /* one loop for both directions: gamma_bar's code is inlined once here */
+    const bool up = gbar > g_av;
+    int ks = 0;
+    while (up ? gbar > g_av : gbar < g_av) {
+      The_new = up ? The_new * F32(1.005) : The_new / F32(1.005);
+      g_av = gamma_bar_m(The_new, ++ks > 2);
+      if (!up && The_new < 1.0e-2) break;
+      if (guard > GUARD_MAX) break;
     }
+    PF_END(pf_gb);
     if (guard > GUARD_MAX) {
       if (tid == 0) atomicOr(P.err, FPERR_GUARD);
       return;
@@ -679,6 +858,15 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
     zo[FO_DIAG + C2D_FP_STEPS] = (double)fp_steps;
     zo[FO_DIAG + C2D_FP_SKIPPED] = 0.0;
     zo[FO_DIAG + 7] = 0.0;
+#ifdef C2D_FP_PROF
+    zo[FO_DIAG + 0] = (double)pf_gb;
+    zo[FO_DIAG + 1] = (double)pf_tri;
+    zo[FO_DIAG + 2] = (double)(clock64() - pf_loop0);
+    zo[FO_DIAG + 3] = (double)pf_mcd;
+    zo[FO_DIAG + 4] = (double)f_pf[0];
+    zo[FO_DIAG + 6] = (double)f_pf[1];
+    zo[FO_DIAG + 7] = (double)f_pf[2];
+#endif
   }
 }
 
@@ -690,6 +878,9 @@ __global__ void __launch_bounds__(BS) c2d_fp_fast_kernel(const FpParams* __restr
   B.lane = B.tid & (FPB - 1);
   B.wave = B.tid / FPB;
   if (B.tid == 0) {
+#ifdef C2D_FP_PROF
+    f_pf[0] = f_pf[1] = f_pf[2] = f_pf[3] = 0;
+#endif
     f_eg[0] = c2d_exp_bf(gammln(5.0e-1 + 2.0));
     f_eg[1] = c2d_exp_bf(gammln(5.0e-1 + 3.0));
   }
@@ -700,14 +891,18 @@ __global__ void __launch_bounds__(BS) c2d_fp_fast_kernel(const FpParams* __restr
 }  // namespace
 }  // namespace c2d
 
-/* threads per zone (one workgroup per zone): 4 waves, one per SIMD of the
- * zone's CU; with <= 256 VGPRs two zones share a CU */
-extern "C" int c2d_fp_fast_block(int, int) { return 256; }
+/* threads per zone (one workgroup per zone; C2D_FPF_BS, 256 or 512): 4 waves,
+ * one per SIMD of the zone's CU, or 8, two per SIMD, so one wave's
+ * dependent f64 chains (McDonald's exp) issue under the other's */
+#ifndef C2D_FPF_BS
+#define C2D_FPF_BS 256
+#endif
+extern "C" int c2d_fp_fast_block(int, int) { return C2D_FPF_BS; }
 
 /* dP: the parameters in device memory (uploaded by the caller on `stream`) */
 extern "C" int c2d_launch_fp_fast(const c2d::FpParams* dP, int ncell, int block, hipStream_t stream) {
   if (ncell <= 0) return 0;
-  if (block != 256) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(c2d::c2d_fp_fast_kernel<256>, dim3(ncell), dim3(256), 0, stream, dP);
+  if (block != C2D_FPF_BS) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(c2d::c2d_fp_fast_kernel<C2D_FPF_BS>, dim3(ncell), dim3(C2D_FPF_BS), 0, stream, dP);
   return (int)hipGetLastError();
 }

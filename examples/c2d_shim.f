@@ -36,7 +36,9 @@ c     it fits ucens, and imported from them after read_record.
 c
 c     Environment: C2D_SHIM_EXACT=1 (exact comtot build),
 c     C2D_SHIM_CENSUS_CAPACITY=n, C2D_SHIM_EVENTS=0 (no event file),
-c     C2D_SHIM_CENSUS_MIRROR=0 (no dbufout mirror).
+c     C2D_SHIM_CENSUS_MIRROR=0 (no dbufout mirror),
+c     C2D_SHIM_ALLREDUCE=0 (N workers: no all-reduce inside the C-ABI;
+c     every worker deposits its own tallies into COMMON instead).
 c     Errors print the library's message and MPI_ABORT (the reference
 c     `stop`s, src/imctrk2d.f:573-577).
 c
@@ -58,6 +60,16 @@ c     (2*jmax + 2*kmax slots x 5 tables of nfmax)
      1     sidx_u(99), sidx_l(99)
       integer, save :: ev_on = 1, mirror_on = 1, warned = 0
       logical, save :: static_done = .false.
+c     the run's lineage seed: the master's rseed, the same on every
+c     worker (setup_bcast leaves each worker rseed + myid*84725,
+c     src/fp_mpi.f:66-68)
+      integer, save :: seed0 = 0
+c     N workers: the step's tallies all-reduced over the workers inside
+c     the C-ABI (c2d_comm_init / c2d_allreduce_tallies: one RCCL
+c     all-reduce of the fused buffer), deposited into COMMON by worker 1
+c     only (C2D_SHIM_ALLREDUCE=0: every worker deposits its own share)
+      integer, save :: ar_on = 0
+      integer(c_int8_t), save :: commid(C2D_COMM_ID_BYTES)
       end module c2d_shim_state
 c
 c
@@ -109,6 +121,7 @@ c     workers' transport context, or the master's FP-only context
      1                         qcap)
       use iso_c_binding
       use compton2d
+      use c2d_shim_state, only: seed0
       implicit none
       include 'mpif.h'
       include 'general.pa'
@@ -148,7 +161,7 @@ c     hazard H3: census + volume transport see the previous kappa_tot
       if (c2d_shim_env('C2D_SHIM_EXACT', 0_8) .eq. 1)
      1     cfg%comtot_mode = C2D_COMTOT_EXACT
       cfg%device = device
-      cfg%seed = rseed
+      cfg%seed = seed0
       cfg%rank = rank
       cfg%world = world
       cfg%census_capacity = ccap
@@ -164,7 +177,7 @@ c
       use compton2d
       use c2d_shim_state, only: tctx, tready, lay, tal, spec, sptab,
      1     sidx_i, sidx_o, sidx_u, sidx_l, ev_on, mirror_on, warned,
-     2     static_done
+     2     static_done, seed0, ar_on, commid
       implicit none
       include 'mpif.h'
       include 'general.pa'
@@ -221,6 +234,23 @@ c     and volume jobs (reader.f; z_surf_bcast, vol_bcast), once
      1        MPI_COMM_WORLD, ierr)
          call MPI_BCAST(t1, ntmax, MPI_DOUBLE_PRECISION, master,
      1        MPI_COMM_WORLD, ierr)
+         seed0 = rseed
+         call MPI_BCAST(seed0, 1, MPI_INTEGER, master, MPI_COMM_WORLD,
+     1        ierr)
+c        the workers' exchange: worker 1 makes the unique id, every rank
+c        takes part in its broadcast (128 bytes, once per run)
+         if (numprocs .gt. 2) ar_on =
+     1        int(c2d_shim_env('C2D_SHIM_ALLREDUCE', 1_8))
+         if (ar_on .eq. 1) then
+            if (myid .eq. 1) then
+               rc = c2d_comm_unique_id(commid,
+     1              int(C2D_COMM_ID_BYTES, c_int64_t))
+               if (rc .ne. C2D_OK) call c2d_shim_fail(c_null_ptr,
+     1              'c2d_comm_unique_id', rc)
+            endif
+            call MPI_BCAST(commid, C2D_COMM_ID_BYTES, MPI_BYTE, 1,
+     1           MPI_COMM_WORLD, ierr)
+         endif
          static_done = .true.
       endif
 c
@@ -336,6 +366,12 @@ c        restart: census records read by read_record (census2d.f)
      1           'c2d_census_import', rc)
             deallocate(i5, keys)
          endif
+         if (ar_on .eq. 1) then
+            rc = c2d_comm_init(tctx, commid, int(myid - 1, c_int32_t),
+     1           int(nw, c_int32_t))
+            if (rc .ne. C2D_OK) call c2d_shim_fail(tctx,
+     1           'c2d_comm_init', rc)
+         endif
          tready = .true.
       endif
 c
@@ -423,11 +459,22 @@ c
       if (rc .ne. C2D_OK) call c2d_shim_fail(tctx,
      1     'c2d_transport_step', rc)
 c
-c     this worker's tallies, added where the reference's workers
-c     accumulate them (imctrk2d.f, compb_2d.f, imcleak2d.f)
+c     this worker's tallies (N workers: all workers', summed by one
+c     all-reduce over the workers inside the C-ABI), added where the
+c     reference's workers accumulate them (imctrk2d.f, compb_2d.f,
+c     imcleak2d.f).  With the all-reduce only worker 1 deposits: the
+c     reference's own reductions (xec_add, graphics_collect,
+c     cens_add_up -- the latter 400 x nz x nr doubles per step) then
+c     carry zeros from every other worker.
+      if (ar_on .eq. 1) then
+         rc = c2d_allreduce_tallies(tctx)
+         if (rc .ne. C2D_OK) call c2d_shim_fail(tctx,
+     1        'c2d_allreduce_tallies', rc)
+      endif
       rc = c2d_tally_download(tctx, tal, lay%total)
       if (rc .ne. C2D_OK) call c2d_shim_fail(tctx,
      1     'c2d_tally_download', rc)
+      if (ar_on .eq. 1 .and. myid .ne. 1) tal = 0.d0
       do 52 j = 1, nz
          do 51 k = 1, nr
             cell = (j-1)*nr + (k-1)

@@ -321,6 +321,11 @@ typedef struct c2o_ctx {
   int probe_bundles;            /* lineage mode: split1 probes as bundles (C2O_PROBE_BUNDLES=0: per copy) */
   int spec_switch, cr_sent, pair_switch, kappa_lag, rand_switch;
   int rng_mode, h4_stale;
+  /* MPI-worker emulation (c2o_set_dt_lag): the workers receive dt only in
+   * z_surf_bcast (src/surf_mpi.f:68), after their census and volume jobs,
+   * so those see the previous step's dt -- 0 in the first step */
+  int dt_lag;
+  double dt_prev;
   int rank, world;              /* lineage-sharded sources (global index % world == rank) */
   uint64_t seed;
   double t_bound_last;
@@ -1500,6 +1505,8 @@ int c2o_step(c2o_ctx* c, const c2d_step_in* in) {
   c->ncycle = in->ncycle;
   c->time = in->time;
   c->dt = in->dt;
+  const double dt_now = in->dt;
+  if (c->dt_lag) c->dt = c->dt_prev;
   memset(c->T, 0, sizeof(double) * c->L.total);
   c->nev = 0;
   gather3(c, &in->kappa_tot, C2D_N_VOL, c->kappa);
@@ -1573,8 +1580,9 @@ int c2o_step(c2o_ctx* c, const c2d_step_in* in) {
         if (c->err) return c->err;
       }
     }
-  /* surfaces use the current kappa_tot (broadcast in z_surf_bcast) */
+  /* surfaces use the current kappa_tot and dt (broadcast in z_surf_bcast) */
   c->kappa_use = c->kappa;
+  c->dt = dt_now;
   for (int js = 1; js <= c->nz; js++) {
     if (c->rng_mode == C2O_RNG_FIB) initialize_rand(fs, c->zseeds[js - 1]);
     for (int side = 0; side < 2; side++) {
@@ -1612,8 +1620,12 @@ int c2o_step(c2o_ctx* c, const c2d_step_in* in) {
     }
   }
   memcpy(c->kappa_prev, c->kappa, sizeof(double) * (int64_t)c->ncell * C2D_N_VOL);
+  c->dt_prev = dt_now;
   return c->err;
 }
+
+/* hazard H11 (MPI workers' stale dt, see c2o_ctx.dt_lag): off by default */
+void c2o_set_dt_lag(c2o_ctx* c, int on) { c->dt_lag = on; }
 
 const double* c2o_tallies(c2o_ctx* c, int64_t* n) {
   *n = c->L.total;

@@ -11,7 +11,13 @@
 # strong ones win at link time; nothing else in them changes.
 #
 # Objects come from oracle/ref/build_ref.sh (oracle/_ref/obj); outputs go
-# ONLY to oracle/_ref/shim/ (git-ignored, never shipped to the GPU box).
+# ONLY to oracle/_ref/ (git-ignored, never shipped to the GPU box):
+#   shim/compton2d_gpu      the reference host + shim over libcompton2d.so
+#   shim/compton2d_standin  the same, linked against oracle/c2d_standin.c
+#                           (the C-ABI over the C oracle in its reference
+#                           mode: runs here, without a GPU)
+#   shim/compton2d_ref      the unmodified reference (its main + every
+#                           object), for the comparison
 set -euo pipefail
 HERE="$(cd "$(dirname "$0")" && pwd)"
 REPO="$(cd "$HERE/../.." && pwd)"
@@ -49,3 +55,19 @@ LIB="$REPO/compton2d_amd"
 "$FC" -o "$OUT/compton2d_gpu" "$OUT/c2d_shim.o" "$OUT/compton2d_mod.o" "$OUT/compton2d.o" $objs \
   -L"$LIB" -lcompton2d -Wl,-rpath,"$LIB" -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
 echo "build_shim: $OUT/compton2d_gpu"
+
+# the stand-in library: the C-ABI symbols the shim calls, over the oracle
+STANDIN="$REF/standin"
+mkdir -p "$STANDIN"
+gcc -O2 -fPIC -ffp-contract=off -fno-fast-math -fno-math-errno -std=gnu11 -w -shared \
+  -o "$STANDIN/libcompton2d.so" "$REPO/oracle/c2d_standin.c" "$REPO/oracle/c2d_oracle.c" \
+  "$REPO/oracle/c2d_fp_oracle.c" -lm
+"$FC" -o "$OUT/compton2d_standin" "$OUT/c2d_shim.o" "$OUT/compton2d_mod.o" "$OUT/compton2d.o" $objs \
+  -L"$STANDIN" -lcompton2d -Wl,-rpath,"$STANDIN" -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
+echo "build_shim: $OUT/compton2d_standin"
+# the unmodified reference
+refobjs=""
+for f in $OBJS; do refobjs="$refobjs $REF/obj/$f.o"; done
+"$FC" -o "$OUT/compton2d_ref" "$OUT/compton2d.o" $refobjs \
+  -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
+echo "build_shim: $OUT/compton2d_ref"

@@ -20,18 +20,26 @@ def main():
     ap.add_argument("--nz", type=int, default=8)
     ap.add_argument("--nr", type=int, default=8)
     ap.add_argument("--vary", action="store_true")
+    ap.add_argument("--mode", choices=("exact", "fast"), default="exact")
     args = ap.parse_args()
+    from compton2d_amd import abi
     c, g, tile = tiled_case(args.nz, args.nr, vary=args.vary)
     g.device = 0
     eng = Engine(g)
     eng.fp_set_config(c.constants())
+    eng.fp_set_mode(abi.FP_FAST if args.mode == "fast" else abi.FP_EXACT)
     r = eng.fp_step(tile["ncycle"], tile["time"], tile["dt"], tile, tile)
     d = np.asarray(r["zone_diag"]).reshape(-1, 8)
     steps = d[:, 5]
-    out = {"zones": len(d), "substeps_mean": float(steps.mean()), "kernel_ms": eng.last_fp_ms(),
+    out = {"mode": args.mode, "zones": len(d), "substeps_mean": float(steps.mean()), "kernel_ms": eng.last_fp_ms(),
            "waves_per_zone": eng.last_fp_waves() if hasattr(eng, "last_fp_waves") else None}
     for i, k in enumerate(("search_cycles", "tridag_cycles", "loop_cycles", "search_calls")):
         out[k + "_per_substep"] = float((d[:, i] / steps).mean())
+    if args.mode == "fast":           # McDonald internals (fp_fast.hip, C2D_FP_PROF)
+        calls = np.maximum(d[:, 3], 1)
+        out["mcd_passes_per_call"] = float((d[:, 4] / calls).mean())
+        out["mcd_loop_cycles_per_call"] = float((d[:, 6] / calls).mean())
+        out["mcd_finish_cycles_per_call"] = float((d[:, 7] / calls).mean())
     print(json.dumps(out))
     eng.close()
 
