@@ -1829,6 +1829,9 @@ extern "C" int c2d_last_kernel_ms(c2d_ctx* c, double* gen0_ms, double* all_ms, i
  * loop forms it, with the argument-independent factors of each term (same
  * c2d_math code and rounding as the kernels).  Built once per context. */
 #define C2D_FP_MEMO_SLOTS (1u << 16)
+/* the fast kernel's table: every zone off the clamp inserts its own chain
+ * values, so it is sized so that probes stay short (16 MB) */
+#define C2D_FPF_MEMO_SLOTS (1u << 20)
 static int ensure_mcd(c2d_ctx* c) {
   if (c->fp_mcd) return C2D_OK;
   std::vector<double> mt((size_t)C2D_FP_MCD_N * 4);
@@ -1852,10 +1855,10 @@ static int ensure_mcd(c2d_ctx* c) {
     HIPCHK(c, dalloc(&c->fp_gb_val, C2D_FP_MEMO_SLOTS));
     HIPCHK(c, hipMemset(c->fp_gb_key, 0, sizeof(unsigned long long) * C2D_FP_MEMO_SLOTS));
     HIPCHK(c, hipMemset(c->fp_gb_val, 0, sizeof(double) * C2D_FP_MEMO_SLOTS));
-    HIPCHK(c, dalloc(&c->fpf_gb_key, C2D_FP_MEMO_SLOTS));
-    HIPCHK(c, dalloc(&c->fpf_gb_val, C2D_FP_MEMO_SLOTS));
-    HIPCHK(c, hipMemset(c->fpf_gb_key, 0, sizeof(unsigned long long) * C2D_FP_MEMO_SLOTS));
-    HIPCHK(c, hipMemset(c->fpf_gb_val, 0, sizeof(double) * C2D_FP_MEMO_SLOTS));
+    HIPCHK(c, dalloc(&c->fpf_gb_key, C2D_FPF_MEMO_SLOTS));
+    HIPCHK(c, dalloc(&c->fpf_gb_val, C2D_FPF_MEMO_SLOTS));
+    HIPCHK(c, hipMemset(c->fpf_gb_key, 0, sizeof(unsigned long long) * C2D_FPF_MEMO_SLOTS));
+    HIPCHK(c, hipMemset(c->fpf_gb_val, 0, sizeof(double) * C2D_FPF_MEMO_SLOTS));
   }
   HIPCHK(c, dalloc(&c->fp_dP, 1));
   return C2D_OK;
@@ -1993,7 +1996,7 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   HIPCHK(c, hipEventRecord(c->ev_g0a, st));
   int rc;
   if (c->fp_mode == C2D_FP_FAST) {
-    P.gb_key = c->fpf_gb_key; P.gb_val = c->fpf_gb_val;
+    P.gb_key = c->fpf_gb_key; P.gb_val = c->fpf_gb_val; P.gb_mask = C2D_FPF_MEMO_SLOTS - 1u;
     HIPCHK(c, hipMemcpyAsync(c->fp_dP, &P, sizeof P, hipMemcpyHostToDevice, st));
     const int bs = c2d_fp_fast_block(nc, 4 * c->n_cu);
     c->last_fp_waves = bs / 64;

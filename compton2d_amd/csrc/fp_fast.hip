@@ -289,6 +289,88 @@ __device__ __forceinline__ double exp_nonpos(double x) {
   return __builtin_ldexp(p, (int)kd);
 }
 
+/* 2^(j/64), j = 0..63, correctly rounded (decimal arithmetic at 50 digits) */
+__constant__ double c_exp2_64[64] = {
+    1, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
+    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
+    1.0905077326652577, 1.1023825833078409, 1.1143867425958924, 1.1265216186082418,
+    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
+    1.189207115002721, 1.2021567314527031, 1.215247359980469, 1.22848053610687,
+    1.241857812073484, 1.2553807570246911, 1.2690509571917332, 1.2828700160787783,
+    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.3396675240533029,
+    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
+    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
+    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
+    1.5422108254079407, 1.5590044002378369, 1.5759808451078865, 1.593142151342267,
+    1.6104903319492543, 1.6280274218573478, 1.6457554781539649, 1.6636765803267364,
+    1.681792830507429, 1.7001063537185235, 1.7186192981224779, 1.7373338352737062,
+    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
+    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
+    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.9784560263879509,
+};
+__shared__ double f_e64[64];
+
+#ifndef C2D_FPF_EXPTAB
+#define C2D_FPF_EXPTAB 1
+#endif
+#ifndef C2D_FPF_ONTHEFLY
+#define C2D_FPF_ONTHEFLY 0
+#endif
+
+/* exp(x), -745 < x <= 0, table-driven: x = (64 m + j) ln2/64 + r with
+ * |r| <= ln2/128, e^x = 2^m 2^(j/64) e^r, e^r by its Taylor polynomial to
+ * degree 5 (truncation < 4e-17); the N chains interleaved as below */
+template <int N>
+__device__ __forceinline__ void exp_nonpos_tab(const double (&x)[N], double (&e)[N]) {
+  double kd[N], r[N], p[N];
+  int ki[N];
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    kd[j] = __builtin_rint(x[j] * 92.332482616893658);            /* 64 / ln2 */
+    r[j] = __builtin_fma(-kd[j], 6.93147180369123816490e-01 / 64.0, x[j]);
+    r[j] = __builtin_fma(-kd[j], 1.90821492927058770002e-10 / 64.0, r[j]);
+    ki[j] = (int)kd[j];
+    p[j] = 1.0 / 120.0;
+  }
+  constexpr double C[5] = {1.0 / 24.0, 1.0 / 6.0, 0.5, 1.0, 1.0};
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+#pragma unroll
+    for (int j = 0; j < N; j++) p[j] = __builtin_fma(p[j], r[j], C[i]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int j = 0; j < N; j++) e[j] = __builtin_ldexp(p[j] * f_e64[ki[j] & 63], ki[j] >> 6);
+}
+
+/* exp_nonpos of N arguments with the N Horner chains interleaved step by
+ * step: one wave per SIMD hides nothing, so N independent dependent chains
+ * in lockstep divide the exposed latency by N (sched_barrier keeps each
+ * step's N FMAs together; the scheduler would otherwise serialise them) */
+template <int N>
+__device__ __forceinline__ void exp_nonpos_n(const double (&x)[N], double (&e)[N]) {
+  double kd[N], r[N], p[N];
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    kd[j] = __builtin_rint(x[j] * 1.4426950408889634);
+    r[j] = __builtin_fma(-kd[j], 6.93147180369123816490e-01, x[j]);
+    r[j] = __builtin_fma(-kd[j], 1.90821492927058770002e-10, r[j]);
+    p[j] = 1.6059043836821613e-10;                       /* 1/13! */
+  }
+  constexpr double C[13] = {2.0876756987868100e-09, 2.5052108385441720e-08, 2.7557319223985893e-07,
+                            2.7557319223985888e-06, 2.4801587301587302e-05, 1.9841269841269841e-04,
+                            1.3888888888888889e-03, 8.3333333333333332e-03, 4.1666666666666664e-02,
+                            1.6666666666666666e-01, 0.5, 1.0, 1.0};
+#pragma unroll
+  for (int i = 0; i < 13; i++) {
+#pragma unroll
+    for (int j = 0; j < N; j++) p[j] = __builtin_fma(p[j], r[j], C[i]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int j = 0; j < N; j++) e[j] = __builtin_ldexp(p[j], (int)kd[j]);
+}
+
 /* one abscissa row through a global (not flat) pointer */
 __device__ __forceinline__ double4 gld4(const double* p) {
   const C2D_GLOBAL double* q = (const C2D_GLOBAL double*)p;
@@ -321,16 +403,26 @@ __device__ __forceinline__ void mcd_pass(Blk<BS>& B, double z, const double4 (&x
   const double dt = 1.001, d = dt - 1.0;
   double v2[TPT], v3[TPT];
   bool st2[TPT], st3[TPT];
+  /* branch-free, so the TPT exp chains interleave: exp of the argument
+   * clamped to the reference's cut, the term zeroed beyond it */
+  double em[TPT], ny[TPT];
 #pragma unroll
   for (int k = 0; k < TPT; k++) {
     const double y = z * x[k].y;
-    v2[k] = 0.0;
-    v3[k] = 0.0;
-    if (y < 2.25e2) {
-      const double em = exp_nonpos(-y);
-      v2[k] = x[k].z * em;
-      v3[k] = x[k].w * em;
-    }
+    ny[k] = -(y < 2.25e2 ? y : 2.25e2);
+  }
+#if C2D_FPF_EXPTAB
+  exp_nonpos_tab<TPT>(ny, em);
+#else
+  exp_nonpos_n<TPT>(ny, em);
+#endif
+#pragma unroll
+  for (int k = 0; k < TPT; k++)
+    if (!(ny[k] > -2.25e2)) em[k] = 0.0;              /* y >= 225: the reference's zero term */
+#pragma unroll
+  for (int k = 0; k < TPT; k++) {
+    v2[k] = x[k].z * em[k];
+    v3[k] = x[k].w * em[k];
     const double tn = x[k].x * dt;
     st2[k] = !(tn < 2.0 || v2[k] > 1.0e-8);
     st3[k] = !(tn < 2.0 || v3[k] > 1.0e-8);
@@ -362,11 +454,35 @@ __device__ void mcdonald23_fast(Blk<BS>& B, double z, const double* __restrict__
 #ifdef C2D_FP_PROF
   const long long pt0 = clock64();
 #endif
+  int n0 = 0;
+#if C2D_FPF_ONTHEFLY
+  /* the abscissa rows computed per term (no table loads): t_n = 1.001^n as
+   * exp(n ln 1.001), the same values to rounding */
+  const double ldt = 9.9950033308342321e-04;          /* ln(1.001) */
+  for (; n0 < C2D_FP_MCD_N; n0 += PASS) {
+#ifdef C2D_FP_PROF
+    if (B.tid == 0) f_pf[0]++;
+#endif
+    double4 x[TPT];
+    double nl[TPT], tt[TPT];
+#pragma unroll
+    for (int k = 0; k < TPT; k++) nl[k] = (double)(n0 + k * BS + B.tid) * ldt;
+    exp_nonpos_tab<TPT>(nl, tt);                       /* valid for these x > 0 too */
+#pragma unroll
+    for (int k = 0; k < TPT; k++) {
+      const double t = tt[k], ts = t * (5.0e-1 * (1.0 + 1.001));
+      const double q = ts * ts - 1.0, rq = __builtin_sqrt(q);
+      x[k] = make_double4(t, ts, q * rq, q * q * rq);
+    }
+    mcd_pass<BS>(B, z, x, s2, s3, run2, run3);
+    guard += PASS;
+    if (!run2 && !run3) break;
+  }
+#else
   const double* row = tab + (size_t)B.tid * 4;
   double4 e[TPT];
 #pragma unroll
   for (int k = 0; k < TPT; k++) e[k] = gld4((row + (size_t)k * BS * 4));
-  int n0 = 0;
   for (; n0 < C2D_FP_MCD_N; n0 += PASS) {
 #ifdef C2D_FP_PROF
     if (B.tid == 0) f_pf[0]++;
@@ -384,6 +500,7 @@ __device__ void mcdonald23_fast(Blk<BS>& B, double z, const double* __restrict__
     guard += PASS;
     if (!run2 && !run3) break;
   }
+#endif
   /* past the table (never reached on the reference's decks) */
   for (; (run2 || run3) && guard <= GUARD_MAX; n0 += PASS) {
     double4 x[TPT];
@@ -446,7 +563,14 @@ __device__ double pcr_solve(Blk<BS>& B, double a, double b, double c, double dd)
         ap = f_pcr[buf][0][i + s]; bp = f_pcr[buf][1][i + s];
         cp = f_pcr[buf][2][i + s]; dp = f_pcr[buf][3][i + s];
       }
-      const double k1 = a / bm, k2 = c / bp;
+      /* a / bm and c / bp through reciprocals: v_rcp_f64 and two Newton
+       * steps each, the two chains side by side (fast mode: < 1 ulp) */
+      double q1 = __builtin_amdgcn_rcp(bm), q2 = __builtin_amdgcn_rcp(bp);
+      q1 = __builtin_fma(__builtin_fma(-bm, q1, 1.0), q1, q1);
+      q2 = __builtin_fma(__builtin_fma(-bp, q2, 1.0), q2, q2);
+      q1 = __builtin_fma(__builtin_fma(-bm, q1, 1.0), q1, q1);
+      q2 = __builtin_fma(__builtin_fma(-bp, q2, 1.0), q2, q2);
+      const double k1 = a * q1, k2 = c * q2;
       const double na = -am * k1, nc = -cp * k2;
       const double nb = b - cm * k1 - ap * k2;
       const double nd = dd - dm * k1 - dp * k2;
@@ -771,7 +895,10 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
     int ks = 0;
     while (up ? gbar > g_av : gbar < g_av) {
       The_new = up ? The_new * F32(1.005) : The_new / F32(1.005);
-      g_av = gamma_bar_m(The_new, ++ks > 2);
+#ifndef C2D_FPF_GLOB
+#define C2D_FPF_GLOB 1
+#endif
+      g_av = gamma_bar_m(The_new, C2D_FPF_GLOB ? true : ++ks > 2);
       if (!up && The_new < 1.0e-2) break;
       if (guard > GUARD_MAX) break;
     }
@@ -882,6 +1009,7 @@ __global__ void __launch_bounds__(BS) c2d_fp_fast_kernel(const FpParams* __restr
     f_pf[0] = f_pf[1] = f_pf[2] = f_pf[3] = 0;
 #endif
     f_eg[0] = c2d_exp_bf(gammln(5.0e-1 + 2.0));
+    for (int j = 0; j < 64; j++) f_e64[j] = c_exp2_64[j];
     f_eg[1] = c2d_exp_bf(gammln(5.0e-1 + 3.0));
   }
   __syncthreads();

@@ -71,6 +71,20 @@ def kernel_registers(lib: Path) -> dict:
     return res
 
 
+def disassemble(lib: Path, pattern: str) -> str:
+    """llvm-objdump of the gfx950 code object holding a kernel whose name contains `pattern`."""
+    for co in gfx950_objects(lib):
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            syms = subprocess.run([str(LLVM / "llvm-readelf"), "-s", f.name], check=True,
+                                  capture_output=True, text=True).stdout
+            if pattern in syms:
+                return subprocess.run([str(LLVM / "llvm-objdump"), "-d", "--no-show-raw-insn", f.name],
+                                      check=True, capture_output=True, text=True).stdout
+    return ""
+
+
 def describe(lib: Path, pattern: str = "") -> str:
     lines = []
     for name, d in sorted(kernel_registers(lib).items()):
@@ -88,7 +102,11 @@ def main(argv=None) -> int:
     ap.add_argument("lib", nargs="?", default=str(Path(__file__).resolve().parents[1] /
                                                   "compton2d_amd" / "libcompton2d.so"))
     ap.add_argument("--kernel", default="")
+    ap.add_argument("--disasm", action="store_true", help="print the ISA of the code object with --kernel")
     a = ap.parse_args(argv)
+    if a.disasm:
+        print(disassemble(Path(a.lib), a.kernel))
+        return 0
     print(describe(Path(a.lib), a.kernel))
     return 0
 

@@ -35,6 +35,13 @@ def main():
            "waves_per_zone": eng.last_fp_waves() if hasattr(eng, "last_fp_waves") else None}
     for i, k in enumerate(("search_cycles", "tridag_cycles", "loop_cycles", "search_calls")):
         out[k + "_per_substep"] = float((d[:, i] / steps).mean())
+    # the zone that bounds the launch (largest loop cycles) and the spread
+    zmax = int(np.argmax(d[:, 2]))
+    out["critical_zone"] = {"zone": zmax, "substeps": float(steps[zmax]), "loop_cycles": float(d[zmax, 2]),
+                            "search_cycles": float(d[zmax, 0]), "tridag_cycles": float(d[zmax, 1]),
+                            "mcd_calls": float(d[zmax, 3])}
+    out["loop_cycles_max_over_mean"] = float(d[:, 2].max() / d[:, 2].mean())
+    out["substeps_max"] = float(steps.max())
     if args.mode == "fast":           # McDonald internals (fp_fast.hip, C2D_FP_PROF)
         calls = np.maximum(d[:, 3], 1)
         out["mcd_passes_per_call"] = float((d[:, 4] / calls).mean())

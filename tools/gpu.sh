@@ -83,7 +83,7 @@ for r in "$@"; do
       done ;;
     fppmc)   # kernel trace + SQ counters of the off-clamp FP run (memo on)
       R=$PWD; F=$R/$O/fpprof; mkdir -p "$F"
-      FPB="$R/tools/fp_bench.py --nz 30 --nr 9 --vary --reps 3 --cpu-zones 1"
+      FPB="$R/tools/fp_bench.py --nz 30 --nr 9 --vary --reps 3 --cpu-zones 1 --mode ${FPMODE:-exact}"
       ( cd /tmp && export TMPDIR=/tmp &&
         timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$F/kt" -o run --output-format csv -- \
             python3 $FPB > "$F/kt.out" 2> "$F/kt.err" &&
