@@ -37,7 +37,7 @@ FP_EXACT, FP_FAST = 0, 1   # c2d_fp_set_mode
 ERRORS = {
     0: "C2D_OK", -1: "C2D_E_ARG", -2: "C2D_E_HIP", -3: "C2D_E_CENSUS_OVERFLOW",
     -4: "C2D_E_EVENT_OVERFLOW", -5: "C2D_E_QUEUE_OVERFLOW", -6: "C2D_E_NOMEM",
-    -7: "C2D_E_STATE", -9: "C2D_E_RCCL",
+    -7: "C2D_E_STATE", -8: "C2D_E_FP", -9: "C2D_E_RCCL", -10: "C2D_E_IO",
 }
 
 PD = C.POINTER(C.c_double)

@@ -314,6 +314,11 @@ struct FpParams {
   unsigned long long* gb_key;
   double* gb_val;
   uint32_t gb_mask;        /* slots - 1 (power of two)                         */
+  /* fast kernel only: zones taken from a queue, zorder[q] the q-th zone
+   * (costliest first, from the previous update's sub-step counts) */
+  const int32_t* zorder;   /* [ncell] or null: q-th zone = q                  */
+  int32_t* zq;             /* queue head, zeroed before the launch            */
+  int32_t ncell;
 };
 
 /* ---- observer-frame binning (observe.hip) ---- */

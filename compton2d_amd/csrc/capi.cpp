@@ -19,6 +19,7 @@
 #include "c2d_device.hpp"
 #include "c2d_math.h"
 #include "c2d_rng.h"
+#include "pspt_host.h"
 
 using namespace c2d;
 
@@ -44,7 +45,7 @@ extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
                                       double* tab, int ncell, hipStream_t s);
 extern "C" int c2d_launch_fp(const FpParams* P, int ncell, int waves, hipStream_t s);
-extern "C" int c2d_launch_fp_fast(const FpParams* dP, int ncell, int block, hipStream_t s);
+extern "C" int c2d_launch_fp_fast(const FpParams* dP, int ncell, int block, int grid, hipStream_t s);
 extern "C" int c2d_fp_fast_block(int ncell, int n_simd);
 extern "C" int c2d_fp_waves(int ncell, int n_simd);
 extern "C" int c2d_launch_vem(const VemParams* P, int ncell, hipStream_t s);
@@ -210,6 +211,9 @@ struct c2d_ctx {
   unsigned long long* fpf_gb_key = nullptr;  /* the fast kernel's own gamma_bar memo */
   double* fpf_gb_val = nullptr;
   FpParams* fp_dP = nullptr;                 /* FpParams in device memory (fast kernel) */
+  int32_t* fpf_zq = nullptr;                 /* fast kernel: zone queue head + order [1 + ncell] */
+  std::vector<int32_t> fpf_order;            /* zones by the last update's sub-steps, costliest first */
+  bool fpf_ordered = false;                  /* fpf_order holds a measured order */
   float last_fp_ms = 0.f;
   int last_fp_waves = 0;
   /* emission / absorption tables (c2d_volume_em) */
@@ -220,6 +224,8 @@ struct c2d_ctx {
   bool obs_ready = false;
   ObsDev obs;
   double *obs_edges = nullptr, *obs_hist = nullptr, *obs_ev = nullptr;
+  c2d_pspt_deck pspt;                         /* c2d_obs_begin_pspt's deck */
+  bool pspt_on = false;
   int64_t obs_ev_cap = 0;
   int obs_wg_per_cu = 1;
   double obs_ms = 0.0;
@@ -491,7 +497,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
     if (q) (void)hipFree(q);
   void* fptrs[] = {c->fp_FT, c->fp_mcd, c->fp_zin, c->fp_fin, c->fp_Pin, c->fp_nf, c->fp_fout, c->fp_Pout,
                    c->fp_zout, c->fp_err, c->fp_gb_key, c->fp_gb_val, c->fpf_gb_key, c->fpf_gb_val,
-                   c->fp_dP};
+                   c->fp_dP, c->fpf_zq};
   for (void* p : fptrs)
     if (p) (void)hipFree(p);
   c->pk.release();
@@ -1861,6 +1867,9 @@ static int ensure_mcd(c2d_ctx* c) {
     HIPCHK(c, hipMemset(c->fpf_gb_val, 0, sizeof(double) * C2D_FPF_MEMO_SLOTS));
   }
   HIPCHK(c, dalloc(&c->fp_dP, 1));
+  HIPCHK(c, dalloc(&c->fpf_zq, (size_t)c->ncell + 1));
+  c->fpf_order.resize(c->ncell);
+  for (int q = 0; q < c->ncell; q++) c->fpf_order[q] = q;
   return C2D_OK;
 }
 
@@ -1993,14 +2002,28 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   P.P_out = c->fp_Pout;
   P.zout = c->fp_zout; P.err = c->fp_err;
   P.gb_key = c->fp_gb_key; P.gb_val = c->fp_gb_val; P.gb_mask = C2D_FP_MEMO_SLOTS - 1u;
+  if (c->fp_mode == C2D_FP_FAST) {
+    P.gb_key = c->fpf_gb_key; P.gb_val = c->fpf_gb_val; P.gb_mask = C2D_FPF_MEMO_SLOTS - 1u;
+    /* zones from a queue, costliest first (by the last update's sub-step
+     * counts), on one workgroup per CU (C2D_FPF_GRID: another grid size,
+     * 0 = one workgroup per zone) */
+    P.zq = c->fpf_zq;
+    P.zorder = c->fpf_zq + 1;
+    P.ncell = (int32_t)nc;
+    HIPCHK(c, hipMemcpyAsync(c->fpf_zq + 1, c->fpf_order.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemsetAsync(c->fpf_zq, 0, sizeof(int32_t), st));
+    HIPCHK(c, hipMemcpyAsync(c->fp_dP, &P, sizeof P, hipMemcpyHostToDevice, st));
+  }
   HIPCHK(c, hipEventRecord(c->ev_g0a, st));
   int rc;
   if (c->fp_mode == C2D_FP_FAST) {
-    P.gb_key = c->fpf_gb_key; P.gb_val = c->fpf_gb_val; P.gb_mask = C2D_FPF_MEMO_SLOTS - 1u;
-    HIPCHK(c, hipMemcpyAsync(c->fp_dP, &P, sizeof P, hipMemcpyHostToDevice, st));
     const int bs = c2d_fp_fast_block(nc, 4 * c->n_cu);
+    /* before any order is known: every zone at once (one workgroup each) */
+    const char* ge = getenv("C2D_FPF_GRID");
+    int grid = ge ? atoi(ge) : (c->fpf_ordered ? c->n_cu : 0);
+    if (grid <= 0) grid = (int)nc;
     c->last_fp_waves = bs / 64;
-    rc = c2d_launch_fp_fast(c->fp_dP, nc, bs, st);
+    rc = c2d_launch_fp_fast(c->fp_dP, nc, bs, grid, st);
   } else {
     c->last_fp_waves = c2d_fp_waves(nc, 4 * c->n_cu);
     rc = c2d_launch_fp(&P, nc, c->last_fp_waves, st);
@@ -2021,6 +2044,13 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   if (herr & FPERR_STEPS)
     return fail(c, C2D_E_FP, "FP sub-step limit exceeded (reference stops, update2d.f:585-599)");
   if (herr & FPERR_GUARD) return fail(c, C2D_E_FP, "FP temperature/McDonald iteration guard tripped");
+  if (c->fp_mode == C2D_FP_FAST) {      /* next update's queue order: most sub-steps first */
+    std::vector<int32_t>& o = c->fpf_order;
+    std::stable_sort(o.begin(), o.end(), [&](int32_t a, int32_t b) {
+      return zout[(size_t)a * FO_N + FO_DIAG + C2D_FP_STEPS] > zout[(size_t)b * FO_N + FO_DIAG + C2D_FP_STEPS];
+    });
+    c->fpf_ordered = true;
+  }
   if (el_dev) {
     HIPCHK(c, hipMemcpyAsync(c->f_nt, c->fp_fout, nt_bytes, hipMemcpyDeviceToDevice, st));
     HIPCHK(c, hipMemcpyAsync(c->Pnt, c->fp_Pout, nt_bytes, hipMemcpyDeviceToDevice, st));
@@ -2338,6 +2368,60 @@ extern "C" int c2d_obs_result(c2d_ctx* c, double* F, double* F2, double* count, 
   if (F2) HIPCHK(c, hipMemcpy(F2, c->obs.F2, nh * sizeof(double), hipMemcpyDeviceToHost));
   if (count) HIPCHK(c, hipMemcpy(count, c->obs.cnt, nh * sizeof(double), hipMemcpyDeviceToHost));
   if (kernel_ms) *kernel_ms = c->obs_ms;
+  return C2D_OK;
+}
+
+/* pspt's dialogue -> the SED binning (postprocessing/pspt.c:105-205) */
+extern "C" int c2d_obs_begin_pspt(c2d_ctx* c, const char* deck) {
+  if (!c) return C2D_E_ARG;
+  c2d_pspt_deck d;
+  if (c2d_pspt_parse(deck ? deck : "", &d))
+    return fail(c, C2D_E_ARG, "c2d_obs_begin_pspt: the deck's grid has no bins or more than %d energy channels",
+                C2D_PSPT_CHMAX);
+  c2d_obs_bins b;
+  b.mode = C2D_OBS_SED; b.gam_bulk = d.gam_bulk; b.rmax = d.rmax; b.t_offset = 0.0;
+  b.n_t = d.n_t; b.t0 = d.t0; b.t1 = d.t1;
+  b.n_mu = 1; b.mu0 = &d.mu0; b.mu1 = &d.mu1;
+  b.n_e = d.n_e; b.E0 = d.E0; b.E1 = d.E1;
+  const int rc = c2d_obs_begin(c, &b);
+  if (rc != C2D_OK) return rc;
+  c->pspt = d;
+  c->pspt_on = true;
+  return C2D_OK;
+}
+
+/* pspt's output file from the histogram so far (postprocessing/pspt.c:323-353);
+ * world_sum: summed over the context's communicator first (every rank calls,
+ * rank 0 writes) */
+extern "C" int c2d_obs_write_pspt(c2d_ctx* c, const char* path, int32_t factor, int32_t world_sum) {
+  if (!c) return C2D_E_ARG;
+  if (!c->pspt_on || !c->obs_ready) return fail(c, C2D_E_STATE, "c2d_obs_write_pspt: c2d_obs_begin_pspt first");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const size_t nh = (size_t)c->obs.n_t * c->obs.n_e;
+  std::vector<double> F(nh), cnt(nh);
+  if (world_sum) {
+    if (!c->comm) return fail(c, C2D_E_STATE, "c2d_obs_write_pspt: world_sum needs c2d_comm_init");
+    double* w = nullptr;
+    HIPCHK(c, dalloc(&w, 2 * nh));
+    HIPCHK(c, hipMemcpyAsync(w, c->obs.F, nh * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(w + nh, c->obs.cnt, nh * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    const ncclResult_t r = ncclAllReduce(w, w, 2 * nh, ncclDouble, ncclSum, c->comm, c->stream);
+    if (r != ncclSuccess) {
+      (void)hipFree(w);
+      return fail(c, C2D_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+    }
+    HIPCHK(c, hipMemcpyAsync(F.data(), w, nh * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(cnt.data(), w + nh, nh * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(w);
+    if (c->comm_rank != 0) return C2D_OK;
+  } else {
+    const int rc = c2d_obs_result(c, F.data(), nullptr, cnt.data(), nullptr);
+    if (rc != C2D_OK) return rc;
+  }
+  const char* out = (path && path[0]) ? path : c->pspt.outfile;
+  if (c2d_pspt_write(out, &c->pspt, F.data(), cnt.data(), factor))
+    return fail(c, C2D_E_IO, "c2d_obs_write_pspt: cannot write '%s'", out);
   return C2D_OK;
 }
 

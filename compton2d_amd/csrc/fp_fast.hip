@@ -53,7 +53,7 @@ constexpr int WMAXF = 8;                      /* waves per zone at most (BS = 51
 
 /* zone state in LDS (namespace scope: ds_* accesses) */
 __shared__ double f_gnt[NT + 2], f_gam[NT + 2], f_fold[NT + 2], f_fnew[NT + 2];
-__shared__ double f_dgic[NT + 2], f_dgdt[NT + 2], f_disp[NT + 2], f_inj[NT + 2];
+__shared__ double f_dgic[NT + 2], f_dgdt[NT + 2], f_disp[NT + 2];
 __shared__ double f_bigW[NT + 2], f_bigC[NT + 2], f_em[NT + 2], f_Pnt[NT + 2], f_nf[NPH];
 __shared__ double f_pcr[2][4][256];          /* PCR rows a, b, c, d (double-buffered) */
 __shared__ double f_red[2][2][WMAXF];        /* block reductions: [slot][value][wave] */
@@ -187,6 +187,34 @@ struct Blk {
       b = f_ired[islot][1][w] < b ? f_ired[islot][1][w] : b;
     }
     islot ^= 1;
+  }
+  /* scan() of v together with the block sum of w, behind the same barrier */
+  __device__ __forceinline__ double scan_sum(double v, double& total, double& w) {
+    v = v + dpp<0x111>(v);
+    v = v + dpp<0x112>(v);
+    v = v + dpp<0x114>(v);
+    v = v + dpp<0x118>(v);
+    const double r0 = rl(v, 15), r1 = rl(v, 31), r2 = rl(v, 47);
+    const int row = lane >> 4;
+    if (row == 1) v = v + r0;
+    if (row == 2) v = v + (r0 + r1);
+    if (row == 3) v = v + ((r0 + r1) + r2);
+    w = wsum(w);
+    if (lane == FPB - 1) f_red[slot][0][wave] = v;
+    if (lane == 0) f_red[slot][1][wave] = w;
+    __syncthreads();
+    double before = 0.0, all = 0.0, ws = 0.0;
+#pragma unroll
+    for (int q = 0; q < W; q++) {
+      const double x = f_red[slot][0][q];
+      if (q < wave) before = before + x;
+      all = all + x;
+      ws = ws + f_red[slot][1][q];
+    }
+    slot ^= 1;
+    total = all;
+    w = ws;
+    return before + v;
   }
   /* inclusive prefix sum of v over the threads in tid order, and the total */
   __device__ __forceinline__ double scan(double v, double& total) {
@@ -440,6 +468,37 @@ __device__ __forceinline__ void mcd_pass(Blk<BS>& B, double z, const double4 (&x
   if (f3 != INT_MAX) run3 = false;
 }
 
+/* The terms that cannot stop either series: a term n stops its series when
+ * t_{n+1} >= 2 and sd_n <= 1e-8; sd(t) = (ts^2-1)^a e^{-z ts} is unimodal in
+ * t (log-concave), hence in n, so no n in [n_a, n_lo] stops when sd > 1e-8
+ * at both ends (n_a: the first n with t_{n+1} >= 2). K2's sd (a = 1.5) is
+ * the smaller one there (ts^2 - 1 >= 1), so K2 decides for both. n_lo comes
+ * from the descending root of log sd = ln 1e-7 (fixed-point iteration, a
+ * contraction there), checked on the table's own rows; returned as a whole
+ * number of passes (0 when a check fails). Those passes need no stopping
+ * test and no barrier. */
+constexpr int MCD_NA = 693;                    /* first n with 1.001^(n+1) >= 2 */
+template <int PASS>
+__device__ int mcd_free_terms(double z, const double* __restrict__ tab) {
+  const double s = 5.0e-1 * (1.0 + 1.001), L = 16.11809565095832;   /* -ln 1e-7 */
+  double t = L / z + 2.0;
+#pragma unroll 1
+  for (int it = 0; it < 8; it++) t = (1.5 * c2d_log(t * t * s * s - 1.0) + L) / (z * s);
+  const double tcut = 2.25e2 / (z * s) * 0.999;          /* y >= 225 zeroes a term */
+  if (t > tcut) t = tcut;
+  int n_lo = (int)(c2d_log(t) / 9.9950033308342321e-04) - 2;
+  if (n_lo >= C2D_FP_MCD_N) n_lo = C2D_FP_MCD_N - 1;
+  if (n_lo < MCD_NA + PASS) return 0;
+  const double* a = tab + (size_t)MCD_NA * 4;
+  const double* b = tab + (size_t)n_lo * 4;
+  const double ya = z * a[1], yb = z * b[1];
+  if (!(ya < 2.25e2 && yb < 2.25e2)) return 0;
+  if (!(a[2] * c2d_exp_bf(-ya) > 1.0e-8 && b[2] * c2d_exp_bf(-yb) > 1.0e-8)) return 0;
+  int nA = (n_lo + 1) / PASS * PASS;
+  if (nA > C2D_FP_MCD_N - PASS) nA = C2D_FP_MCD_N - PASS;
+  return nA;
+}
+
 /* McDonald K2, K3 (volume2d.f:598-626) by the whole block: TPT*BS terms per
  * pass (TPT per thread, the next pass's abscissa rows loaded ahead), each
  * series' first stopping term by ballot + a block minimum (so exactly the
@@ -483,6 +542,37 @@ __device__ void mcdonald23_fast(Blk<BS>& B, double z, const double* __restrict__
   double4 e[TPT];
 #pragma unroll
   for (int k = 0; k < TPT; k++) e[k] = gld4((row + (size_t)k * BS * 4));
+#ifndef C2D_FPF_FREE
+#define C2D_FPF_FREE 1
+#endif
+#if C2D_FPF_FREE
+  /* the passes that cannot hold a stopping term: summed without the test */
+  const int nA = mcd_free_terms<PASS>(z, tab);
+  {
+    const double d = 1.001 - 1.0;
+    for (; n0 < nA; n0 += PASS) {
+      double4 x[TPT];
+#pragma unroll
+      for (int k = 0; k < TPT; k++) x[k] = e[k];
+#pragma unroll
+      for (int k = 0; k < TPT; k++) e[k] = gld4((row + (size_t)(n0 + PASS + k * BS) * 4));
+      double em[TPT], ny[TPT];
+#pragma unroll
+      for (int k = 0; k < TPT; k++) ny[k] = -(z * x[k].y);   /* < 225 below n_lo */
+#if C2D_FPF_EXPTAB
+      exp_nonpos_tab<TPT>(ny, em);
+#else
+      exp_nonpos_n<TPT>(ny, em);
+#endif
+#pragma unroll
+      for (int k = 0; k < TPT; k++) {
+        s2 = s2 + d * x[k].x * (x[k].z * em[k]);
+        s3 = s3 + d * x[k].x * (x[k].w * em[k]);
+      }
+    }
+    guard += nA;
+  }
+#endif
   for (; n0 < C2D_FP_MCD_N; n0 += PASS) {
 #ifdef C2D_FP_PROF
     if (B.tid == 0) f_pf[0]++;
@@ -581,11 +671,122 @@ __device__ double pcr_solve(Blk<BS>& B, double a, double b, double c, double dd)
   return own ? dd / b : 0.0;
 }
 
+/* 1/x: v_rcp_f64 and two Newton steps (fast mode: < 1 ulp) */
+__device__ __forceinline__ double rcp_nr(double x) {
+  double q = __builtin_amdgcn_rcp(x);
+  q = __builtin_fma(__builtin_fma(-x, q, 1.0), q, q);
+  return __builtin_fma(__builtin_fma(-x, q, 1.0), q, q);
+}
+
+/* The same system, rows 1..NT (row i in thread i-1, rows past NT identity
+ * rows), by partitions: wave w holds rows 64w+1..64w+64 and reduces its own
+ * block by cyclic reduction across its lanes (cross-lane moves, no barrier)
+ * for three right-hand sides at once, d and the two spikes that couple the
+ * block to the last unknown L of the previous partition and the first
+ * unknown F of the next (x = y - v L_{w-1} - w F_{w+1}); the partitions' edge
+ * rows form a chain over the W-1 interfaces that every thread then solves
+ * for itself, behind one barrier (8 barriers for pcr_solve). */
+__shared__ double f_if[WMAXF][6];
+#ifndef C2D_FPF_SPIKE
+#define C2D_FPF_SPIKE 2
+#endif
+#if C2D_FPF_SPIKE == 2
+__shared__ double2 f_sac[WMAXF][FPB], f_sdv[WMAXF][FPB];   /* (a, c), (d, v) per lane */
+__shared__ double f_sw[WMAXF][FPB];
+#endif
+__device__ __forceinline__ double lane_from(double v, int src) { return __shfl(v, src, FPB); }
+template <int BS>
+__device__ double spike_solve(Blk<BS>& B, double a, double b, double c, double d) {
+  constexpr int W = BS / FPB;
+  const int lane = B.lane, wave = B.wave;
+  double v = (lane == 0) ? a : 0.0;           /* left spike  */
+  double w = (lane == FPB - 1) ? c : 0.0;     /* right spike */
+  if (lane == 0) a = 0.0;
+  if (lane == FPB - 1) c = 0.0;
+  /* unit diagonal: row r reads x_r + a x_{r-s} + c x_{r+s} = (d, v, w) */
+  double r = rcp_nr(b);
+  a = a * r; c = c * r; d = d * r; v = v * r; w = w * r;
+#if C2D_FPF_SPIKE == 2
+#pragma unroll 1
+#else
+#pragma unroll
+#endif
+  for (int s = 1; s < FPB; s <<= 1) {
+    const int lm = lane - s, lp = lane + s;
+#if C2D_FPF_SPIKE == 2
+    /* through the wave's own LDS rows: the wave's lanes store and then load
+     * in program order, so no barrier (a wavefront fence keeps the order) */
+    f_sac[wave][lane] = make_double2(a, c);
+    f_sdv[wave][lane] = make_double2(d, v);
+    f_sw[wave][lane] = w;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int qm = lm < 0 ? 0 : lm, qp = lp >= FPB ? FPB - 1 : lp;
+    const double2 acm = f_sac[wave][qm], dvm = f_sdv[wave][qm];
+    const double2 acp = f_sac[wave][qp], dvp = f_sdv[wave][qp];
+    double am = acm.x, cm = acm.y, dm = dvm.x, vm = dvm.y, wm = f_sw[wave][qm];
+    double ap = acp.x, cp = acp.y, dp = dvp.x, vp = dvp.y, wp = f_sw[wave][qp];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#else
+    double am = lane_from(a, lm), cm = lane_from(c, lm), dm = lane_from(d, lm);
+    double vm = lane_from(v, lm), wm = lane_from(w, lm);
+    double ap = lane_from(a, lp), cp = lane_from(c, lp), dp = lane_from(d, lp);
+    double vp = lane_from(v, lp), wp = lane_from(w, lp);
+#endif
+    if (lm < 0) am = cm = dm = vm = wm = 0.0;      /* outside the block: a = 0 there */
+    if (lp >= FPB) ap = cp = dp = vp = wp = 0.0;
+    r = rcp_nr(1.0 - a * cm - c * ap);
+    const double na = -(a * am), nc = -(c * cp);
+    d = (d - a * dm - c * dp) * r;
+    v = (v - a * vm - c * vp) * r;
+    w = (w - a * wm - c * wp) * r;
+    a = na * r;
+    c = nc * r;
+  }
+  if (lane == 0) {
+    f_if[wave][0] = d; f_if[wave][1] = v; f_if[wave][2] = w;
+  }
+  if (lane == FPB - 1) {
+    f_if[wave][3] = d; f_if[wave][4] = v; f_if[wave][5] = w;
+  }
+  __syncthreads();
+  /* interfaces p = 1..W-1 carry (L_{p-1}, F_p):
+   *   L_{p-1} = A_p + Bp_p F_p,  F_p = G_p + H_p F_{p+1},  F_W = 0 */
+  double A[W], Bp[W], G[W], H[W], F[W + 1], L[W];
+  A[1] = f_if[0][3];
+  Bp[1] = -f_if[0][5];
+#pragma unroll
+  for (int p = 1; p < W; p++) {
+    const double yf = f_if[p][0], vf = f_if[p][1], wf = f_if[p][2];
+    const double q = rcp_nr(1.0 + vf * Bp[p]);
+    G[p] = (yf - vf * A[p]) * q;
+    H[p] = -(wf * q);
+    if (p + 1 < W) {
+      const double yl = f_if[p][3], vl = f_if[p][4], wl = f_if[p][5];
+      A[p + 1] = yl - vl * (A[p] + Bp[p] * G[p]);
+      Bp[p + 1] = -(vl * Bp[p] * H[p] + wl);
+    }
+  }
+  F[W] = 0.0;
+#pragma unroll
+  for (int p = W - 1; p >= 1; p--) {
+    F[p] = G[p] + H[p] * F[p + 1];
+    L[p - 1] = A[p] + Bp[p] * F[p];
+  }
+  double xl = 0.0, xr = 0.0;
+#pragma unroll
+  for (int p = 0; p < W; p++) {
+    if (p + 1 == wave) xl = L[p];
+    if (p == wave + 1) xr = F[p];
+  }
+  return (B.tid < NT) ? d - v * xl - w * xr : 0.0;
+}
+
 /* FP_calc of one zone (blockIdx.x) by the whole block */
 template <int BS>
-__device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
+__device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, const int cell) {
   const int tid = B.tid;
-  const int cell = blockIdx.x;
   const int j = cell / P.nr + 1, k = cell % P.nr + 1;
   const Geo* G = P.geo;
   const double* zin = P.zin + (size_t)cell * FZ_N;
@@ -669,11 +870,20 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
   /* section timers (tools/fp_prof.py): zone_diag 0 = gamma_bar incl. memo,
    * 1 = PCR solve, 2 = whole sub-step loop, 3 = McDonald pairs computed */
   long long pf_gb = 0, pf_tri = 0, pf_loop0 = clock64(), pf_t0 = 0, pf_mcd = 0;
+  long long pf_sa = 0, pf_sb = 0, pf_sc = 0, pf_s0 = 0;   /* C2D_FP_PROF_SEC sections */
+  long long pm_calls = 0, pm_lds = 0, pm_glob = 0;         /* C2D_FP_PROF_MEMO counts */
 #define PF_BEGIN() pf_t0 = clock64()
 #define PF_END(acc) acc += clock64() - pf_t0
 #else
 #define PF_BEGIN()
 #define PF_END(acc)
+#endif
+#ifdef C2D_FP_PROF_SEC
+#define PS_BEGIN() pf_s0 = clock64()
+#define PS_END(acc) acc += clock64() - pf_s0
+#else
+#define PS_BEGIN()
+#define PS_END(acc)
 #endif
   /* gamma_bar is a pure function of Theta, and a zone's search revisits the
    * lattice values around its temperature sub-step after sub-step: a
@@ -687,6 +897,10 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
   auto gamma_bar_m = [&](double th, bool glob) -> double {
     const uint64_t hb = c2d_bits(th);
     const int slot = (int)((hb ^ (hb >> 17) ^ (hb >> 31)) & (ZMEMO - 1));
+#ifdef C2D_FP_PROF_MEMO
+    pm_calls++;
+    if (f_mth[slot] == th) pm_lds++;
+#endif
     if (f_mth[slot] == th) return f_mgv[slot];
     double g = 0.0;
     if (glob) {
@@ -698,6 +912,9 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
       __syncthreads();
       g = f_red[B.slot][0][0];
       B.slot ^= 1;
+#ifdef C2D_FP_PROF_MEMO
+      if (g != 0.0) pm_glob++;
+#endif
     }
     if (g == 0.0) {
       g = gamma_bar_fast<BS>(B, th, P.mcd, guard);
@@ -718,12 +935,51 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
     return g;
   };
   const double vn = 8.176e-7;
+  /* what does not change between sub-steps, once: the acceleration
+   * dispersion disp and its Chang-Cooper midpoint bigC, the grid factor
+   * Delta_g of the tridiagonal coefficients, and the pick-up injection
+   * profile with its normalisation (the reference recomputes them every
+   * sub-step from the same operands: the same values) */
+  double Delta_g_i = 1.0, inj_prof = 0.0;
+  /* and, as products and reciprocals (fast mode: a few ulp from the
+   * reference's quotients): the synchrotron, acceleration and loop-350
+   * factors of dgdt and hr_nt_A, 1/gamma */
+  const double f_sy = 1.058e-15 * (Bf * Bf) / 8.176e-7;
+  const double sy_i = own ? f_sy * (gi * gi - 1.0) : 0.0;
+  const double rg_i = own ? 1.0 / gi : 0.0;
+  const double base_i = own ? f_dgic[i] + gi / t_acc : 0.0;
+  const double kH_i = (i <= NT - 1) ? gi / t_acc * (f_gam[i + 1] - gi) : 0.0;
+  if (own) {
+    f_disp[i] = gi * gi / t_acc / 2.0;
+    if (P.pick_sw == 1 && i <= NT - 1) {
+      const double x = gi - P.inj_gg;
+      inj_prof = 1.0e2 * c2d_exp_bf(-((x * x) / 2.0 / (P.inj_sigma * P.inj_sigma))) /
+                 (P.inj_sigma * __builtin_sqrt(2.0 * PI_REF));
+    }
+  }
+  __syncthreads();
+  const double bigC_i = (i <= NT - 1) ? (f_disp[i] + f_disp[i + 1]) / 2.0 : 0.0;
+  if (i <= NT - 1) f_bigC[i] = bigC_i;
+  if (i >= 2 && i <= NT - 1) Delta_g_i = __builtin_sqrt(f_gnt[i] / f_gnt[i - 1]) * dgm;
+  const double inj_sum0 = B.sum(inj_prof * dgp);     /* also publishes bigC */
+  /* Chang-Cooper and tridiagonal factors: smw = bigB kS; with kP = 1/(Delta_g
+   * D_gplus), kM = 1/(Delta_g D_gminus): tc = -d_t em_i kP, ta = -d_t bigW_{i-1}
+   * bigC_{i-1} kM, tb = 1 + d_t (bigW_i bigC_i kP + em_{i-1} kM) + d_t/t_esc */
+  double kS = 0.0, kP = 0.0, kM = 0.0, kC = 0.0, kA = 0.0;
+  if (i <= NT - 1) kS = ((i == 1) ? f_gnt[2] - f_gnt[1] : dgp) / bigC_i;
+  if (i >= 2 && i <= NT - 1) {
+    kP = 1.0 / (Delta_g_i * dgp);
+    kM = 1.0 / (Delta_g_i * dgm);
+    kC = bigC_i * kP;
+    kA = f_bigC[i - 1] * kM;
+  }
   for (;;) {
     /* label 200 (:577) */
     PF_BEGIN();
     const double g_av0 = (fp_steps == 0) ? gamma_bar_m(Th_e, true) : g_av_next;
     PF_END(pf_gb);
     double g_av = g_av0;
+    PS_BEGIN();
     const double hr_th_c = (fp_steps == 0)
         ? B.sum((i <= NT - 1) ? -(vn * f_dgic[i] * f_fold[i] * dgp * volume * n_lept) : 0.0)
         : hr_th_c_next;
@@ -734,7 +990,7 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
     const double gamma_R = 2.1e-3 * __builtin_sqrt(n_lept) / (Bf * __builtin_sqrt(g_av));
     const double sT = Th_e + Th_p;
     const double h_T = F32(.79788) * (2. * (sT * sT) + 2.0 * sT + 1.0) /
-                       (c2d_pow(sT, 1.5) * (1.0 + 1.875 * Th_e + .8203 * (Th_e * Th_e)));
+                       (sT * __builtin_sqrt(sT) * (1.0 + 1.875 * Th_e + .8203 * (Th_e * Th_e)));
     const double hr_th_Coul = f_th * 1.7386e-26 * n_p * LNL * h_T * (Tp_flare - Te_new);
     const double yR = gamma_R / g_av;
     const double hr_th_sy = (yR < 100.0) ? -Eloss_sy / (P.dt * c2d_exp_bf(yR)) : 0.0;
@@ -744,24 +1000,23 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
     const double dT_total = 6.25e8 * P.dt * hr_th_total / f_th;
     double f_t_implicit = P.df_implicit * Te_new / fabs(dT_total);
     if (f_t_implicit > P.df_T) f_t_implicit = P.df_T;
-    const double f_sy = 1.058e-15 * (Bf * Bf) / 8.176e-7;
     const double g_thr = 1.0 + 4.0 * Th_e;
     /* dgdt, disp (:880-889, :1035-1049) */
     if (own) {
-      const double y = gamma_R / gi;
-      const double dg_sy = (y < 100.0) ? -(f_sy * (gi * gi - 1.0) / c2d_exp_bf(y)) : -1.0e-50;
-      const double dg_A = gi / t_acc;
-      f_disp[i] = gi * gi / t_acc / 2.0;
-      f_dgdt[i] = dg_sy + f_dgic[i] + dg_A;
+      const double y = gamma_R * rg_i;
+      const double dg_sy = (y < 100.0) ? -(sy_i * c2d_exp_bf(-y)) : -1.0e-50;
+      f_dgdt[i] = dg_sy + base_i;
     }
     /* loop 350 sums */
     double hr_nt_A = 0.0, hr_st_A = 0.0;
     if (i <= NT - 1) {
-      const double v = gi / t_acc * f_fold[i] * (f_gam[i + 1] - gi);
+      const double v = kH_i * f_fold[i];
       hr_nt_A = v;
       hr_st_A = gi > g_thr ? v : 0.0;
     }
-    B.sum2(hr_nt_A, hr_st_A);                          /* also publishes dgdt/disp */
+    B.sum2(hr_nt_A, hr_st_A);                          /* also publishes dgdt */
+    PS_END(pf_sa);
+    PS_BEGIN();
     hr_st_A = hr_st_A * vn * n_lept * volume;
     hr_nt_A = hr_nt_A * vn * n_lept * volume;
     const double heat_total = hr_th_Coul + hr_nt_A;
@@ -782,23 +1037,11 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
     /* injection (:1226-1306) */
     double n_inject = 0.0;
     if (P.pick_sw == 1) {
-      double sv = 0.0;
-      if (i <= NT - 1) {
-        const double x = gi - P.inj_gg;
-        const double v = 1.0e2 * c2d_exp_bf(-((x * x) / 2.0 / (P.inj_sigma * P.inj_sigma))) /
-                         (P.inj_sigma * __builtin_sqrt(2.0 * PI_REF));
-        f_inj[i] = v;
-        sv = v * dgp;
-      }
-      const double inj_sum = B.sum(sv);
+      /* sum_i (inj_rho prof_i / inj_sum) dg_i is inj_rho to rounding: the
+       * fast mode takes it so, without the second block sum */
       const double inj_rho = P.pick_rate * d_t;
-      double nv = 0.0;
-      if (i <= NT - 1) {
-        const double v = inj_rho * f_inj[i] / inj_sum;
-        f_fold[i] = f_fold[i] + v / ne;
-        nv = v * dgp;
-      }
-      n_inject = n_inject + B.sum(nv);
+      if (i <= NT - 1) f_fold[i] = f_fold[i] + inj_rho * inj_prof / inj_sum0 / ne;
+      n_inject = n_inject + inj_rho;
     }
     if (P.inj_switch != 0) {
       const double tt = P.time + t_fp - P.inj_t;
@@ -837,43 +1080,38 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
     ne = ne * t_esc / (t_esc + d_t);                  /* escape (:1309-1313) */
     n_p = n_p * t_esc / (t_esc + d_t);
     n_lept = n_lept * t_esc / (t_esc + d_t);
+    const double dte = d_t / t_esc;
     /* Chang-Cooper coefficients (:1363-1390) */
     if (i <= NT - 1) {
-      double bigB, Dg;
-      if (i == 1) {
-        bigB = -(f_dgdt[1] + f_dgdt[2]);
-        Dg = f_gnt[2] - f_gnt[1];
-      } else {
-        bigB = -(f_dgdt[i] + f_dgdt[i + 1]) / 2.0;
-        Dg = dgp;
-      }
-      const double bigC = (f_disp[i] + f_disp[i + 1]) / 2.0;
-      const double smw = Dg * bigB / bigC;
+      const double bigB = (i == 1) ? -(f_dgdt[1] + f_dgdt[2]) : -(f_dgdt[i] + f_dgdt[i + 1]) * 0.5;
+      const double smw = bigB * kS;
       f_bigW[i] = smw / (c2d_exp_bf(smw) - 1.0);
-      f_em[i] = bigC * smw / (1.0 - c2d_exp_bf(-smw));
-      f_bigC[i] = bigC;
+      f_em[i] = bigC_i * smw / (1.0 - c2d_exp_bf(-smw));
     }
     __syncthreads();
     double ta = 0.0, tb = 1.0, tc = 0.0;
     if (i >= 2 && i <= NT - 1) {
-      const double D_gminus = dgm, D_gplus = dgp;
-      const double Delta_g = __builtin_sqrt(f_gnt[i] / f_gnt[i - 1]) * D_gminus;
-      tc = -d_t * (f_em[i] / Delta_g / D_gplus);
-      tb = 1.0 + d_t / Delta_g * (f_bigC[i] * f_bigW[i] / D_gplus + f_em[i - 1] / D_gminus) + d_t / t_esc;
-      ta = -d_t / Delta_g * f_bigC[i - 1] * f_bigW[i - 1] / D_gminus;
+      tc = -(d_t * (f_em[i] * kP));
+      tb = 1.0 + d_t * (f_bigW[i] * kC + f_em[i - 1] * kM) + dte;
+      ta = -(d_t * (f_bigW[i - 1] * kA));
     }
+    PS_END(pf_sb);
     /* tridag (:2476-2518) by cyclic reduction; clip u(2..num_nt) (:2512) */
     PF_BEGIN();
+#if C2D_FPF_SPIKE
+    double u = spike_solve<BS>(B, ta, tb, tc, own ? f_fold[i] : 0.0);
+#else
     double u = pcr_solve<BS>(B, ta, tb, tc, own ? f_fold[i] : 0.0);
+#endif
     PF_END(pf_tri);
+    PS_BEGIN();
     if (i >= 2 && u < 0.0) u = 0.0;
     if (i == NT || i == 1) u = 0.0;
     /* Pnt prefix, sum_p, sum_E (:1415-1419) */
-    double tot = 0.0;
+    double tot = 0.0, sE = (i <= NT - 1) ? dgp * gi * u : 0.0;
     const double pv = (i <= NT - 1) ? dgp * u : 0.0;
-    const double pref = B.scan(pv, tot);
+    const double pref = B.scan_sum(pv, tot, sE);      /* one barrier for both */
     sum_p = tot;
-    const double sE = B.sum((i <= NT - 1) ? dgp * gi * u : 0.0);
     if (i <= NT - 1) f_Pnt[i] = pref;
     sum_E = sE / sum_p;
     t_fp = t_fp + d_t;
@@ -887,6 +1125,7 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
     double gbar = (i <= NT - 1) ? gi * fn * dgp : 0.0;
     hr_th_c_next = (i <= NT - 1) ? -(vn * f_dgic[i] * fn * dgp * volume * n_lept) : 0.0;
     B.sum2(gbar, hr_th_c_next);
+    PS_END(pf_sc);
     /* new temperature (:1440-1468) */
     double The_new = Th_e;
     PF_BEGIN();
@@ -994,9 +1233,20 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B) {
     zo[FO_DIAG + 6] = (double)f_pf[1];
     zo[FO_DIAG + 7] = (double)f_pf[2];
 #endif
+#ifdef C2D_FP_PROF_MEMO
+    zo[FO_DIAG + 4] = (double)pm_calls;
+    zo[FO_DIAG + 6] = (double)pm_lds;
+    zo[FO_DIAG + 7] = (double)pm_glob;
+#endif
+#ifdef C2D_FP_PROF_SEC
+    zo[FO_DIAG + 4] = (double)pf_sa;
+    zo[FO_DIAG + 6] = (double)pf_sb;
+    zo[FO_DIAG + 7] = (double)pf_sc;
+#endif
   }
 }
 
+__shared__ int f_zone;
 template <int BS>
 __global__ void __launch_bounds__(BS) c2d_fp_fast_kernel(const FpParams* __restrict__ Pp) {
   const FpParams& P = *Pp;
@@ -1005,15 +1255,27 @@ __global__ void __launch_bounds__(BS) c2d_fp_fast_kernel(const FpParams* __restr
   B.lane = B.tid & (FPB - 1);
   B.wave = B.tid / FPB;
   if (B.tid == 0) {
-#ifdef C2D_FP_PROF
-    f_pf[0] = f_pf[1] = f_pf[2] = f_pf[3] = 0;
-#endif
     f_eg[0] = c2d_exp_bf(gammln(5.0e-1 + 2.0));
     for (int j = 0; j < 64; j++) f_e64[j] = c_exp2_64[j];
     f_eg[1] = c2d_exp_bf(gammln(5.0e-1 + 3.0));
   }
-  __syncthreads();
-  fp_zone_fast<BS>(P, B);
+  /* one zone after another from the queue: a zone's time is its sub-step
+   * count x one latency chain, and the costliest zones come first, each on a
+   * CU of its own; the cheap ones fill in behind the first to finish */
+  for (;;) {
+    if (B.tid == 0) {
+#ifdef C2D_FP_PROF
+      f_pf[0] = f_pf[1] = f_pf[2] = f_pf[3] = 0;
+#endif
+      f_zone = atomicAdd(P.zq, 1);
+    }
+    __syncthreads();
+    const int q = f_zone;
+    __syncthreads();                       /* f_zone is rewritten next round */
+    if (q >= P.ncell) break;
+    fp_zone_fast<BS>(P, B, P.zorder ? P.zorder[q] : q);
+    __syncthreads();
+  }
 }
 
 }  // namespace
@@ -1028,9 +1290,10 @@ __global__ void __launch_bounds__(BS) c2d_fp_fast_kernel(const FpParams* __restr
 extern "C" int c2d_fp_fast_block(int, int) { return C2D_FPF_BS; }
 
 /* dP: the parameters in device memory (uploaded by the caller on `stream`) */
-extern "C" int c2d_launch_fp_fast(const c2d::FpParams* dP, int ncell, int block, hipStream_t stream) {
+extern "C" int c2d_launch_fp_fast(const c2d::FpParams* dP, int ncell, int block, int grid, hipStream_t stream) {
   if (ncell <= 0) return 0;
-  if (block != C2D_FPF_BS) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(c2d::c2d_fp_fast_kernel<C2D_FPF_BS>, dim3(ncell), dim3(C2D_FPF_BS), 0, stream, dP);
+  if (block != C2D_FPF_BS || grid <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(c2d::c2d_fp_fast_kernel<C2D_FPF_BS>, dim3(grid < ncell ? grid : ncell), dim3(C2D_FPF_BS), 0,
+                     stream, dP);
   return (int)hipGetLastError();
 }

@@ -129,6 +129,10 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_obs_accumulate_device.argtypes = [vp, C.c_void_p, C.c_int64]
     lib.c2d_obs_result.restype = C.c_int
     lib.c2d_obs_result.argtypes = [vp] + [C.POINTER(C.c_double)] * 4
+    lib.c2d_obs_begin_pspt.restype = C.c_int
+    lib.c2d_obs_begin_pspt.argtypes = [vp, C.c_char_p]
+    lib.c2d_obs_write_pspt.restype = C.c_int
+    lib.c2d_obs_write_pspt.argtypes = [vp, C.c_char_p, C.c_int32, C.c_int32]
     lib.c2d_electron_state.restype = C.c_int
     lib.c2d_electron_state.argtypes = [vp, abi.MArray3, abi.MArray3]
     lib.c2d_comm_unique_id.restype = C.c_int
@@ -441,6 +445,16 @@ class Engine:
                                             F2.ctypes.data_as(abi.PD),
                                             cnt.ctypes.data_as(abi.PD), C.byref(ms)))
         return F, F2, cnt, ms.value
+
+    def obs_begin_pspt(self, deck: str = "") -> None:
+        """The SED binning of pspt's input dialogue `deck` (c2d_obs_begin_pspt)."""
+        from . import observer
+        self._obs = observer.parse_pspt_deck(deck)
+        self._check(self.lib.c2d_obs_begin_pspt(self.ctx, deck.encode()))
+
+    def obs_write_pspt(self, path: str = "", factor: int = 0, world_sum: bool = False) -> None:
+        """Write pspt's output file from the histogram so far (c2d_obs_write_pspt)."""
+        self._check(self.lib.c2d_obs_write_pspt(self.ctx, str(path).encode(), int(factor), int(world_sum)))
 
     def fp_tridag(self, a, b, c, r, x0=None) -> np.ndarray:
         """Batched tridag (src/update2d.f:2476-2518); arrays [ncell, nt]."""

@@ -29,13 +29,22 @@ c     tallies are ADDED into its COMMON exactly where the reference's
 c     workers accumulate them (edep, prdep, ecens, npcen, n_field, E_IC,
 c     nelectron, fout, edout, erlk*, Ed_in), so xec_add,
 c     graphics_collect, cens_add_up and E_add_up reduce them unchanged;
-c     escape events go to the worker's event file (unit nunit_evt, the
-c     reference's format, src/imcleak2d.f:171,181); the census is mirrored
+c     escape events are binned on the GPU into the time-resolved SED of
+c     the post-processing tool pspt (postprocessing/pspt.c: its binning
+c     from its own input deck, its output file, rewritten every step;
+c     N workers: summed over them inside the C-ABI) instead of being
+c     written as text -- or, opted in, written to the worker's event file
+c     (unit nunit_evt, the reference's format, src/imcleak2d.f:171,181)
+c     for the stand-alone tools; the census is mirrored
 c     into dbufout/ibufout/ndxout for write_record (src/census2d.f) when
 c     it fits ucens, and imported from them after read_record.
 c
 c     Environment: C2D_SHIM_EXACT=1 (exact comtot build),
-c     C2D_SHIM_CENSUS_CAPACITY=n, C2D_SHIM_EVENTS=0 (no event file),
+c     C2D_SHIM_CENSUS_CAPACITY=n,
+c     C2D_SHIM_SED_DECK=path (pspt's input deck, e.g.
+c     postprocessing/mrk421_sed.input; unset: pspt's defaults),
+c     C2D_SHIM_SED=0 (no on-device SED),
+c     C2D_SHIM_EVENTS=1 (also write the event file),
 c     C2D_SHIM_CENSUS_MIRROR=0 (no dbufout mirror),
 c     C2D_SHIM_ALLREDUCE=0 (N workers: no all-reduce inside the C-ABI;
 c     every worker deposits its own tallies into COMMON instead).
@@ -58,7 +67,9 @@ c     (2*jmax + 2*kmax slots x 5 tables of nfmax)
       real(c_double), target, save :: sptab(shm_nf, 5, shm_nslot)
       integer(c_int32_t), target, save :: sidx_i(99), sidx_o(99),
      1     sidx_u(99), sidx_l(99)
-      integer, save :: ev_on = 1, mirror_on = 1, warned = 0
+      integer, save :: ev_on = 0, mirror_on = 1, warned = 0
+c     the on-device SED (c2d_obs_begin_pspt / c2d_obs_write_pspt)
+      integer, save :: sed_on = 1
       logical, save :: static_done = .false.
 c     the run's lineage seed: the master's rseed, the same on every
 c     worker (setup_bcast leaves each worker rseed + myid*84725,
@@ -177,7 +188,7 @@ c
       use compton2d
       use c2d_shim_state, only: tctx, tready, lay, tal, spec, sptab,
      1     sidx_i, sidx_o, sidx_u, sidx_l, ev_on, mirror_on, warned,
-     2     static_done, seed0, ar_on, commid
+     2     static_done, seed0, ar_on, commid, sed_on
       implicit none
       include 'mpif.h'
       include 'general.pa'
@@ -349,8 +360,15 @@ c     ---- worker: one GPU context, lineage shard myid-1 of numprocs-1
      1        ccap, ecap, qcap)
          rc = c2d_tally_layout_get(tctx, lay)
          allocate(tal(lay%total))
-         ev_on = int(c2d_shim_env('C2D_SHIM_EVENTS', 1_8))
+         ev_on = int(c2d_shim_env('C2D_SHIM_EVENTS', 0_8))
          mirror_on = int(c2d_shim_env('C2D_SHIM_CENSUS_MIRROR', 1_8))
+         sed_on = int(c2d_shim_env('C2D_SHIM_SED', 1_8))
+c        N workers without the all-reduce cannot sum one SED: events
+         if (sed_on .eq. 1 .and. nw .gt. 1 .and. ar_on .ne. 1) then
+            sed_on = 0
+            ev_on = 1
+         endif
+         if (sed_on .eq. 1) call c2d_shim_sed_begin(tctx)
 c        restart: census records read by read_record (census2d.f)
          if (ndxout .gt. 0) then
             allocate(i5(5, ndxout), keys(ndxout))
@@ -512,6 +530,19 @@ c     carry zeros from every other worker.
          Ed_in(k) = Ed_in(k) + tal(lay%Ed_in + k)
  58   continue
 c
+c     escape events -> the SED on the device, rewritten every step (N
+c     workers: summed over them; worker 1 writes)
+      if (sed_on .eq. 1 .and. ncycle .gt. 0) then
+         rc = c2d_obs_accumulate(tctx, c_null_ptr, 0_c_int64_t)
+         if (rc .ne. C2D_OK) call c2d_shim_fail(tctx,
+     1        'c2d_obs_accumulate', rc)
+c        factor 1: what pspt prints for one series p001..pNNN_evb.dat
+c        (pspt.c:222-238 counts the series end that is not p001)
+         rc = c2d_obs_write_pspt(tctx, c_null_char, 1_c_int32_t,
+     1        int(ar_on, c_int32_t))
+         if (rc .ne. C2D_OK) call c2d_shim_fail(tctx,
+     1        'c2d_obs_write_pspt', rc)
+      endif
 c     escape events -> this worker's event file (imcleak2d.f:171,181)
       if (ev_on .eq. 1 .and. ncycle .gt. 0) then
          rc = c2d_events(tctx, tal, 0_c_int64_t, nev)
@@ -548,6 +579,46 @@ c     6 f64 + 6 i32 per record, the 6th the record's seed)
             warned = 1
          endif
       endif
+      end
+c
+c
+c     the SED binning from pspt's input deck (C2D_SHIM_SED_DECK: a file
+c     with one answer a line; unset: every default of pspt)
+      subroutine c2d_shim_sed_begin(ctx)
+      use iso_c_binding
+      use compton2d
+      implicit none
+      type(c_ptr) ctx
+      character(kind=c_char, len=4096) :: deck
+      character*512 fname, line
+      integer st, u, ios, n, l
+      integer(c_int) rc
+      deck = ' '
+      n = 0
+      call get_environment_variable('C2D_SHIM_SED_DECK', fname,
+     1     status=st)
+      if (st .eq. 0 .and. len_trim(fname) .gt. 0) then
+         open(newunit=u, file=trim(fname), status='old', iostat=ios)
+         if (ios .ne. 0) then
+            write(*,*) 'c2d_shim: cannot open ', trim(fname)
+            call c2d_shim_fail(c_null_ptr, 'C2D_SHIM_SED_DECK', -1)
+         endif
+ 10      read(u, '(a)', iostat=ios) line
+         if (ios .eq. 0) then
+            l = len_trim(line)
+            if (n + l + 1 .lt. len(deck)) then
+               if (l .gt. 0) deck(n+1:n+l) = line(1:l)
+               deck(n+l+1:n+l+1) = char(10)
+               n = n + l + 1
+            endif
+            goto 10
+         endif
+         close(u)
+      endif
+      deck(n+1:n+1) = c_null_char
+      rc = c2d_obs_begin_pspt(ctx, deck)
+      if (rc .ne. C2D_OK) call c2d_shim_fail(ctx, 'c2d_obs_begin_pspt',
+     1     rc)
       end
 c
 c

@@ -63,6 +63,7 @@ extern "C" {
 #define C2D_E_FP               -8   /* FP sub-step limit (reference `stop`,
                                        src/update2d.f:585-599) or a solver guard  */
 #define C2D_E_RCCL             -9   /* RCCL (communicator / all-reduce) error     */
+#define C2D_E_IO              -10   /* a file could not be written                */
 
 /* comtot (src/comtot2d.f:1-334, icoms=6) evaluation mode. */
 #define C2D_COMTOT_EXACT  0   /* 199-term electron-spectrum sum per call (reference)   */
@@ -443,6 +444,18 @@ int  c2d_obs_accumulate_device(c2d_ctx* ctx, const double* d_events, int64_t n);
 /* Download the raw sums ([n_t][n_mu][n_e] each; any pointer may be NULL)
  * and the device time of the binning launches so far (ms). */
 int  c2d_obs_result(c2d_ctx* ctx, double* F, double* F2, double* count, double* kernel_ms);
+/* The SED tool's binning from its own input dialogue: `deck` is pspt's stdin
+ * (one answer a line, an empty line keeps pspt's default, "" or NULL = all
+ * defaults; e.g. postprocessing/mrk421_sed.input), parsed and turned into
+ * edges with pspt's arithmetic (postprocessing/pspt.c:105-205), then
+ * c2d_obs_begin.  Replaces writing p###_evb.dat and running pspt on it. */
+int  c2d_obs_begin_pspt(c2d_ctx* ctx, const char* deck);
+/* Write pspt's output file (pspt.c:323-353, byte for byte its format) from
+ * the histogram so far: `path` (NULL/"" = the deck's output file name),
+ * `factor` as pspt's "#factor" line.  world_sum != 0: the histograms of every
+ * rank of the context's communicator are summed first (RCCL; every rank
+ * calls, rank 0 writes). */
+int  c2d_obs_write_pspt(c2d_ctx* ctx, const char* path, int32_t factor, int32_t world_sum);
 
 /* Copy the context's device electron state (C2D_DEV_ELECTRONS) into the
  * caller's f_nt / Pnt views (either may have NULL data), e.g. before

@@ -12,7 +12,7 @@ module compton2d
 
   integer(c_int), parameter :: C2D_OK = 0, C2D_E_ARG = -1, C2D_E_HIP = -2, &
        C2D_E_CENSUS_OVERFLOW = -3, C2D_E_EVENT_OVERFLOW = -4, C2D_E_QUEUE_OVERFLOW = -5, &
-       C2D_E_NOMEM = -6, C2D_E_STATE = -7, C2D_E_FP = -8, C2D_E_RCCL = -9
+       C2D_E_NOMEM = -6, C2D_E_STATE = -7, C2D_E_FP = -8, C2D_E_RCCL = -9, C2D_E_IO = -10
   ! c2d_step_in%device_tables flags; RCCL unique-id size (c2d_comm_unique_id)
   integer(c_int32_t), parameter :: C2D_DEV_EMISSION = 1, C2D_DEV_ELECTRONS = 2
   integer, parameter :: C2D_COMM_ID_BYTES = 128
@@ -279,6 +279,23 @@ module compton2d
        type(c_ptr), value :: ctx, F, F2, cnt       ! [n_e, n_mu, n_t] in Fortran order
        real(c_double), intent(out) :: kernel_ms
      end function c2d_obs_result
+
+     ! pspt's dialogue (one answer a line, C string) -> the SED binning
+     integer(c_int) function c2d_obs_begin_pspt(ctx, deck) bind(C, name='c2d_obs_begin_pspt')
+       import :: c_int, c_ptr, c_char
+       type(c_ptr), value :: ctx
+       character(kind=c_char), intent(in) :: deck(*)   ! NUL-terminated
+     end function c2d_obs_begin_pspt
+
+     ! pspt's output file from the histogram so far (path NUL-terminated,
+     ! empty = the deck's name); world_sum: summed over the communicator
+     integer(c_int) function c2d_obs_write_pspt(ctx, path, factor, world_sum) &
+          bind(C, name='c2d_obs_write_pspt')
+       import :: c_int, c_ptr, c_char, c_int32_t
+       type(c_ptr), value :: ctx
+       character(kind=c_char), intent(in) :: path(*)
+       integer(c_int32_t), value :: factor, world_sum
+     end function c2d_obs_write_pspt
 
      ! ---- RCCL tally all-reduce (replaces xec_add / graphics_collect,
      !      src/xec2d.f:325-399, and cens_add_up / E_add_up,

@@ -41,6 +41,7 @@
 #include <unistd.h>
 
 #include "../include/compton2d.h"
+#include "../compton2d_amd/csrc/pspt_host.h"   /* the product's pspt dialogue/file code */
 
 typedef struct c2o_ctx c2o_ctx;
 c2o_ctx* c2o_create(const c2d_config* cfg, int rng_mode, int rand_switch, int32_t rseed, int h4_stale);
@@ -55,6 +56,7 @@ int c2o_census_import(c2o_ctx* c, const double* d6, const int32_t* i5, const uin
 void c2o_set_dt_lag(c2o_ctx* c, int on);
 int c2o_fp_step(const c2d_config* g, const c2d_fp_config* fc, const c2d_fp_step_in* in,
                 c2d_fp_step_out* out);
+int c2o_obs_bin(const c2d_obs_bins* b, const double* ev, int64_t n, double* F, double* F2, double* cnt);
 
 enum { RNG_FIB = 1, RNG_LINEAGE = 3 };
 
@@ -69,6 +71,10 @@ struct c2d_ctx {
   int comm_rank, comm_world;
   char comm_id[C2D_COMM_ID_BYTES];
   int64_t comm_round;
+  int64_t obs_round;
+  c2d_pspt_deck pspt;   /* c2d_obs_begin_pspt */
+  int pspt_on;
+  double *oF, *oF2, *ocnt;
   char err[512];
 };
 
@@ -122,6 +128,9 @@ int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
 void c2d_finalize(c2d_ctx* c) {
   if (!c) return;
   if (c->o) c2o_destroy(c->o);
+  free(c->oF);
+  free(c->oF2);
+  free(c->ocnt);
   free(c->fic);
   free(c->T);
   free(c);
@@ -225,21 +234,21 @@ int c2d_comm_init(c2d_ctx* c, const void* id, int32_t rank, int32_t world) {
   return C2D_OK;
 }
 
-int c2d_allreduce_tallies(c2d_ctx* c) {
-  if (!c) return C2D_E_ARG;
-  if (c->comm_world < 1) return fail(c, C2D_E_STATE, "c2d_comm_init must precede c2d_allreduce_tallies");
-  const size_t bytes = sizeof(double) * (size_t)c->L.total;
+/* sum `n` doubles over the group's ranks in rank order, round `round` of
+ * the exchange named `tag` */
+static int file_allreduce(c2d_ctx* c, double* v, int64_t n, const char* tag, int64_t round) {
+  const size_t bytes = sizeof(double) * (size_t)n;
   char path[C2D_COMM_ID_BYTES + 64], tmp[C2D_COMM_ID_BYTES + 64];
-  snprintf(tmp, sizeof tmp, "%s/.r%d.%lld", c->comm_id, c->comm_rank, (long long)c->comm_round);
-  snprintf(path, sizeof path, "%s/r%d.%lld", c->comm_id, c->comm_rank, (long long)c->comm_round);
+  snprintf(tmp, sizeof tmp, "%s/.%s%d.%lld", c->comm_id, tag, c->comm_rank, (long long)round);
+  snprintf(path, sizeof path, "%s/%s%d.%lld", c->comm_id, tag, c->comm_rank, (long long)round);
   FILE* f = fopen(tmp, "wb");
-  if (!f || fwrite(c->T, 1, bytes, f) != bytes || fclose(f)) return fail(c, C2D_E_RCCL, "write %s", tmp);
+  if (!f || fwrite(v, 1, bytes, f) != bytes || fclose(f)) return fail(c, C2D_E_RCCL, "write %s", tmp);
   if (rename(tmp, path)) return fail(c, C2D_E_RCCL, "rename %s", path);
-  double* sum = (double*)calloc((size_t)c->L.total, sizeof(double));
+  double* sum = (double*)calloc((size_t)n, sizeof(double));
   double* buf = (double*)malloc(bytes);
   if (!sum || !buf) return fail(c, C2D_E_NOMEM, "allreduce buffers");
   for (int r = 0; r < c->comm_world; r++) {
-    snprintf(path, sizeof path, "%s/r%d.%lld", c->comm_id, r, (long long)c->comm_round);
+    snprintf(path, sizeof path, "%s/%s%d.%lld", c->comm_id, tag, r, (long long)round);
     for (int tries = 0;; tries++) {
       f = fopen(path, "rb");
       if (f) break;
@@ -258,11 +267,82 @@ int c2d_allreduce_tallies(c2d_ctx* c) {
       free(buf);
       return fail(c, C2D_E_RCCL, "short read %s", path);
     }
-    for (int64_t i = 0; i < c->L.total; i++) sum[i] = sum[i] + buf[i];
+    for (int64_t i = 0; i < n; i++) sum[i] = sum[i] + buf[i];
   }
-  memcpy(c->T, sum, bytes);
+  memcpy(v, sum, bytes);
   free(sum);
   free(buf);
+  return C2D_OK;
+}
+
+int c2d_allreduce_tallies(c2d_ctx* c) {
+  if (!c) return C2D_E_ARG;
+  if (c->comm_world < 1) return fail(c, C2D_E_STATE, "c2d_comm_init must precede c2d_allreduce_tallies");
+  const int rc = file_allreduce(c, c->T, c->L.total, "r", c->comm_round);
+  if (rc) return rc;
   c->comm_round++;
   return C2D_OK;
+}
+
+/* ---- observer-frame SED binning (the oracle's restatement of pspt's loop,
+ * oracle/c2d_obs_oracle.c) with the product's pspt dialogue and file code ---- */
+int c2d_obs_begin_pspt(c2d_ctx* c, const char* deck) {
+  if (!c) return C2D_E_ARG;
+  if (c2d_pspt_parse(deck ? deck : "", &c->pspt)) return fail(c, C2D_E_ARG, "c2d_standin: pspt deck");
+  const size_t nh = (size_t)c->pspt.n_t * c->pspt.n_e;
+  free(c->oF);
+  free(c->oF2);
+  free(c->ocnt);
+  c->oF = (double*)calloc(nh, sizeof(double));
+  c->oF2 = (double*)calloc(nh, sizeof(double));
+  c->ocnt = (double*)calloc(nh, sizeof(double));
+  if (!c->oF || !c->oF2 || !c->ocnt) return fail(c, C2D_E_NOMEM, "c2d_standin: histogram");
+  c->pspt_on = 1;
+  return C2D_OK;
+}
+
+int c2d_obs_accumulate(c2d_ctx* c, const double* events, int64_t n) {
+  if (!c) return C2D_E_ARG;
+  if (!c->pspt_on) return fail(c, C2D_E_STATE, "c2d_standin: c2d_obs_begin_pspt first");
+  double* ev = NULL;
+  if (!events) {                                   /* the last step's events */
+    n = c2o_event_count(c->o);
+    ev = (double*)malloc(sizeof(double) * C2D_EVENT_WORDS * (size_t)(n > 0 ? n : 1));
+    if (!ev) return fail(c, C2D_E_NOMEM, "c2d_standin: events");
+    if (n > 0) c2o_events(c->o, ev, n);
+    events = ev;
+  }
+  c2d_obs_bins b;
+  b.mode = C2D_OBS_SED; b.gam_bulk = c->pspt.gam_bulk; b.rmax = c->pspt.rmax; b.t_offset = 0.0;
+  b.n_t = c->pspt.n_t; b.t0 = c->pspt.t0; b.t1 = c->pspt.t1;
+  b.n_mu = 1; b.mu0 = &c->pspt.mu0; b.mu1 = &c->pspt.mu1;
+  b.n_e = c->pspt.n_e; b.E0 = c->pspt.E0; b.E1 = c->pspt.E1;
+  const int rc = c2o_obs_bin(&b, events, n, c->oF, c->oF2, c->ocnt);
+  free(ev);
+  return rc ? fail(c, rc, "c2d_standin: c2o_obs_bin") : C2D_OK;
+}
+
+int c2d_obs_write_pspt(c2d_ctx* c, const char* path, int32_t factor, int32_t world_sum) {
+  if (!c) return C2D_E_ARG;
+  if (!c->pspt_on) return fail(c, C2D_E_STATE, "c2d_standin: c2d_obs_begin_pspt first");
+  const int64_t nh = (int64_t)c->pspt.n_t * c->pspt.n_e;
+  double* w = (double*)malloc(sizeof(double) * 2 * (size_t)nh);
+  if (!w) return fail(c, C2D_E_NOMEM, "c2d_standin: histogram copy");
+  memcpy(w, c->oF, sizeof(double) * (size_t)nh);
+  memcpy(w + nh, c->ocnt, sizeof(double) * (size_t)nh);
+  if (world_sum) {
+    if (c->comm_world < 1) {
+      free(w);
+      return fail(c, C2D_E_STATE, "c2d_standin: world_sum needs c2d_comm_init");
+    }
+    const int rc = file_allreduce(c, w, 2 * nh, "s", c->obs_round++);
+    if (rc || c->comm_rank != 0) {
+      free(w);
+      return rc;
+    }
+  }
+  const char* out = (path && path[0]) ? path : c->pspt.outfile;
+  const int rc = c2d_pspt_write(out, &c->pspt, w, w + nh, factor);
+  free(w);
+  return rc ? fail(c, C2D_E_IO, "c2d_standin: cannot write %s", out) : C2D_OK;
 }

@@ -61,7 +61,7 @@ STANDIN="$REF/standin"
 mkdir -p "$STANDIN"
 gcc -O2 -fPIC -ffp-contract=off -fno-fast-math -fno-math-errno -std=gnu11 -w -shared \
   -o "$STANDIN/libcompton2d.so" "$REPO/oracle/c2d_standin.c" "$REPO/oracle/c2d_oracle.c" \
-  "$REPO/oracle/c2d_fp_oracle.c" -lm
+  "$REPO/oracle/c2d_fp_oracle.c" "$REPO/oracle/c2d_obs_oracle.c" -lm
 "$FC" -o "$OUT/compton2d_standin" "$OUT/c2d_shim.o" "$OUT/compton2d_mod.o" "$OUT/compton2d.o" $objs \
   -L"$STANDIN" -lcompton2d -Wl,-rpath,"$STANDIN" -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
 echo "build_shim: $OUT/compton2d_standin"

@@ -89,6 +89,10 @@ SHIM_DECK = dict(T_const=0, tstop=2.0e5, nst=1500)
 # files whose every byte the reference writes from state the shim delivers
 SAME_FILES = ("p001_evb.dat", "output/nfield.dat", "output/temp_b.dat", "output/eic.dat",
               "output/seb.dat", "esp.dat")
+PSPT = ROOT / "oracle" / "_ref" / "pspt"
+# pspt's dialogue for this small run: no bulk boost, every direction, the
+# run's whole time range, 100 log channels (postprocessing/pspt.c:105-205)
+SED_DECK = "p001_evb.dat\n1\n1e16\nsed_shim.dat\n30\n0\n2.5e5\n-1\n1\n1\n1e-7\n1e10\n100\n0\nn\n"
 
 
 def _mpirun(exe, case, nproc, env_extra):
@@ -112,14 +116,17 @@ def shim_runs(tmp_path_factory):
                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     from concurrent.futures import ThreadPoolExecutor
     base = tmp_path_factory.mktemp("shim")
+    ev = {"C2D_SHIM_EVENTS": "1"}          # the text events too (the SED is the default)
     runs = {"ref": (REFEXE, 2, {}),
-            "shim": (STANDIN, 2, {"C2D_STANDIN_RSEED": str(refcase.BASE_CASE["rseed"])}),
-            "lin1": (STANDIN, 2, {"C2D_STANDIN_RNG": "lineage"}),
-            "lin2": (STANDIN, 3, {"C2D_STANDIN_RNG": "lineage"})}
+            "shim": (STANDIN, 2, dict(ev, C2D_STANDIN_RSEED=str(refcase.BASE_CASE["rseed"]))),
+            "lin1": (STANDIN, 2, dict(ev, C2D_STANDIN_RNG="lineage")),
+            "lin2": (STANDIN, 3, dict(ev, C2D_STANDIN_RNG="lineage"))}
     dirs = {}
     for k in runs:
         dirs[k] = base / k
         refcase.write_input_deck(dirs[k], SHIM_DECK)
+        (dirs[k] / "sed.input").write_text(SED_DECK)
+        runs[k][2]["C2D_SHIM_SED_DECK"] = str(dirs[k] / "sed.input")
     with ThreadPoolExecutor(len(runs)) as ex:
         futs = {k: ex.submit(_mpirun, exe, dirs[k], n, dict(env, C2D_STANDIN_COMM_DIR=str(dirs[k])))
                 for k, (exe, n, env) in runs.items()}
@@ -205,3 +212,45 @@ def test_shim_two_workers_allreduce_equals_one_worker(shim_runs):
     assert sorted(l.split(None, 1)[1] for l in ea) == sorted(l.split(None, 1)[1] for l in eb)
     lower = lambda ev: sorted(l for l in ev if l.split()[4] != "0.0000000E+00")
     assert lower(ea) == lower(eb)
+
+
+def _sed(path):
+    """(header lines, E, F [n_e, n_t], counts of the last time bin) of a pspt file."""
+    import numpy as np
+    lines = Path(path).read_text().splitlines()
+    rows = [l.split() for l in lines[4:]]
+    a = np.array([[float(x) for x in r[:-1]] for r in rows])
+    return lines[:4], a[:, 0], a[:, 1:], np.array([int(r[-1]) for r in rows])
+
+
+@pytest.mark.parametrize("run", ["shim", "lin2"])
+def test_shim_sed_on_device_equals_pspt_on_its_event_files(shim_runs, run):
+    """The shim's default event output: every step's escapes binned with
+    pspt's own binning from its deck (c2d_obs_begin_pspt; N workers summed
+    inside the C-ABI, c2d_obs_write_pspt) and pspt's file written, instead
+    of event text.  Against the reference's pspt (postprocessing/pspt.c,
+    built from the reference) run on the same run's event files (written
+    here too, C2D_SHIM_EVENTS=1): the same header, energies and last-bin
+    counts but for events within text rounding of a bin edge (pspt bins the
+    7-digit event text, the engine the doubles), fluxes to that rounding."""
+    import numpy as np
+    if not PSPT.exists():
+        pytest.skip("reference pspt not built (oracle/ref/build_ref.sh)")
+    d = shim_runs[run]
+    ours = d / "sed_shim.dat"
+    assert ours.exists()
+    ref_dir = d / "pspt_ref"
+    ref_dir.mkdir(exist_ok=True)
+    for f in d.glob("p00*_evb.dat"):
+        (ref_dir / f.name).write_bytes(f.read_bytes())
+    subprocess.run([str(PSPT)], input=SED_DECK, text=True, cwd=ref_dir, check=True, capture_output=True)
+    h0, E0, F0, c0 = _sed(ref_dir / "sed_shim.dat")
+    h1, E1, F1, c1 = _sed(ours)
+    assert h0 == h1
+    np.testing.assert_array_equal(E1, E0)
+    assert np.sum(np.abs(c1 - c0)) <= 2 and c0.sum() > 0
+    live = F0 > 1e-19
+    assert live.sum() > 20
+    assert np.all((F1 > 1e-19) == live)
+    rel = np.abs(F1[live] - F0[live]) / F0[live]
+    assert np.median(rel) < 1e-6 and np.mean(rel < 1e-5) > 0.98, (np.max(rel), np.median(rel))

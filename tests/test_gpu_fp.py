@@ -121,6 +121,11 @@ def test_gpu_fp_fast_within_tolerance(name, capsys):
         dev = fast_vs_oracle(g, o, "%s step %d" % (name, n))
         with capsys.disabled():
             print("\nC2D_FP_FAST %s step %d: %s" % (name, n, {k: "%.1e" % v for k, v in dev.items()}))
+    # the same update again: now through the zone queue (costliest zones first,
+    # one workgroup per CU, the gamma_bar memo warm): bit for bit the same
+    g2 = eng.fp_step(fi["ncycle"], fi["time"], fi["dt"], fi, fi)
+    for k in ("f_nt", "Pnt", "Te_new", "tea", "n_e", "gmin", "gmax", "amxwl", "p_nth"):
+        np.testing.assert_array_equal(np.asarray(g2[k]), np.asarray(g[k]), err_msg="queue rerun %s" % k)
     with pytest.raises(Exception, match="C2D_E_ARG"):
         eng.fp_set_mode(7)
     eng.close()

@@ -127,3 +127,26 @@ def test_gpu_bins_device_event_buffer():
         h = observer.bin_events(e, b, [None])
         _check_sums(h, OL.obs_bin(b, ev, "det"))
         assert h.count.sum() > 1000
+
+
+@pytest.mark.parametrize("name", [n for n in DECKS if str(G["tool_" + n]) == "pspt"])
+def test_gpu_pspt_deck_and_file_through_the_c_abi(eng, name, tmp_path):
+    """c2d_obs_begin_pspt (pspt's dialogue parsed and turned into edges by
+    the library, postprocessing/pspt.c:105-205) + c2d_obs_write_pspt (its
+    file, :323-353), the drop-in shim's default event output: the reference
+    pspt's own output file of the same deck and events (tests/golden/obs.npz),
+    as test_gpu_binning_matches_oracle_and_reference_files checks the
+    Python writer."""
+    deck = str(G["deck_" + name])
+    ev = G["events"]
+    n1 = int(G["n_file1"])
+    eng.obs_begin_pspt(deck)
+    eng.obs_accumulate(ev[:n1])
+    eng.obs_accumulate(ev[n1:])
+    b = observer.parse_pspt_deck(deck)
+    out = tmp_path / b.outfiles[0]
+    eng.obs_write_pspt(str(out), factor=1)
+    (f,) = G["files_" + name]
+    _same_text(out.read_text(), str(G["out_%s__%s" % (name, f)]))
+    with pytest.raises(Exception, match="C2D_E_ARG"):
+        eng.obs_begin_pspt("p001_evb.dat\n33\n1e16\nx\n30\n1.6e4\n6e4\n0.99944\n0.99964\n1\n1e-7\n1e10\n201\n")

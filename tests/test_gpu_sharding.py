@@ -36,7 +36,7 @@ def _close(a, b, what):
     np.testing.assert_allclose(a, b, rtol=1e-11, atol=1e-13 * scale, err_msg=what)
 
 
-@pytest.mark.parametrize("name", ["ssc_tau", "c3_mrk421"])
+@pytest.mark.parametrize("name", ["ssc_tau", "c3_mrk421", "c2_32x32"])
 def test_sharded_contexts_sum_to_world_one(name):
     gc = GoldenCase(name)
     steps = range(gc.nsteps)

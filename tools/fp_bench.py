@@ -95,6 +95,7 @@ def main():
     from compton2d_amd import abi
     eng.fp_set_mode(abi.FP_FAST if args.mode == "fast" else abi.FP_EXACT)
     r = eng.fp_step(tile["ncycle"], tile["time"], tile["dt"], tile, tile)   # warm-up
+    first_ms = eng.last_fp_ms()    # cold gamma_bar memo, zones in index order
     walls, kms = [], []
     for _ in range(args.reps):
         t0 = time.perf_counter()
@@ -132,6 +133,7 @@ def main():
         "zones": nz * nr,
         "implicit_substeps": substeps,
         "kernel_ms": ms,
+        "kernel_ms_first_call": first_ms,
         "wall_ms": float(np.median(walls)) * 1e3,
         "zones_per_s": nz * nr / (ms * 1e-3),
         "substeps_per_s": substeps / (ms * 1e-3),

@@ -21,6 +21,13 @@ def main():
     ap.add_argument("--nr", type=int, default=8)
     ap.add_argument("--vary", action="store_true")
     ap.add_argument("--mode", choices=("exact", "fast"), default="exact")
+    ap.add_argument("--sections", action="store_true",
+                    help="the library was built with C2D_FP_PROF_SEC: slots 4/6/7 are the sub-step's "
+                         "sections A (scalars..loop-350 sums), B (injection..tridiagonal coefficients), "
+                         "C (after the solve..gbar sums)")
+    ap.add_argument("--memo", action="store_true",
+                    help="built with C2D_FP_PROF_MEMO: slots 4/6/7 are gamma_bar calls, LDS-memo hits, "
+                         "global-memo hits")
     args = ap.parse_args()
     from compton2d_amd import abi
     c, g, tile = tiled_case(args.nz, args.nr, vary=args.vary)
@@ -42,7 +49,15 @@ def main():
                             "mcd_calls": float(d[zmax, 3])}
     out["loop_cycles_max_over_mean"] = float(d[:, 2].max() / d[:, 2].mean())
     out["substeps_max"] = float(steps.max())
-    if args.mode == "fast":           # McDonald internals (fp_fast.hip, C2D_FP_PROF)
+    if args.memo:
+        for name, q in (("memo_calls", 4), ("memo_lds_hits", 6), ("memo_global_hits", 7)):
+            out[name + "_per_substep"] = float((d[:, q] / steps).mean())
+            out["critical_zone"][name] = float(d[zmax, q])
+    elif args.sections:
+        for name, q in (("sec_a", 4), ("sec_b", 6), ("sec_c", 7)):
+            out[name + "_cycles_per_substep"] = float((d[:, q] / steps).mean())
+            out["critical_zone"][name + "_cycles"] = float(d[zmax, q])
+    elif args.mode == "fast":         # McDonald internals (fp_fast.hip, C2D_FP_PROF)
         calls = np.maximum(d[:, 3], 1)
         out["mcd_passes_per_call"] = float((d[:, 4] / calls).mean())
         out["mcd_loop_cycles_per_call"] = float((d[:, 6] / calls).mean())
