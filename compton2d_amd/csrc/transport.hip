@@ -1684,6 +1684,48 @@ __device__ __forceinline__ void pf_apply(const KParams& P0, Pkt& p, const CensRe
   p.dcen = P.cdt;                                    /* imcfield2d.f:117 */
 }
 
+/* C2D_PF_LDS: the prefetched record goes straight to LDS (gfx950 global ->
+ * LDS loads, no VGPRs held while it is in flight): 16 dwords per lane in a
+ * wave-private staging area, read back when the source starts */
+#ifndef C2D_PF_LDS
+#define C2D_PF_LDS 0
+#endif
+#if C2D_PF_LDS
+__shared__ uint32_t c2d_pf_lds[C2D_TR_BLOCK / 64][16][64];
+typedef const __attribute__((address_space(1))) void* c2d_gptr_t;
+typedef __attribute__((address_space(3))) void* c2d_lptr_t;
+__device__ __forceinline__ void pf_dword(const void* src, int w, int f) {
+  __builtin_amdgcn_global_load_lds((c2d_gptr_t)src, (c2d_lptr_t)&c2d_pf_lds[w][f][0], 4, 0, 0);
+}
+__device__ __forceinline__ void pf_issue_lds(const KParams& P0, long long i) {
+  const KParams& P = cold(P0);
+  const int w = (int)(threadIdx.x >> 6);
+  const double* d[6] = {P.cin.rpre + i, P.cin.zpre + i, P.cin.wmu + i, P.cin.phi + i, P.cin.ew + i,
+                        P.cin.xnu + i};
+#pragma unroll
+  for (int f = 0; f < 6; f++) {
+    pf_dword(d[f], w, 2 * f);
+    pf_dword(reinterpret_cast<const uint32_t*>(d[f]) + 1, w, 2 * f + 1);
+  }
+  pf_dword(P.cin.jk + i, w, 12);
+  pf_dword(P.cin.bins + i, w, 13);
+  pf_dword(P.cin.key + i, w, 14);
+  pf_dword(reinterpret_cast<const uint32_t*>(P.cin.key + i) + 1, w, 15);
+}
+__device__ __forceinline__ void pf_read_lds(CensRec& r) {
+  /* the loads' LDS writes complete in vmcnt order: wait for all of them */
+  __builtin_amdgcn_s_waitcnt(0xF70);                 /* vmcnt(0) */
+  const int w = (int)(threadIdx.x >> 6), l = (int)(threadIdx.x & 63);
+  auto dbl = [&](int f) {
+    return __hiloint2double((int)c2d_pf_lds[w][2 * f + 1][l], (int)c2d_pf_lds[w][2 * f][l]);
+  };
+  r.rpre = dbl(0); r.zpre = dbl(1); r.wmu = dbl(2); r.cphi = dbl(3); r.ew = dbl(4); r.xnu = dbl(5);
+  r.jk = c2d_pf_lds[w][12][l];
+  r.bn = c2d_pf_lds[w][13][l];
+  r.key = ((uint64_t)c2d_pf_lds[w][15][l] << 32) | (uint64_t)c2d_pf_lds[w][14][l];
+}
+#endif
+
 __device__ __forceinline__ void load_source(const KParams& P0, Pkt& p, long long src) {
   const KParams& P = cold(P0);
   if (src >= 0) {
@@ -1897,8 +1939,19 @@ __device__ __forceinline__ double UB(Bundle& b) {
 __device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bundle& b,
                                              bool from_pf = false, const CensRec* pr = nullptr) {
   Pkt& p = b.p;
+#if C2D_PF_LDS
+  (void)pr;
+  if (from_pf) {                      /* the census record prefetched into LDS */
+    CensRec r;
+    pf_read_lds(r);
+    pf_apply(P, p, r);
+  } else {
+    load_source(P, p, b.src);
+  }
+#else
   if (from_pf) pf_apply(P, p, *pr);   /* the census record prefetched into pr */
   else load_source(P, p, b.src);
+#endif
   const double ew0 = p.ew;
   const double s_ew = FDIV_POS(ew0, (double)P.split1);   /* imctrk2d.f:106-123 */
   const int G = min(P.split1 - b.g0, BUNDLE_MAX);
@@ -2196,7 +2249,12 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
    * next source's record loads issue here and complete under the VALU-only
    * point loop and the refill */
   if (nst == 1 && nitem >= 0) {
+#if C2D_PF_LDS
+    pf_issue_lds(P, nitem);
+    (void)nr;
+#else
     pf_issue(P, nr, nitem);
+#endif
     nst = 2;
   }
 #else
