@@ -45,7 +45,8 @@ c     C2D_SHIM_SED_DECK=path (pspt's input deck, e.g.
 c     postprocessing/mrk421_sed.input; unset: pspt's defaults),
 c     C2D_SHIM_SED=0 (no on-device SED),
 c     C2D_SHIM_EVENTS=1 (also write the event file),
-c     C2D_SHIM_CENSUS_MIRROR=0 (no dbufout mirror),
+c     C2D_SHIM_CENSUS_MIRROR=1|0 (dbufout mirror every step | never;
+c     default: only near write_record's elapsed-time mark),
 c     C2D_SHIM_ALLREDUCE=0 (N workers: no all-reduce inside the C-ABI;
 c     every worker deposits its own tallies into COMMON instead).
 c     Errors print the library's message and MPI_ABORT (the reference
@@ -67,7 +68,7 @@ c     (2*jmax + 2*kmax slots x 5 tables of nfmax)
       real(c_double), target, save :: sptab(shm_nf, 5, shm_nslot)
       integer(c_int32_t), target, save :: sidx_i(99), sidx_o(99),
      1     sidx_u(99), sidx_l(99)
-      integer, save :: ev_on = 0, mirror_on = 1, warned = 0
+      integer, save :: ev_on = 0, mirror_on = 2, warned = 0
 c     the on-device SED (c2d_obs_begin_pspt / c2d_obs_write_pspt)
       integer, save :: sed_on = 1
       logical, save :: static_done = .false.
@@ -208,6 +209,7 @@ c
       integer(c_int64_t) nev, ncs, m
       integer*8 npk, ccap, ecap, qcap, c2d_shim_env
       integer i, j, k, n, l, nw, cell, nsp
+      logical mir
 c
 c     the time-window index of this step (imcsurf2d_para.f:55-64)
       if (myid .eq. master) then
@@ -361,7 +363,7 @@ c     ---- worker: one GPU context, lineage shard myid-1 of numprocs-1
          rc = c2d_tally_layout_get(tctx, lay)
          allocate(tal(lay%total))
          ev_on = int(c2d_shim_env('C2D_SHIM_EVENTS', 0_8))
-         mirror_on = int(c2d_shim_env('C2D_SHIM_CENSUS_MIRROR', 1_8))
+         mirror_on = int(c2d_shim_env('C2D_SHIM_CENSUS_MIRROR', 2_8))
          sed_on = int(c2d_shim_env('C2D_SHIM_SED', 1_8))
 c        N workers without the all-reduce cannot sum one SED: events
          if (sed_on .eq. 1 .and. nw .gt. 1 .and. ar_on .ne. 1) then
@@ -558,9 +560,19 @@ c     escape events -> this worker's event file (imcleak2d.f:171,181)
  105  format(6(e14.7,1x),e14.7)
 c
 c     census mirror for write_record (imctrk2d.f:558-572 layout:
-c     6 f64 + 6 i32 per record, the 6th the record's seed)
+c     6 f64 + 6 i32 per record, the 6th the record's seed), which is
+c     the mirror's only reader: write_record runs once, when the
+c     master's elapsed time etotal (COMMON, broadcast by xec_bcast before
+c     this call) passes (0.95*wallm-3)*60 s with wallm = 480 minutes
+c     (xec2d.f:24,50,150).  C2D_SHIM_CENSUS_MIRROR=2 (default): mirror
+c     only once etotal is within two of its last increments of that
+c     mark; 1: every step; 0: never (the census stays on the GPU)
       rc = c2d_census_count(tctx, ncs)
-      if (mirror_on .eq. 1 .and. ncs .le. ucens) then
+      mir = mirror_on .eq. 1
+      if (mirror_on .eq. 2) mir = dble(etotal) + 2.d0 *
+     1     max(dble(etotal) - dble(etotal_old), 0.d0) .gt.
+     2     (0.95d0*480.d0 - 3.d0)*60.d0
+      if (mir .and. ncs .le. ucens) then
          allocate(i5(5, max(ncs, 1_8)), keys(max(ncs, 1_8)))
          rc = c2d_census_export(tctx, dbufout, i5, keys, ncs, m)
          do 70 n = 1, int(ncs)
@@ -573,7 +585,7 @@ c     6 f64 + 6 i32 per record, the 6th the record's seed)
          deallocate(i5, keys)
       else
          ndxout = 0
-         if (warned .eq. 0 .and. mirror_on .eq. 1) then
+         if (warned .eq. 0 .and. mir) then
             write(*,*) 'c2d_shim: census of', ncs, ' records exceeds',
      1           ' ucens: kept on the GPU only (c2d_census_export)'
             warned = 1
