@@ -542,8 +542,11 @@ __device__ void mcdonald23_fast(Blk<BS>& B, double z, const double* __restrict__
   double4 e[TPT];
 #pragma unroll
   for (int k = 0; k < TPT; k++) e[k] = gld4((row + (size_t)k * BS * 4));
+/* measured neutral to slightly slower (r04v: 30.57 vs 30.53 ms; the bound's
+ * fixed-point solve and its two checks cost what the skipped tests save):
+ * off by default */
 #ifndef C2D_FPF_FREE
-#define C2D_FPF_FREE 1
+#define C2D_FPF_FREE 0
 #endif
 #if C2D_FPF_FREE
   /* the passes that cannot hold a stopping term: summed without the test */

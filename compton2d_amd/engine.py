@@ -449,8 +449,8 @@ class Engine:
     def obs_begin_pspt(self, deck: str = "") -> None:
         """The SED binning of pspt's input dialogue `deck` (c2d_obs_begin_pspt)."""
         from . import observer
-        self._obs = observer.parse_pspt_deck(deck)
         self._check(self.lib.c2d_obs_begin_pspt(self.ctx, deck.encode()))
+        self._obs = observer.parse_pspt_deck(deck)
 
     def obs_write_pspt(self, path: str = "", factor: int = 0, world_sum: bool = False) -> None:
         """Write pspt's output file from the histogram so far (c2d_obs_write_pspt)."""
