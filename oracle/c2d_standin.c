@@ -202,6 +202,12 @@ int c2d_fp_set_config(c2d_ctx* c, const c2d_fp_config* fc) {
   return C2D_OK;
 }
 
+/* the oracle has one FP arithmetic (the reference's order): either mode maps to it */
+int c2d_fp_set_mode(c2d_ctx* c, int32_t mode) {
+  if (!c || (mode != C2D_FP_EXACT && mode != C2D_FP_FAST)) return C2D_E_ARG;
+  return C2D_OK;
+}
+
 int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out* out) {
   if (!c || !in || !out) return C2D_E_ARG;
   if (!c->fp_ready) return fail(c, C2D_E_STATE, "c2d_fp_set_config must precede c2d_fp_step");
