@@ -338,13 +338,6 @@ __constant__ double c_exp2_64[64] = {
 };
 __shared__ double f_e64[64];
 
-#ifndef C2D_FPF_EXPTAB
-#define C2D_FPF_EXPTAB 1
-#endif
-#ifndef C2D_FPF_ONTHEFLY
-#define C2D_FPF_ONTHEFLY 0
-#endif
-
 /* exp(x), -745 < x <= 0, table-driven: x = (64 m + j) ln2/64 + r with
  * |r| <= ln2/128, e^x = 2^m 2^(j/64) e^r, e^r by its Taylor polynomial to
  * degree 5 (truncation < 4e-17); the N chains interleaved as below */
@@ -369,34 +362,6 @@ __device__ __forceinline__ void exp_nonpos_tab(const double (&x)[N], double (&e)
   }
 #pragma unroll
   for (int j = 0; j < N; j++) e[j] = __builtin_ldexp(p[j] * f_e64[ki[j] & 63], ki[j] >> 6);
-}
-
-/* exp_nonpos of N arguments with the N Horner chains interleaved step by
- * step: one wave per SIMD hides nothing, so N independent dependent chains
- * in lockstep divide the exposed latency by N (sched_barrier keeps each
- * step's N FMAs together; the scheduler would otherwise serialise them) */
-template <int N>
-__device__ __forceinline__ void exp_nonpos_n(const double (&x)[N], double (&e)[N]) {
-  double kd[N], r[N], p[N];
-#pragma unroll
-  for (int j = 0; j < N; j++) {
-    kd[j] = __builtin_rint(x[j] * 1.4426950408889634);
-    r[j] = __builtin_fma(-kd[j], 6.93147180369123816490e-01, x[j]);
-    r[j] = __builtin_fma(-kd[j], 1.90821492927058770002e-10, r[j]);
-    p[j] = 1.6059043836821613e-10;                       /* 1/13! */
-  }
-  constexpr double C[13] = {2.0876756987868100e-09, 2.5052108385441720e-08, 2.7557319223985893e-07,
-                            2.7557319223985888e-06, 2.4801587301587302e-05, 1.9841269841269841e-04,
-                            1.3888888888888889e-03, 8.3333333333333332e-03, 4.1666666666666664e-02,
-                            1.6666666666666666e-01, 0.5, 1.0, 1.0};
-#pragma unroll
-  for (int i = 0; i < 13; i++) {
-#pragma unroll
-    for (int j = 0; j < N; j++) p[j] = __builtin_fma(p[j], r[j], C[i]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#pragma unroll
-  for (int j = 0; j < N; j++) e[j] = __builtin_ldexp(p[j], (int)kd[j]);
 }
 
 /* one abscissa row through a global (not flat) pointer */
@@ -439,11 +404,7 @@ __device__ __forceinline__ void mcd_pass(Blk<BS>& B, double z, const double4 (&x
     const double y = z * x[k].y;
     ny[k] = -(y < 2.25e2 ? y : 2.25e2);
   }
-#if C2D_FPF_EXPTAB
   exp_nonpos_tab<TPT>(ny, em);
-#else
-  exp_nonpos_n<TPT>(ny, em);
-#endif
 #pragma unroll
   for (int k = 0; k < TPT; k++)
     if (!(ny[k] > -2.25e2)) em[k] = 0.0;              /* y >= 225: the reference's zero term */
@@ -468,37 +429,6 @@ __device__ __forceinline__ void mcd_pass(Blk<BS>& B, double z, const double4 (&x
   if (f3 != INT_MAX) run3 = false;
 }
 
-/* The terms that cannot stop either series: a term n stops its series when
- * t_{n+1} >= 2 and sd_n <= 1e-8; sd(t) = (ts^2-1)^a e^{-z ts} is unimodal in
- * t (log-concave), hence in n, so no n in [n_a, n_lo] stops when sd > 1e-8
- * at both ends (n_a: the first n with t_{n+1} >= 2). K2's sd (a = 1.5) is
- * the smaller one there (ts^2 - 1 >= 1), so K2 decides for both. n_lo comes
- * from the descending root of log sd = ln 1e-7 (fixed-point iteration, a
- * contraction there), checked on the table's own rows; returned as a whole
- * number of passes (0 when a check fails). Those passes need no stopping
- * test and no barrier. */
-constexpr int MCD_NA = 693;                    /* first n with 1.001^(n+1) >= 2 */
-template <int PASS>
-__device__ int mcd_free_terms(double z, const double* __restrict__ tab) {
-  const double s = 5.0e-1 * (1.0 + 1.001), L = 16.11809565095832;   /* -ln 1e-7 */
-  double t = L / z + 2.0;
-#pragma unroll 1
-  for (int it = 0; it < 8; it++) t = (1.5 * c2d_log(t * t * s * s - 1.0) + L) / (z * s);
-  const double tcut = 2.25e2 / (z * s) * 0.999;          /* y >= 225 zeroes a term */
-  if (t > tcut) t = tcut;
-  int n_lo = (int)(c2d_log(t) / 9.9950033308342321e-04) - 2;
-  if (n_lo >= C2D_FP_MCD_N) n_lo = C2D_FP_MCD_N - 1;
-  if (n_lo < MCD_NA + PASS) return 0;
-  const double* a = tab + (size_t)MCD_NA * 4;
-  const double* b = tab + (size_t)n_lo * 4;
-  const double ya = z * a[1], yb = z * b[1];
-  if (!(ya < 2.25e2 && yb < 2.25e2)) return 0;
-  if (!(a[2] * c2d_exp_bf(-ya) > 1.0e-8 && b[2] * c2d_exp_bf(-yb) > 1.0e-8)) return 0;
-  int nA = (n_lo + 1) / PASS * PASS;
-  if (nA > C2D_FP_MCD_N - PASS) nA = C2D_FP_MCD_N - PASS;
-  return nA;
-}
-
 /* McDonald K2, K3 (volume2d.f:598-626) by the whole block: TPT*BS terms per
  * pass (TPT per thread, the next pass's abscissa rows loaded ahead), each
  * series' first stopping term by ballot + a block minimum (so exactly the
@@ -514,68 +444,10 @@ __device__ void mcdonald23_fast(Blk<BS>& B, double z, const double* __restrict__
   const long long pt0 = clock64();
 #endif
   int n0 = 0;
-#if C2D_FPF_ONTHEFLY
-  /* the abscissa rows computed per term (no table loads): t_n = 1.001^n as
-   * exp(n ln 1.001), the same values to rounding */
-  const double ldt = 9.9950033308342321e-04;          /* ln(1.001) */
-  for (; n0 < C2D_FP_MCD_N; n0 += PASS) {
-#ifdef C2D_FP_PROF
-    if (B.tid == 0) f_pf[0]++;
-#endif
-    double4 x[TPT];
-    double nl[TPT], tt[TPT];
-#pragma unroll
-    for (int k = 0; k < TPT; k++) nl[k] = (double)(n0 + k * BS + B.tid) * ldt;
-    exp_nonpos_tab<TPT>(nl, tt);                       /* valid for these x > 0 too */
-#pragma unroll
-    for (int k = 0; k < TPT; k++) {
-      const double t = tt[k], ts = t * (5.0e-1 * (1.0 + 1.001));
-      const double q = ts * ts - 1.0, rq = __builtin_sqrt(q);
-      x[k] = make_double4(t, ts, q * rq, q * q * rq);
-    }
-    mcd_pass<BS>(B, z, x, s2, s3, run2, run3);
-    guard += PASS;
-    if (!run2 && !run3) break;
-  }
-#else
   const double* row = tab + (size_t)B.tid * 4;
   double4 e[TPT];
 #pragma unroll
   for (int k = 0; k < TPT; k++) e[k] = gld4((row + (size_t)k * BS * 4));
-/* measured neutral to slightly slower (r04v: 30.57 vs 30.53 ms; the bound's
- * fixed-point solve and its two checks cost what the skipped tests save):
- * off by default */
-#ifndef C2D_FPF_FREE
-#define C2D_FPF_FREE 0
-#endif
-#if C2D_FPF_FREE
-  /* the passes that cannot hold a stopping term: summed without the test */
-  const int nA = mcd_free_terms<PASS>(z, tab);
-  {
-    const double d = 1.001 - 1.0;
-    for (; n0 < nA; n0 += PASS) {
-      double4 x[TPT];
-#pragma unroll
-      for (int k = 0; k < TPT; k++) x[k] = e[k];
-#pragma unroll
-      for (int k = 0; k < TPT; k++) e[k] = gld4((row + (size_t)(n0 + PASS + k * BS) * 4));
-      double em[TPT], ny[TPT];
-#pragma unroll
-      for (int k = 0; k < TPT; k++) ny[k] = -(z * x[k].y);   /* < 225 below n_lo */
-#if C2D_FPF_EXPTAB
-      exp_nonpos_tab<TPT>(ny, em);
-#else
-      exp_nonpos_n<TPT>(ny, em);
-#endif
-#pragma unroll
-      for (int k = 0; k < TPT; k++) {
-        s2 = s2 + d * x[k].x * (x[k].z * em[k]);
-        s3 = s3 + d * x[k].x * (x[k].w * em[k]);
-      }
-    }
-    guard += nA;
-  }
-#endif
   for (; n0 < C2D_FP_MCD_N; n0 += PASS) {
 #ifdef C2D_FP_PROF
     if (B.tid == 0) f_pf[0]++;
@@ -593,7 +465,6 @@ __device__ void mcdonald23_fast(Blk<BS>& B, double z, const double* __restrict__
     guard += PASS;
     if (!run2 && !run3) break;
   }
-#endif
   /* past the table (never reached on the reference's decks) */
   for (; (run2 || run3) && guard <= GUARD_MAX; n0 += PASS) {
     double4 x[TPT];
@@ -683,21 +554,16 @@ __device__ __forceinline__ double rcp_nr(double x) {
 
 /* The same system, rows 1..NT (row i in thread i-1, rows past NT identity
  * rows), by partitions: wave w holds rows 64w+1..64w+64 and reduces its own
- * block by cyclic reduction across its lanes (cross-lane moves, no barrier)
+ * block by cyclic reduction across its lanes (through wave-private LDS rows,
+ * no barrier; lane shuffles measured slower, r04s)
  * for three right-hand sides at once, d and the two spikes that couple the
  * block to the last unknown L of the previous partition and the first
  * unknown F of the next (x = y - v L_{w-1} - w F_{w+1}); the partitions' edge
  * rows form a chain over the W-1 interfaces that every thread then solves
  * for itself, behind one barrier (8 barriers for pcr_solve). */
 __shared__ double f_if[WMAXF][6];
-#ifndef C2D_FPF_SPIKE
-#define C2D_FPF_SPIKE 2
-#endif
-#if C2D_FPF_SPIKE == 2
 __shared__ double2 f_sac[WMAXF][FPB], f_sdv[WMAXF][FPB];   /* (a, c), (d, v) per lane */
 __shared__ double f_sw[WMAXF][FPB];
-#endif
-__device__ __forceinline__ double lane_from(double v, int src) { return __shfl(v, src, FPB); }
 template <int BS>
 __device__ double spike_solve(Blk<BS>& B, double a, double b, double c, double d) {
   constexpr int W = BS / FPB;
@@ -709,14 +575,9 @@ __device__ double spike_solve(Blk<BS>& B, double a, double b, double c, double d
   /* unit diagonal: row r reads x_r + a x_{r-s} + c x_{r+s} = (d, v, w) */
   double r = rcp_nr(b);
   a = a * r; c = c * r; d = d * r; v = v * r; w = w * r;
-#if C2D_FPF_SPIKE == 2
 #pragma unroll 1
-#else
-#pragma unroll
-#endif
   for (int s = 1; s < FPB; s <<= 1) {
     const int lm = lane - s, lp = lane + s;
-#if C2D_FPF_SPIKE == 2
     /* through the wave's own LDS rows: the wave's lanes store and then load
      * in program order, so no barrier (a wavefront fence keeps the order) */
     f_sac[wave][lane] = make_double2(a, c);
@@ -731,12 +592,6 @@ __device__ double spike_solve(Blk<BS>& B, double a, double b, double c, double d
     double ap = acp.x, cp = acp.y, dp = dvp.x, vp = dvp.y, wp = f_sw[wave][qp];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-#else
-    double am = lane_from(a, lm), cm = lane_from(c, lm), dm = lane_from(d, lm);
-    double vm = lane_from(v, lm), wm = lane_from(w, lm);
-    double ap = lane_from(a, lp), cp = lane_from(c, lp), dp = lane_from(d, lp);
-    double vp = lane_from(v, lp), wp = lane_from(w, lp);
-#endif
     if (lm < 0) am = cm = dm = vm = wm = 0.0;      /* outside the block: a = 0 there */
     if (lp >= FPB) ap = cp = dp = vp = wp = 0.0;
     r = rcp_nr(1.0 - a * cm - c * ap);
@@ -1101,6 +956,10 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
     PS_END(pf_sb);
     /* tridag (:2476-2518) by cyclic reduction; clip u(2..num_nt) (:2512) */
     PF_BEGIN();
+    /* C2D_FPF_SPIKE=0: plain PCR with a barrier per level (measured equal, r04s) */
+#ifndef C2D_FPF_SPIKE
+#define C2D_FPF_SPIKE 1
+#endif
 #if C2D_FPF_SPIKE
     double u = spike_solve<BS>(B, ta, tb, tc, own ? f_fold[i] : 0.0);
 #else
@@ -1134,13 +993,9 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
     PF_BEGIN();
     /* one loop for both directions: gamma_bar's code is inlined once here */
     const bool up = gbar > g_av;
-    int ks = 0;
     while (up ? gbar > g_av : gbar < g_av) {
       The_new = up ? The_new * F32(1.005) : The_new / F32(1.005);
-#ifndef C2D_FPF_GLOB
-#define C2D_FPF_GLOB 1
-#endif
-      g_av = gamma_bar_m(The_new, C2D_FPF_GLOB ? true : ++ks > 2);
+      g_av = gamma_bar_m(The_new, true);
       if (!up && The_new < 1.0e-2) break;
       if (guard > GUARD_MAX) break;
     }
