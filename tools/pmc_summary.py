@@ -72,7 +72,7 @@ def main(root):
             res["gen0_ms_timed_mean"] = mean(dur[-k:])
         names = {}
         for r in rows:
-            n = r["Kernel_Name"].split("(")[0]
+            n = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
             names.setdefault(n, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
         for n, v in sorted(names.items(), key=lambda kv: -sum(kv[1])):
             print("  %-60s n=%4d total=%9.3f ms mean=%8.3f ms" % (n[:60], len(v), sum(v), mean(v)))
@@ -136,13 +136,15 @@ def main(root):
                                        wk * 1024.0 / (res["write"]["ms"] * 1e-3)) / 1e9
             print("HBM bytes per lane path-step: fetch(x2) %.2f + write %.2f = %.2f; measured %.0f GB/s"
                   % (fpb, wpb, fpb + wpb, res["hbm_gbs_measured"]))
-    # the FP kernel (c2d_fp_kernel<W>): last dispatch of each pass
+    # the FP kernel (c2d_fp_kernel<W>, or c2d_fp_fast_kernel<BS> in the fast
+    # mode): last dispatch of each pass
     fp = {}
     for sub in ("fetch", "write", "sq"):
         f = find(os.path.join(root, sub), "kernel_trace.csv")
         if not f:
             continue
-        rows = [r for r in dispatches(f) if "c2d_fp_kernel" in r["Kernel_Name"]]
+        rows = [r for r in dispatches(f)
+                if "c2d_fp_kernel" in r["Kernel_Name"] or "c2d_fp_fast_kernel" in r["Kernel_Name"]]
         if not rows:
             continue
         r = rows[-1]
