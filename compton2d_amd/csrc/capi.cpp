@@ -2012,6 +2012,13 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
     P.ncell = (int32_t)nc;
     HIPCHK(c, hipMemcpyAsync(c->fpf_zq + 1, c->fpf_order.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, st));
     HIPCHK(c, hipMemsetAsync(c->fpf_zq, 0, sizeof(int32_t), st));
+    /* C2D_FPF_MEMO_RESET=1: every update starts from an empty gamma_bar memo
+     * (measurement: the cost of temperatures the memo has not seen) */
+    const char* mr = getenv("C2D_FPF_MEMO_RESET");
+    if (mr && mr[0] == '1' && c->fpf_gb_key) {
+      HIPCHK(c, hipMemsetAsync(c->fpf_gb_key, 0, sizeof(unsigned long long) * C2D_FPF_MEMO_SLOTS, st));
+      HIPCHK(c, hipMemsetAsync(c->fpf_gb_val, 0, sizeof(double) * C2D_FPF_MEMO_SLOTS, st));
+    }
     HIPCHK(c, hipMemcpyAsync(c->fp_dP, &P, sizeof P, hipMemcpyHostToDevice, st));
   }
   HIPCHK(c, hipEventRecord(c->ev_g0a, st));
