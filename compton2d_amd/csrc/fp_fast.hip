@@ -385,7 +385,7 @@ __device__ __forceinline__ double4 mcd_row(const double* __restrict__ tab, int n
 
 /* McDonald terms per thread per pass (C2D_FPF_TPT: 2 or 4) */
 #ifndef C2D_FPF_TPT
-#define C2D_FPF_TPT 2
+#define C2D_FPF_TPT 4
 #endif
 constexpr int TPT = C2D_FPF_TPT;
 
@@ -417,7 +417,13 @@ __device__ __forceinline__ void mcd_pass(Blk<BS>& B, double z, const double4 (&x
     st3[k] = !(tn < 2.0 || v3[k] > 1.0e-8);
   }
   int f2, f3;
+#ifdef C2D_FP_PROF_MCD
+  const long long pa = clock64();
+#endif
   B.template firsts<TPT>(st2, st3, f2, f3);
+#ifdef C2D_FP_PROF_MCD
+  if (B.tid == 0) f_pf[3] += clock64() - pa;        /* the stopping test incl. its barrier */
+#endif
   /* terms up to and including each series' first stopping term */
 #pragma unroll
   for (int k = 0; k < TPT; k++) {
@@ -1090,6 +1096,9 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
     zo[FO_DIAG + 4] = (double)f_pf[0];
     zo[FO_DIAG + 6] = (double)f_pf[1];
     zo[FO_DIAG + 7] = (double)f_pf[2];
+#endif
+#ifdef C2D_FP_PROF_MCD
+    zo[FO_DIAG + 7] = (double)f_pf[3];
 #endif
 #ifdef C2D_FP_PROF_MEMO
     zo[FO_DIAG + 4] = (double)pm_calls;

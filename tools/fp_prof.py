@@ -25,6 +25,8 @@ def main():
                     help="the library was built with C2D_FP_PROF_SEC: slots 4/6/7 are the sub-step's "
                          "sections A (scalars..loop-350 sums), B (injection..tridiagonal coefficients), "
                          "C (after the solve..gbar sums)")
+    ap.add_argument("--mcd", action="store_true",
+                    help="built with C2D_FP_PROF_MCD: slot 7 is the McDonald stopping tests' cycles")
     ap.add_argument("--memo", action="store_true",
                     help="built with C2D_FP_PROF_MEMO: slots 4/6/7 are gamma_bar calls, LDS-memo hits, "
                          "global-memo hits")
@@ -57,6 +59,11 @@ def main():
         for name, q in (("sec_a", 4), ("sec_b", 6), ("sec_c", 7)):
             out[name + "_cycles_per_substep"] = float((d[:, q] / steps).mean())
             out["critical_zone"][name + "_cycles"] = float(d[zmax, q])
+    elif args.mcd:                    # built with C2D_FP_PROF_MCD: slot 7 = the stopping tests
+        calls = np.maximum(d[:, 3], 1)
+        out["mcd_passes_per_call"] = float((d[:, 4] / calls).mean())
+        out["mcd_loop_cycles_per_call"] = float((d[:, 6] / calls).mean())
+        out["mcd_firsts_cycles_per_call"] = float((d[:, 7] / calls).mean())
     elif args.mode == "fast":         # McDonald internals (fp_fast.hip, C2D_FP_PROF)
         calls = np.maximum(d[:, 3], 1)
         out["mcd_passes_per_call"] = float((d[:, 4] / calls).mean())
