@@ -126,7 +126,10 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
  *   C2D_RSQ_NR    Newton steps after v_rsq_f64 in the survivors' point loop.
  * A/B on the C3 census (profiles/r03_microopt.txt): FAST_DIV +2 % (on),
  * FAST_EXP=1 -4 % (ocml's exp keeps more VGPRs live), RSQ_NR=1 +1 %
- * (within noise; kept at 2 for the geometry's precision).  On the
+ * (within noise then; round 4, two A/B pairs on the steady-state census,
+ * profiles/r05j: generation 0 126.5/126.6 vs 126.9/126.9 ms, now the
+ * default: one Newton step after v_rsq_f64 leaves ~1e-14 relative in the
+ * absorption-point deposits).  On the
  * steady-state C3 census (profiles/r03k): FAST_EXP=2 +1 % (default),
  * C2D_FAST_MDIV +1.2 %. */
 #ifndef C2D_FAST_EXP
@@ -136,7 +139,7 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 #define C2D_FAST_DIV 1
 #endif
 #ifndef C2D_RSQ_NR
-#define C2D_RSQ_NR 2
+#define C2D_RSQ_NR 1
 #endif
 /* C2D_FAST_LOG (fast build): log(x) for normal x > 0 by fdlibm's reduction
  * and polynomial with one of its two final forms for every x (c2d_log_pos
