@@ -28,6 +28,20 @@ __global__ void c2d_selftest_math_kernel(int fn, const double* x, double* y, int
     case 6: r = v / 3.0; break;
     case 8: r = c2d_log_pos(v); break;
     case 9: r = c2d_exp_bf(v); break;
+    /* the fast build's reciprocal / reciprocal-sqrt sequences (transport.hip):
+     * the hardware estimate alone and after one Newton step */
+    case 10: r = __builtin_amdgcn_rcp(v); break;
+    case 11: {
+      const double q = __builtin_amdgcn_rcp(v);
+      r = __builtin_fma(q, __builtin_fma(-v, q, 1.0), q);
+      break;
+    }
+    case 12: r = __builtin_amdgcn_rsq(v); break;
+    case 13: {
+      const double q = __builtin_amdgcn_rsq(v);
+      r = q * __builtin_fma(-0.5 * v, q * q, 1.5);
+      break;
+    }
     default: r = c2d_draw((uint64_t)(int64_t)v, (uint32_t)i); break;
   }
   y[i] = r;

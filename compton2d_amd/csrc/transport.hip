@@ -128,8 +128,8 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
  * FAST_EXP=1 -4 % (ocml's exp keeps more VGPRs live), RSQ_NR=1 +1 %
  * (within noise then; round 4, two A/B pairs on the steady-state census,
  * profiles/r05j: generation 0 126.5/126.6 vs 126.9/126.9 ms, now the
- * default: one Newton step after v_rsq_f64 leaves ~1e-14 relative in the
- * absorption-point deposits).  On the
+ * default: one Newton step after v_rsq_f64 leaves 4.1e-15 relative in the
+ * absorption-point deposits, r05k).  On the
  * steady-state C3 census (profiles/r03k): FAST_EXP=2 +1 % (default),
  * C2D_FAST_MDIV +1.2 %. */
 #ifndef C2D_FAST_EXP
@@ -201,10 +201,19 @@ __device__ __forceinline__ double exp_neg(double x) {
 #define FEXP(x) c2d_exp(x)
 #endif
 #if C2D_TABLE_COMTOT && C2D_FAST_DIV
+/* C2D_FAST_NR: Newton steps after the v_rcp_f64 / v_rsq_f64 estimates of
+ * the bundle step's divisions and square roots (rcp_pos, fsqrt_nn).  The
+ * estimates are good to 4.6e-8 / 5.2e-8 relative, one step to 2.2e-15 /
+ * 4.1e-15 over 1e-6..1e6 (tests/test_gpu_rcp_precision.py, r05k); one step:
+ * generation 0 126.2/126.3 -> 125.4/125.5 ms in two A/B pairs (r05k) */
+#ifndef C2D_FAST_NR
+#define C2D_FAST_NR 1
+#endif
 __device__ __forceinline__ double rcp_pos(double b) {
   double y = __builtin_amdgcn_rcp(b);
-  y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
-  return __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+#pragma unroll
+  for (int k = 0; k < C2D_FAST_NR; k++) y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+  return y;
 }
 #define FDIV_POS(a, b) ((a) * rcp_pos(b))
 /* C2D_FAST_SQRT: the bundle step's square roots (distances, radii, |sin|)
@@ -220,8 +229,8 @@ __device__ __forceinline__ double fsqrt_nn(double x) {
   x = fmax(x, 1.0e-300);
   const double h = 0.5 * x;
   double y = __builtin_amdgcn_rsq(x);
-  y = y * __builtin_fma(-h, y * y, 1.5);
-  y = y * __builtin_fma(-h, y * y, 1.5);
+#pragma unroll
+  for (int k = 0; k < C2D_FAST_NR; k++) y = y * __builtin_fma(-h, y * y, 1.5);
   return x * y;
 }
 #define FSQRT(x) fsqrt_nn(x)
