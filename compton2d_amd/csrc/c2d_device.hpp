@@ -153,9 +153,12 @@ __device__ __forceinline__ void gor(int32_t* p, int32_t v) {
  * replica b mod C2D_NF_REPL), summed into the tally buffer after the last
  * generation.  f64 atomics execute at the memory side and serialise per
  * address; packets that census together share (cell, energy bin), so a single
- * copy is a hot spot (2.5x on the EC light-curve workload). */
+ * copy is a hot spot (2.5x on the EC light-curve workload).  8 replicas (one
+ * per XCD under the usual round-robin placement, a speed matter only) beat 16
+ * and 32 on C3 generation 0 (124.2/124.0 vs 124.6/124.7 vs 125.1/125.2 ms)
+ * with C5 unchanged (profiles/r05q); 128 lost 2 % (r05n). */
 #ifndef C2D_NF_REPL
-#define C2D_NF_REPL 32
+#define C2D_NF_REPL 8
 #endif
 
 /* internal counter slot (not part of the tally buffer's counters, zeroed

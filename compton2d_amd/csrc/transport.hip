@@ -917,14 +917,18 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
   int cell = (p.jph - 1) * P.nr + (p.kph - 1);
   cell_add(P, T, TC_NPCEN, cell, 1.0);
   cell_add(P, T, TC_ECENS, cell, p.ew);
-#ifdef C2D_ABLATE_NFIELD                /* profiling ablation only (tools/build_sweep.sh) */
+#if defined(C2D_ABLATE_NFIELD) && C2D_ABLATE_NFIELD == 1   /* profiling ablations only */
   if (p.xnu < 0.0) {
 #else
   if (p.xnu > P.egg_min) {              /* Egg_min = E_field(1)^2/E_field(2), host-computed */
 #endif
     const int i = grid_lookup(g->E_field, C2D_NPHFIELD, g->efl_start, g->efl_k0, p.xnu);
+    const double v = FDIV_POS(6.25e8 * p.ew, p.xnu);
+#if defined(C2D_ABLATE_NFIELD) && C2D_ABLATE_NFIELD == 2   /* the lookup without the add */
+    if (v == 1.25e300)
+#endif
     gadd(&P.nf_rep[(int64_t)(blockIdx.x % C2D_NF_REPL) * P.ncell * C2D_NPHFIELD +
-                   (int64_t)cell * C2D_NPHFIELD + (i - 1)], FDIV_POS(6.25e8 * p.ew, p.xnu));
+                   (int64_t)cell * C2D_NPHFIELD + (i - 1)], v);
   }
   const unsigned long long slot = census_slot_chunk(P);
   if (slot < (unsigned long long)P.cap_cout) {
