@@ -927,6 +927,11 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
 #if defined(C2D_ABLATE_NFIELD) && C2D_ABLATE_NFIELD == 2   /* the lookup without the add */
     if (v == 1.25e300)
 #endif
+#if defined(C2D_ABLATE_NFIELD) && C2D_ABLATE_NFIELD == 3   /* a plain store in place of the add */
+    gst(&P.nf_rep[(int64_t)(blockIdx.x % C2D_NF_REPL) * P.ncell * C2D_NPHFIELD +
+                  (int64_t)cell * C2D_NPHFIELD + (i - 1)], v);
+    if (v == 1.25e300)
+#endif
     gadd(&P.nf_rep[(int64_t)(blockIdx.x % C2D_NF_REPL) * P.ncell * C2D_NPHFIELD +
                    (int64_t)cell * C2D_NPHFIELD + (i - 1)], v);
   }
