@@ -67,8 +67,10 @@ struct SpecDev {             /* file_sp table (imcsurf2d_para.f:544-685) */
  * the step's launches).  After the step the partly filled chunks (one per wave slot at most)
  * are packed into full ones and the chunks taken become the next list
  * (capi.cpp census_chunks_close). */
-#define C2D_CCHUNK 1024
+#ifndef C2D_CCHUNK_LOG
 #define C2D_CCHUNK_LOG 10
+#endif
+#define C2D_CCHUNK (1 << C2D_CCHUNK_LOG)
 #define C2D_CT_TRACK 16      /* census chunks a wave counts down at once (pow 2) */
 #define C2D_CT_STACK 8       /* freed chunks a wave holds for its next appends */
 struct CensusSoA {

@@ -107,7 +107,7 @@ constexpr int SBLOCK = 256;       /* source / scatter kernels */
 /* generation-0 items a wave takes per fetch (one returning atomic on a work
  * shard counter: 64 -> 256 -> 1024 items, +6 %, +2 %) */
 #ifndef C2D_WORK_CHUNK
-#define C2D_WORK_CHUNK 1024
+#define C2D_WORK_CHUNK C2D_CCHUNK
 #endif
 constexpr long long CHUNK = C2D_WORK_CHUNK;
 /* fast build: -log(1-x) of the survivors' absorption points by its series
