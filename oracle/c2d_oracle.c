@@ -326,6 +326,12 @@ typedef struct c2o_ctx {
    * so those see the previous step's dt -- 0 in the first step */
   int dt_lag;
   double dt_prev;
+  /* MPI-worker emulation (c2o_set_grid_lag, hazard H12): the workers learn
+   * nphtotal, nph_lc, hu and Elcmin/Elcmax only in their first z_surf_bcast
+   * (src/surf_mpi.f:24-27,76-81; reader runs on the master alone,
+   * src/compton2d.f:23-31), after the first step's census and volume jobs:
+   * every spectral / light-curve bin those jobs compute is 0 */
+  int grid_lag, grid_seen, grid_missing;
   int rank, world;              /* lineage-sharded sources (global index % world == rank) */
   uint64_t seed;
   double t_bound_last;
@@ -460,6 +466,9 @@ static double comtot_cell(const c2o_ctx* c, int cell, double xnuc) {
  * differ per caller (REAL vs DOUBLE literals); `top_value` is what the caller
  * assigns when xnu >= hutop (vol_calc uses nphtotal, all others 0). */
 static int bin_sp(const c2o_ctx* c, double xnu, double fbot, double ftop, int top_value) {
+  /* H12: nphtotal = 0 on the worker, so jtop = 1 and hutop = 0.999999*hu(1)
+   * with hu not yet broadcast: every xnu takes the top branch, jgpsp = 0 */
+  if (c->grid_missing) return 0;
   int jbot = 1, jtop = c->nphtotal + 1, jmid;
   double hubot = fbot * c->hu[1];
   double hutop = ftop * c->hu[jtop];
@@ -478,6 +487,7 @@ static int bin_sp(const c2o_ctx* c, double xnu, double fbot, double ftop, int to
 }
 
 static int bin_lc(const c2o_ctx* c, double xnu) {
+  if (c->grid_missing) return 0;            /* H12: nph_lc = 0 on the worker */
   for (int m = 1; m <= c->nph_lc; m++)
     if (xnu > c->Elcmin[m] && xnu <= c->Elcmax[m]) return m;
   return 0;
@@ -1507,6 +1517,7 @@ int c2o_step(c2o_ctx* c, const c2d_step_in* in) {
   c->dt = in->dt;
   const double dt_now = in->dt;
   if (c->dt_lag) c->dt = c->dt_prev;
+  c->grid_missing = c->grid_lag && !c->grid_seen;
   memset(c->T, 0, sizeof(double) * c->L.total);
   c->nev = 0;
   gather3(c, &in->kappa_tot, C2D_N_VOL, c->kappa);
@@ -1580,9 +1591,11 @@ int c2o_step(c2o_ctx* c, const c2d_step_in* in) {
         if (c->err) return c->err;
       }
     }
-  /* surfaces use the current kappa_tot and dt (broadcast in z_surf_bcast) */
+  /* surfaces use the current kappa_tot, dt and grids (broadcast in z_surf_bcast) */
   c->kappa_use = c->kappa;
   c->dt = dt_now;
+  c->grid_missing = 0;
+  c->grid_seen = 1;
   for (int js = 1; js <= c->nz; js++) {
     if (c->rng_mode == C2O_RNG_FIB) initialize_rand(fs, c->zseeds[js - 1]);
     for (int side = 0; side < 2; side++) {
@@ -1626,6 +1639,9 @@ int c2o_step(c2o_ctx* c, const c2d_step_in* in) {
 
 /* hazard H11 (MPI workers' stale dt, see c2o_ctx.dt_lag): off by default */
 void c2o_set_dt_lag(c2o_ctx* c, int on) { c->dt_lag = on; }
+/* hazard H12 (MPI workers' grids before the first z_surf_bcast, see
+ * c2o_ctx.grid_lag): off by default */
+void c2o_set_grid_lag(c2o_ctx* c, int on) { c->grid_lag = on; }
 
 const double* c2o_tallies(c2o_ctx* c, int64_t* n) {
   *n = c->L.total;

@@ -25,7 +25,9 @@
  * Environment: C2D_STANDIN_RNG = fib (default) | lineage,
  * C2D_STANDIN_RAND_SWITCH (default 1), C2D_STANDIN_H4 (default 1: stale
  * t_bound), C2D_STANDIN_DT_LAG (default 1: the MPI workers' previous-step
- * dt for census and volume packets, hazard H11), C2D_STANDIN_RSEED (the
+ * dt for census and volume packets, hazard H11), C2D_STANDIN_GRID_LAG
+ * (default 1: bins 0 for the first step's census and volume packets, hazard
+ * H12), C2D_STANDIN_RSEED (the
  * deck's rseed: the oracle replays the master's seed_zone chain from it).
  */
 #include <errno.h>
@@ -54,6 +56,7 @@ int64_t c2o_census_count(c2o_ctx* c);
 int64_t c2o_census_export(c2o_ctx* c, double* d6, int32_t* i5, uint64_t* keys, int64_t cap);
 int c2o_census_import(c2o_ctx* c, const double* d6, const int32_t* i5, const uint64_t* keys, int64_t n);
 void c2o_set_dt_lag(c2o_ctx* c, int on);
+void c2o_set_grid_lag(c2o_ctx* c, int on);
 int c2o_fp_step(const c2d_config* g, const c2d_fp_config* fc, const c2d_fp_step_in* in,
                 c2d_fp_step_out* out);
 int c2o_obs_bin(const c2d_obs_bins* b, const double* ev, int64_t n, double* F, double* F2, double* cnt);
@@ -119,6 +122,10 @@ int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   /* hazard H11: the reference's MPI workers transport census and volume
    * packets with the dt of the previous z_surf_bcast (0 in the first step) */
   c2o_set_dt_lag(c->o, (int)envl("C2D_STANDIN_DT_LAG", 1));
+  /* hazard H12: the workers' spectral / light-curve grids are unset during
+   * the first step's census and volume jobs, so those packets carry bins 0
+   * and their escapes never reach fout / edout */
+  c2o_set_grid_lag(c->o, (int)envl("C2D_STANDIN_GRID_LAG", 1));
   c2d_tally_layout_for(cfg->nz, cfg->nr, cfg->nmu, &c->L);
   c->T = (double*)calloc((size_t)c->L.total, sizeof(double));
   if (!c->T) return fail(c, C2D_E_NOMEM, "c2d_standin: tally buffer");

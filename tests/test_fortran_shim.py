@@ -87,8 +87,9 @@ STANDIN = ROOT / "oracle" / "_ref" / "shim" / "compton2d_standin"
 REFEXE = ROOT / "oracle" / "_ref" / "shim" / "compton2d_ref"
 SHIM_DECK = dict(T_const=0, tstop=2.0e5, nst=1500)
 # files whose every byte the reference writes from state the shim delivers
+# (the spectra and light curves since hazard H12 is reproduced by the stand-in)
 SAME_FILES = ("p001_evb.dat", "output/nfield.dat", "output/temp_b.dat", "output/eic.dat",
-              "output/seb.dat", "esp.dat")
+              "output/seb.dat", "esp.dat", "output/spb.dat", "output/phb.dat", "output/lcb_01.dat")
 PSPT = ROOT / "oracle" / "_ref" / "pspt"
 # pspt's dialogue for this small run: no bulk boost, every direction, the
 # run's whole time range, 100 log channels (postprocessing/pspt.c:105-205)
@@ -108,8 +109,8 @@ def _mpirun(exe, case, nproc, env_extra):
 @pytest.fixture(scope="module")
 def shim_runs(tmp_path_factory):
     """The reference (1 worker), the shim over the stand-in in fib mode (1
-    worker), and the shim over the stand-in in lineage mode with 1 and 2
-    workers, run concurrently."""
+    worker) with and without hazard H12 reproduced, and the shim over the
+    stand-in in lineage mode with 1 and 2 workers, run concurrently."""
     if not _reference_available():
         pytest.skip("reference sources / MPI not in this container")
     subprocess.run(["bash", str(ROOT / "oracle" / "ref" / "build_shim.sh")], check=True,
@@ -119,6 +120,8 @@ def shim_runs(tmp_path_factory):
     ev = {"C2D_SHIM_EVENTS": "1"}          # the text events too (the SED is the default)
     runs = {"ref": (REFEXE, 2, {}),
             "shim": (STANDIN, 2, dict(ev, C2D_STANDIN_RSEED=str(refcase.BASE_CASE["rseed"]))),
+            "nolag": (STANDIN, 2, dict(ev, C2D_STANDIN_RSEED=str(refcase.BASE_CASE["rseed"]),
+                                       C2D_STANDIN_GRID_LAG="0")),
             "lin1": (STANDIN, 2, dict(ev, C2D_STANDIN_RNG="lineage")),
             "lin2": (STANDIN, 3, dict(ev, C2D_STANDIN_RNG="lineage"))}
     dirs = {}
@@ -175,13 +178,20 @@ def test_shim_over_standin_reproduces_the_reference_mpi_run(shim_runs):
 
 
 def test_shim_spectrum_is_its_event_spectrum(shim_runs):
-    """spb.dat of the shim run is F(E) of its escape events (to the file's 6
-    digits).  The reference's own spb.dat of the same run, whose event file
-    is byte-identical, is NOT: its MPI reduction path delivers ~3/4 of the
-    escapes' energy to graphics (measured: a bin-dependent 0.6-0.85), which
-    is why spb.dat / phb.dat / lcb_01.dat are not in SAME_FILES."""
+    """Hazard H12 isolated.  With the workers' first-step grids supplied
+    (C2D_STANDIN_GRID_LAG=0: what the GPU engine does), spb.dat is F(E) of
+    the run's escape events (to the file's 6 digits).  The reference's own
+    spb.dat, from the byte-identical event file, is not: the packets its
+    worker creates in step 0, before its first z_surf_bcast delivers
+    nphtotal / hu / nph_lc / Elcmin / Elcmax (src/surf_mpi.f:24-27,76-81),
+    carry spectral and light-curve bins 0 (src/imcvol2d_para.f:334-374)
+    through the census until they scatter, so their escapes are written to
+    the event file but never reach fout / edout (src/imcleak2d.f:172-175,
+    206-209, 307-310).  Only energy is removed (every bin <= the event
+    spectrum), and the stand-in with the lag on (the "shim" run) reproduces
+    the reference's spb.dat byte for byte (SAME_FILES)."""
     import numpy as np
-    F, f_ev = _spectrum_from_events(shim_runs["shim"])
+    F, f_ev = _spectrum_from_events(shim_runs["nolag"])
     # the last step's time + dt (graphics2d.f:146), from the spectrum's own normalisation
     live = F > 1e-20
     scale = np.median(f_ev[live] / F[live])
@@ -189,7 +199,10 @@ def test_shim_spectrum_is_its_event_spectrum(shim_runs):
     Fr, f_evr = _spectrum_from_events(shim_runs["ref"])
     assert np.array_equal(f_evr, f_ev)                       # same events ...
     r = Fr[live] / F[live]
-    assert np.median(r) < 0.9                               # ... a different spb.dat
+    assert np.all(r <= 1 + 1e-5) and np.median(r) < 0.9      # ... energy missing from spb.dat
+    lc0 = np.loadtxt(shim_runs["nolag"] / "output" / "lcb_01.dat")
+    lc1 = np.loadtxt(shim_runs["ref"] / "output" / "lcb_01.dat")
+    assert np.all(lc1[:, 1:] <= lc0[:, 1:] * (1 + 1e-5)) and np.any(lc1[:, 1:] < 0.9 * lc0[:, 1:])
 
 
 def test_shim_two_workers_allreduce_equals_one_worker(shim_runs):
