@@ -224,6 +224,7 @@ struct c2d_ctx {
   bool obs_ready = false;
   ObsDev obs;
   double *obs_edges = nullptr, *obs_hist = nullptr, *obs_ev = nullptr;
+  double* pspt_red = nullptr;                 /* world_sum reduction buffer, 2 x n_t x n_e */
   c2d_pspt_deck pspt;                         /* c2d_obs_begin_pspt's deck */
   bool pspt_on = false;
   int64_t obs_ev_cap = 0;
@@ -489,7 +490,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
     if (c->cens[b].key) (void)hipFree(c->cens[b].key);
   }
   for (double* p : c->spec_bufs) (void)hipFree(p);
-  void* optrs[] = {c->obs_edges, c->obs_hist, c->obs_ev};
+  void* optrs[] = {c->obs_edges, c->obs_hist, c->obs_ev, c->pspt_red};
   for (void* p : optrs)
     if (p) (void)hipFree(p);
   void* vptrs[] = {c->vem_zin, c->vem_fnt, c->vem_eph, c->vem_kap, c->vem_et, c->vem_eh, c->vem_zout};
@@ -1839,37 +1840,56 @@ extern "C" int c2d_last_kernel_ms(c2d_ctx* c, double* gen0_ms, double* all_ms, i
  * values, so it is sized so that probes stay short (16 MB) */
 #define C2D_FPF_MEMO_SLOTS (1u << 20)
 static int ensure_mcd(c2d_ctx* c) {
-  if (c->fp_mcd) return C2D_OK;
-  std::vector<double> mt((size_t)C2D_FP_MCD_N * 4);
-  const double dtm = 1.001, sm = 5.0e-1 * (1.0 + dtm);
-  double t = 1.0;
-  for (int n = 0; n < C2D_FP_MCD_N; n++) {
-    const double ts = t * sm;
-    mt[(size_t)n * 4 + 0] = t;
-    mt[(size_t)n * 4 + 1] = ts;
-    mt[(size_t)n * 4 + 2] = c2d_pow(ts * ts - 1.0, 1.5);
-    mt[(size_t)n * 4 + 3] = c2d_pow(ts * ts - 1.0, 2.5);
-    t = t * dtm;
+  /* every buffer has its own guard, so a failed allocation is retried by the
+   * next call instead of being reported as done with null pointers */
+  if (!c->fp_mcd) {
+    std::vector<double> mt((size_t)C2D_FP_MCD_N * 4);
+    const double dtm = 1.001, sm = 5.0e-1 * (1.0 + dtm);
+    double t = 1.0;
+    for (int n = 0; n < C2D_FP_MCD_N; n++) {
+      const double ts = t * sm;
+      mt[(size_t)n * 4 + 0] = t;
+      mt[(size_t)n * 4 + 1] = ts;
+      mt[(size_t)n * 4 + 2] = c2d_pow(ts * ts - 1.0, 1.5);
+      mt[(size_t)n * 4 + 3] = c2d_pow(ts * ts - 1.0, 2.5);
+      t = t * dtm;
+    }
+    double* m = nullptr;
+    HIPCHK(c, dalloc(&m, mt.size()));
+    const hipError_t e = hipMemcpy(m, mt.data(), mt.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(m);
+      HIPCHK(c, e);
+    }
+    c->fp_mcd = m;
   }
-  HIPCHK(c, dalloc(&c->fp_mcd, mt.size()));
-  HIPCHK(c, hipMemcpy(c->fp_mcd, mt.data(), mt.size() * sizeof(double), hipMemcpyHostToDevice));
   /* the gamma_bar memo lives as long as the context (gamma_bar is a pure
    * function of Theta); C2D_FP_MEMO=0 disables it (A/B) */
   const char* e = getenv("C2D_FP_MEMO");
   if (!(e && e[0] == '0')) {
-    HIPCHK(c, dalloc(&c->fp_gb_key, C2D_FP_MEMO_SLOTS));
-    HIPCHK(c, dalloc(&c->fp_gb_val, C2D_FP_MEMO_SLOTS));
-    HIPCHK(c, hipMemset(c->fp_gb_key, 0, sizeof(unsigned long long) * C2D_FP_MEMO_SLOTS));
-    HIPCHK(c, hipMemset(c->fp_gb_val, 0, sizeof(double) * C2D_FP_MEMO_SLOTS));
-    HIPCHK(c, dalloc(&c->fpf_gb_key, C2D_FPF_MEMO_SLOTS));
-    HIPCHK(c, dalloc(&c->fpf_gb_val, C2D_FPF_MEMO_SLOTS));
-    HIPCHK(c, hipMemset(c->fpf_gb_key, 0, sizeof(unsigned long long) * C2D_FPF_MEMO_SLOTS));
-    HIPCHK(c, hipMemset(c->fpf_gb_val, 0, sizeof(double) * C2D_FPF_MEMO_SLOTS));
+    if (!c->fp_gb_key) {
+      HIPCHK(c, dalloc(&c->fp_gb_key, C2D_FP_MEMO_SLOTS));
+      HIPCHK(c, hipMemset(c->fp_gb_key, 0, sizeof(unsigned long long) * C2D_FP_MEMO_SLOTS));
+    }
+    if (!c->fp_gb_val) {
+      HIPCHK(c, dalloc(&c->fp_gb_val, C2D_FP_MEMO_SLOTS));
+      HIPCHK(c, hipMemset(c->fp_gb_val, 0, sizeof(double) * C2D_FP_MEMO_SLOTS));
+    }
+    if (!c->fpf_gb_key) {
+      HIPCHK(c, dalloc(&c->fpf_gb_key, C2D_FPF_MEMO_SLOTS));
+      HIPCHK(c, hipMemset(c->fpf_gb_key, 0, sizeof(unsigned long long) * C2D_FPF_MEMO_SLOTS));
+    }
+    if (!c->fpf_gb_val) {
+      HIPCHK(c, dalloc(&c->fpf_gb_val, C2D_FPF_MEMO_SLOTS));
+      HIPCHK(c, hipMemset(c->fpf_gb_val, 0, sizeof(double) * C2D_FPF_MEMO_SLOTS));
+    }
   }
-  HIPCHK(c, dalloc(&c->fp_dP, 1));
-  HIPCHK(c, dalloc(&c->fpf_zq, (size_t)c->ncell + 1));
-  c->fpf_order.resize(c->ncell);
-  for (int q = 0; q < c->ncell; q++) c->fpf_order[q] = q;
+  if (!c->fp_dP) HIPCHK(c, dalloc(&c->fp_dP, 1));
+  if (!c->fpf_zq) HIPCHK(c, dalloc(&c->fpf_zq, (size_t)c->ncell + 1));
+  if ((int)c->fpf_order.size() != c->ncell) {
+    c->fpf_order.resize(c->ncell);
+    for (int q = 0; q < c->ncell; q++) c->fpf_order[q] = q;
+  }
   return C2D_OK;
 }
 
@@ -2003,6 +2023,8 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   P.zout = c->fp_zout; P.err = c->fp_err;
   P.gb_key = c->fp_gb_key; P.gb_val = c->fp_gb_val; P.gb_mask = C2D_FP_MEMO_SLOTS - 1u;
   if (c->fp_mode == C2D_FP_FAST) {
+    if (!c->fp_dP || !c->fpf_zq || !c->fp_mcd)
+      return fail(c, C2D_E_STATE, "c2d_fp_step: the fast kernel's buffers are not allocated");
     P.gb_key = c->fpf_gb_key; P.gb_val = c->fpf_gb_val; P.gb_mask = C2D_FPF_MEMO_SLOTS - 1u;
     /* zones from a queue, costliest first (by the last update's sub-step
      * counts), on one workgroup per CU (C2D_FPF_GRID: another grid size,
@@ -2258,6 +2280,9 @@ extern "C" int c2d_obs_begin(c2d_ctx* c, const c2d_obs_bins* b) {
     return fail(c, C2D_E_ARG, "c2d_obs_begin: bad binning");
   if (b->mode == C2D_OBS_SED && b->n_mu != 1)
     return fail(c, C2D_E_ARG, "c2d_obs_begin: the SED mode has one angular window");
+  /* a new binning ends any pspt deck: c2d_obs_begin_pspt sets it again */
+  c->pspt_on = false;
+  c->obs_ready = false;
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (c->obs_edges) (void)hipFree(c->obs_edges);
   if (c->obs_hist) (void)hipFree(c->obs_hist);
@@ -2392,6 +2417,11 @@ extern "C" int c2d_obs_begin_pspt(c2d_ctx* c, const char* deck) {
   b.n_e = d.n_e; b.E0 = d.E0; b.E1 = d.E1;
   const int rc = c2d_obs_begin(c, &b);
   if (rc != C2D_OK) return rc;
+  /* the world_sum reduction buffer lives as long as the deck, so a rank can
+   * no longer fail an allocation and skip the collective the others enter */
+  if (c->pspt_red) (void)hipFree(c->pspt_red);
+  c->pspt_red = nullptr;
+  HIPCHK(c, dalloc(&c->pspt_red, 2 * (size_t)d.n_t * d.n_e));
   c->pspt = d;
   c->pspt_on = true;
   return C2D_OK;
@@ -2403,24 +2433,22 @@ extern "C" int c2d_obs_begin_pspt(c2d_ctx* c, const char* deck) {
 extern "C" int c2d_obs_write_pspt(c2d_ctx* c, const char* path, int32_t factor, int32_t world_sum) {
   if (!c) return C2D_E_ARG;
   if (!c->pspt_on || !c->obs_ready) return fail(c, C2D_E_STATE, "c2d_obs_write_pspt: c2d_obs_begin_pspt first");
+  if (c->obs.mode != C2D_OBS_SED || c->obs.n_mu != 1 || c->obs.n_t != c->pspt.n_t || c->obs.n_e != c->pspt.n_e ||
+      !c->pspt_red)
+    return fail(c, C2D_E_STATE, "c2d_obs_write_pspt: the binning is not the pspt deck's");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  const size_t nh = (size_t)c->obs.n_t * c->obs.n_e;
+  const size_t nh = (size_t)c->obs.n_t * c->obs.n_mu * c->obs.n_e;
   std::vector<double> F(nh), cnt(nh);
   if (world_sum) {
     if (!c->comm) return fail(c, C2D_E_STATE, "c2d_obs_write_pspt: world_sum needs c2d_comm_init");
-    double* w = nullptr;
-    HIPCHK(c, dalloc(&w, 2 * nh));
+    double* w = c->pspt_red;
     HIPCHK(c, hipMemcpyAsync(w, c->obs.F, nh * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(w + nh, c->obs.cnt, nh * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     const ncclResult_t r = ncclAllReduce(w, w, 2 * nh, ncclDouble, ncclSum, c->comm, c->stream);
-    if (r != ncclSuccess) {
-      (void)hipFree(w);
-      return fail(c, C2D_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
-    }
+    if (r != ncclSuccess) return fail(c, C2D_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
     HIPCHK(c, hipMemcpyAsync(F.data(), w, nh * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(cnt.data(), w + nh, nh * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    (void)hipFree(w);
     if (c->comm_rank != 0) return C2D_OK;
   } else {
     const int rc = c2d_obs_result(c, F.data(), nullptr, cnt.data(), nullptr);

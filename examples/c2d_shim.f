@@ -70,6 +70,14 @@ c     (2*jmax + 2*kmax slots x 5 tables of nfmax)
       integer(c_int32_t), target, save :: sidx_i(99), sidx_o(99),
      1     sidx_u(99), sidx_l(99)
       integer, save :: ev_on = 0, mirror_on = 2, warned = 0
+c     census mirror (mode 2): write_record's mark in seconds of etotal
+c     (C2D_SHIM_MIRROR_MARK overrides it, a test hook) and the latch that
+c     keeps the mirror on every step once it has started
+      double precision, save :: mirror_mark = (0.95d0*480.d0-3.d0)*60.d0
+      logical, save :: mir_latch = .false.
+c     test hook (C2D_SHIM_WRITE_CENS=1): after every mirror, write the
+c     mirrored census as write_record would (write_record.f:433-437)
+      integer, save :: wcens_on = 0
 c     the on-device SED (c2d_obs_begin_pspt / c2d_obs_write_pspt)
       integer, save :: sed_on = 1
       logical, save :: static_done = .false.
@@ -190,7 +198,8 @@ c
       use compton2d
       use c2d_shim_state, only: tctx, tready, lay, tal, spec, sptab,
      1     sidx_i, sidx_o, sidx_u, sidx_l, ev_on, mirror_on, warned,
-     2     static_done, seed0, ar_on, commid, sed_on
+     2     static_done, seed0, ar_on, commid, sed_on, mirror_mark,
+     3     mir_latch, wcens_on
       implicit none
       include 'mpif.h'
       include 'general.pa'
@@ -209,8 +218,9 @@ c
       integer(c_int32_t) ngpu
       integer(c_int64_t) nev, ncs, m
       integer*8 npk, ccap, ecap, qcap, c2d_shim_env
-      integer i, j, k, n, l, nw, cell, nsp
+      integer i, j, k, n, l, nw, cell, nsp, ucf
       logical mir
+      character*40 cfname
 c
 c     the time-window index of this step (imcsurf2d_para.f:55-64)
       if (myid .eq. master) then
@@ -365,6 +375,9 @@ c     ---- worker: one GPU context, lineage shard myid-1 of numprocs-1
          allocate(tal(lay%total))
          ev_on = int(c2d_shim_env('C2D_SHIM_EVENTS', 0_8))
          mirror_on = int(c2d_shim_env('C2D_SHIM_CENSUS_MIRROR', 2_8))
+         mirror_mark = dble(c2d_shim_env('C2D_SHIM_MIRROR_MARK',
+     1        int(mirror_mark, 8)))
+         wcens_on = int(c2d_shim_env('C2D_SHIM_WRITE_CENS', 0_8))
          sed_on = int(c2d_shim_env('C2D_SHIM_SED', 1_8))
 c        N workers without the all-reduce cannot sum one SED: events
          if (sed_on .eq. 1 .and. nw .gt. 1 .and. ar_on .ne. 1) then
@@ -562,17 +575,26 @@ c     escape events -> this worker's event file (imcleak2d.f:171,181)
 c
 c     census mirror for write_record (imctrk2d.f:558-572 layout:
 c     6 f64 + 6 i32 per record, the 6th the record's seed), which is
-c     the mirror's only reader: write_record runs once, when the
-c     master's elapsed time etotal (COMMON, broadcast by xec_bcast before
-c     this call) passes (0.95*wallm-3)*60 s with wallm = 480 minutes
-c     (xec2d.f:24,50,150).  C2D_SHIM_CENSUS_MIRROR=2 (default): mirror
-c     only once etotal is within two of its last increments of that
-c     mark; 1: every step; 0: never (the census stays on the GPU)
+c     the mirror's only reader: write_record runs once, at the start of
+c     the step whose etotal (the master's elapsed time, COMMON, broadcast
+c     by xec_bcast) passes the mark (0.95*wallm-3)*60 s, wallm = 480
+c     minutes (xec2d.f:24,50,150).  That etotal is not known here, so
+c     C2D_SHIM_CENSUS_MIRROR=2 (default) starts mirroring once etotal
+c     plus two of its last increments passes 0.8 of the mark and then
+c     mirrors every step to the end of the run (a step would have to
+c     take ~90 minutes to jump the margin); 1: every step; 0: never (the
+c     census stays on the GPU)
       rc = c2d_census_count(tctx, ncs)
       mir = mirror_on .eq. 1
-      if (mirror_on .eq. 2) mir = dble(etotal) + 2.d0 *
-     1     max(dble(etotal) - dble(etotal_old), 0.d0) .gt.
-     2     (0.95d0*480.d0 - 3.d0)*60.d0
+      if (mirror_on .eq. 2) then
+         if (.not. mir_latch .and. dble(etotal) + 2.d0 *
+     1        max(dble(etotal) - dble(etotal_old), 0.d0) .gt.
+     2        0.8d0*mirror_mark) then
+            mir_latch = .true.
+            write(*,*) 'c2d_shim: census mirror on from ncycle', ncycle
+         endif
+         mir = mir_latch
+      endif
       if (mir .and. ncs .le. ucens) then
          allocate(i5(5, max(ncs, 1_8)), keys(max(ncs, 1_8)))
          rc = c2d_census_export(tctx, dbufout, i5, keys, ncs, m)
@@ -580,11 +602,20 @@ c     mark; 1: every step; 0: never (the census stays on the GPU)
             do 69 i = 1, 5
                ibufout(6*(n-1) + i) = i5(i, n)
  69         continue
-            ibufout(6*n) = int(mod(keys(n), 100000_8))
+            ibufout(6*n) = int(modulo(keys(n), 100000_8))
  70      continue
          ndxout = int(ncs)
          deallocate(i5, keys)
+         if (wcens_on .eq. 1) then
+            write(cfname, '(a,i3.3,a)') 'p', myid, '_census_mirror.dat'
+            open(newunit=ucf, file=trim(cfname), status='replace')
+            call write_cens(ndxout, ucf)
+            close(ucf)
+         endif
       else
+         if (ndxout .gt. 0) write(*,*) 'c2d_shim: census mirror of',
+     1        ndxout, ' records dropped at ncycle', ncycle,
+     2        ': write_record would see no census'
          ndxout = 0
          if (warned .eq. 0 .and. mir) then
             write(*,*) 'c2d_shim: census of', ncs, ' records exceeds',

@@ -96,6 +96,12 @@ PSPT = ROOT / "oracle" / "_ref" / "pspt"
 SED_DECK = "p001_evb.dat\n1\n1e16\nsed_shim.dat\n30\n0\n2.5e5\n-1\n1\n1\n1e-7\n1e10\n100\n0\nn\n"
 
 
+# the census mirror's test hooks: write_record's mark lowered to 0 s of
+# etotal (the mirror starts at once and stays on), and every mirror written
+# by the reference's own write_cens as write_record would
+MIRROR_HOOK = {"C2D_SHIM_MIRROR_MARK": "0", "C2D_SHIM_WRITE_CENS": "1"}
+
+
 def _mpirun(exe, case, nproc, env_extra):
     def big_stack():
         resource.setrlimit(resource.RLIMIT_STACK, (resource.RLIM_INFINITY, resource.RLIM_INFINITY))
@@ -103,6 +109,7 @@ def _mpirun(exe, case, nproc, env_extra):
     r = subprocess.run([str(MPIEXEC), "-n", str(nproc), str(exe)], cwd=case, capture_output=True,
                        text=True, timeout=600, preexec_fn=big_stack, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    (case / "run.log").write_text(r.stdout + r.stderr)
     return r
 
 
@@ -122,8 +129,8 @@ def shim_runs(tmp_path_factory):
             "shim": (STANDIN, 2, dict(ev, C2D_STANDIN_RSEED=str(refcase.BASE_CASE["rseed"]))),
             "nolag": (STANDIN, 2, dict(ev, C2D_STANDIN_RSEED=str(refcase.BASE_CASE["rseed"]),
                                        C2D_STANDIN_GRID_LAG="0")),
-            "lin1": (STANDIN, 2, dict(ev, C2D_STANDIN_RNG="lineage")),
-            "lin2": (STANDIN, 3, dict(ev, C2D_STANDIN_RNG="lineage"))}
+            "lin1": (STANDIN, 2, dict(ev, C2D_STANDIN_RNG="lineage", **MIRROR_HOOK)),
+            "lin2": (STANDIN, 3, dict(ev, C2D_STANDIN_RNG="lineage", **MIRROR_HOOK))}
     dirs = {}
     for k in runs:
         dirs[k] = base / k
@@ -267,3 +274,37 @@ def test_shim_sed_on_device_equals_pspt_on_its_event_files(shim_runs, run):
     assert np.all((F1 > 1e-19) == live)
     rel = np.abs(F1[live] - F0[live]) / F0[live]
     assert np.median(rel) < 1e-6 and np.mean(rel < 1e-5) > 0.98, (np.max(rel), np.median(rel))
+
+
+def _census_records(path):
+    """(6 f64 text, 6 i32 text) record pairs of a write_cens file (census2d.f:23-25)."""
+    lines = Path(path).read_text().splitlines()
+    assert len(lines) % 2 == 0
+    return [(lines[i], lines[i + 1]) for i in range(0, len(lines), 2)]
+
+
+def test_shim_census_mirror_reaches_write_cens(shim_runs):
+    """the census mirror that write_record reads.  With the mark
+    lowered (C2D_SHIM_MIRROR_MARK=0) it starts at ncycle 0 and stays on,
+    and the reference's own write_cens (census2d.f:1-33, called as
+    write_record.f:433-437 calls it) writes the census of the run's last
+    step from COMMON dbufout/ibufout: 2 workers write, between them, the
+    same records as 1 worker (lineage streams: the census does not depend
+    on the worker count).  With the default mark no mirror runs."""
+    a, b = shim_runs["lin1"], shim_runs["lin2"]
+    for d, nw in ((a, 1), (b, 2)):
+        log = (d / "run.log").read_text()
+        import re
+        assert len(re.findall(r"census mirror on from ncycle\s+0\b", log)) == nw, log[-2000:]
+        assert "records dropped" not in log
+    ra = _census_records(a / "p001_census_mirror.dat")
+    rb = _census_records(b / "p001_census_mirror.dat") + _census_records(b / "p002_census_mirror.dat")
+    assert len(ra) > 100
+    assert sorted(ra) == sorted(rb)
+    for d6, i6 in ra:
+        v = [float(d6[14 * i:14 * i + 14]) for i in range(6)]                               # 6e14.7
+        jgpsp, jgplc, jgpmu, jph, kph, seed = (int(i6[5 * i:5 * i + 5]) for i in range(6))   # 6i5
+        assert v[4] > 0 and v[5] > 0 and 1 <= jph <= 2 and 1 <= kph <= 2 and 0 <= seed < 100000
+    shim_log = (shim_runs["shim"] / "run.log").read_text()
+    assert "census mirror on" not in shim_log
+    assert not list(shim_runs["shim"].glob("p00*_census_mirror.dat"))
