@@ -27,6 +27,8 @@ TR_PROF_WORDS = 32                 # C2D_TR_PROF_WORDS (c2d_transport_prof)
 
 COMTOT_EXACT = 0
 COMTOT_TABLE = 1
+TRK_SRC = 0           # c2d_config.trk_variant: src/imctrk2d.f (default)
+TRK_2012_11 = 1       # src_20121113/imctrk2d.f (hazard H1 fixed)
 
 CNT_STEPS, CNT_ESCAPES, CNT_CENSUS, CNT_COLLIDE, CNT_KILLED, CNT_SOURCES, \
     CNT_COMPB, CNT_EVENTS, CNT_GENS, CNT_ABORTED = range(10)
@@ -73,6 +75,7 @@ class Config(C.Structure):
         ("device", C.c_int32), ("seed", C.c_uint64), ("rank", C.c_int32), ("world", C.c_int32),
         ("census_capacity", C.c_int64), ("event_capacity", C.c_int64),
         ("queue_capacity", C.c_int64), ("census_inplace", C.c_int32),
+        ("trk_variant", C.c_int32),
     ]
 
 
@@ -182,6 +185,7 @@ class GridConfig:
     event_capacity: int = 1 << 20
     queue_capacity: int = 1 << 18
     census_inplace: int = 0
+    trk_variant: int = 0          # TRK_SRC | TRK_2012_11 (include/compton2d.h)
 
     def to_ctypes(self) -> Config:
         self._keep = [np.ascontiguousarray(a, dtype=np.float64) for a in (
@@ -198,7 +202,8 @@ class GridConfig:
             kappa_lag=self.kappa_lag, comtot_mode=self.comtot_mode, device=self.device,
             seed=self.seed, rank=self.rank, world=self.world,
             census_capacity=self.census_capacity, event_capacity=self.event_capacity,
-            queue_capacity=self.queue_capacity, census_inplace=self.census_inplace)
+            queue_capacity=self.queue_capacity, census_inplace=self.census_inplace,
+            trk_variant=self.trk_variant)
 
 
 @dataclass

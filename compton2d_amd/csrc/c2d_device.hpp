@@ -182,6 +182,7 @@ struct KParams {
   int32_t split1, split2, split3, spl3_trg, spec_switch;
   int32_t rank, world, ncycle, eps_linear;
   double time, dt, rmin, zmin, cdt;
+  double cens_wlim;         /* census records' |wmu| clamp: 0.99999999 (src), 1 (trk_variant 2012-11) */
   uint64_t step_key;
   const Geo* geo;
   const double* gnt;        /* [200] */

@@ -24,9 +24,9 @@
 using namespace c2d;
 
 extern "C" int c2d_launch_transport_exact(const KParams* P, const GenArgs* A, int grid, size_t lds,
-                                          hipStream_t s);
+                                          int trk, hipStream_t s);
 extern "C" int c2d_launch_transport_fast(const KParams* P, const GenArgs* A, int grid, size_t lds,
-                                         hipStream_t s);
+                                         int trk, hipStream_t s);
 extern "C" int c2d_launch_source_exact(const KParams* P, int grid, hipStream_t s);
 extern "C" int c2d_launch_source_fast(const KParams* P, int grid, hipStream_t s);
 extern "C" int c2d_launch_scatter_exact(const KParams* P, const GenArgs* A, int grid, hipStream_t s);
@@ -36,9 +36,9 @@ extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_aux_occupancy_exact(int which, int* blocks_per_cu);
 extern "C" int c2d_aux_occupancy_fast(int which, int* blocks_per_cu);
 extern "C" int c2d_launch_bundle_exact(const KParams* P, const GenArgs* A, int grid, size_t lds,
-                                       hipStream_t s);
+                                       int trk, hipStream_t s);
 extern "C" int c2d_launch_bundle_fast(const KParams* P, const GenArgs* A, int grid, size_t lds,
-                                      hipStream_t s);
+                                      int trk, hipStream_t s);
 extern "C" int c2d_bundle_occupancy_exact(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_bundle_occupancy_fast(int* blocks_per_cu, size_t lds);
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t s);
@@ -298,6 +298,7 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
       cfg->nph_lc > C2D_NPHLCMAX || cfg->nmu < 1 || cfg->nmu > C2D_NMUMAX)
     return C2D_E_ARG;
   if (cfg->cr_sent != 0) return C2D_E_ARG;   /* Compton reflection not supported */
+  if (cfg->trk_variant != C2D_TRK_SRC && cfg->trk_variant != C2D_TRK_2012_11) return C2D_E_ARG;
   if (cfg->split1 < 1 || cfg->split2 < 1 || cfg->split3 < 1 || cfg->world < 1 ||
       cfg->rank < 0 || cfg->rank >= cfg->world)
     return C2D_E_ARG;
@@ -536,6 +537,7 @@ extern "C" int c2d_set_clock(c2d_ctx* c, int32_t ncycle, double time, double dt)
   c->P.time = time;
   c->P.dt = dt;
   c->P.cdt = 2.9979245620e10 * dt;                 /* dcen = c_light*dt(1), imcfield2d.f:117 */
+  c->P.cens_wlim = c->cfg.trk_variant == C2D_TRK_2012_11 ? 1.0 : 0.99999999;
   c->P.step_key = c2d_step_key(c->cfg.seed, ncycle);
   return C2D_OK;
 }
@@ -1340,7 +1342,7 @@ static int run_step_body(c2d_ctx* c) {
       const int grid = (int)std::max<int64_t>(
           1, std::min<int64_t>(gmax, (A.n_items + C2D_TR_BLOCK - 1) / C2D_TR_BLOCK));
       c->g0_launched = true;
-      int rc = launch_b(c->dP, &A, grid, c->bundle_lds, c->stream);
+      int rc = launch_b(c->dP, &A, grid, c->bundle_lds, cfg.trk_variant, c->stream);
       if (rc) return fail(c, C2D_E_HIP, "bundle launch (gen 0): %s", hipGetErrorString((hipError_t)rc));
       launches++;
     }
@@ -1377,7 +1379,7 @@ static int run_step_body(c2d_ctx* c) {
       A.n2_in = n2; A.n3_in = n3;
       int rc = launch_sc(c->dP, &A, aux_grid(e - b, c->sc_grid), c->stream);
       if (rc) return fail(c, C2D_E_HIP, "scatter launch (gen %d): %s", gen, hipGetErrorString((hipError_t)rc));
-      rc = launch_tr(c->dP, &A, tr_grid(e - b), c->lds_bytes, c->stream);
+      rc = launch_tr(c->dP, &A, tr_grid(e - b), c->lds_bytes, cfg.trk_variant, c->stream);
       if (rc) return fail(c, C2D_E_HIP, "transport launch (gen %d): %s", gen, hipGetErrorString((hipError_t)rc));
       launches += 2;
     }

@@ -267,6 +267,8 @@ struct Pkt {
   uint32_t sub;       /* lineage sub-stream: split1 copies of a source (c2d_rng.h) */
   uint32_t ctr;
   uint32_t nflight;   /* safety cap: a history that stops progressing is aborted */
+  double cmfp;        /* C2D_TRK_2012_11: colmfp carried across cell boundaries
+                         (src_20121113/imctrk2d.f:505,526-533); unused otherwise */
 };
 
 __device__ __forceinline__ int32_t JGPSP(const Pkt& p) { return (int32_t)(p.bins & 0xffu); }
@@ -1064,9 +1066,14 @@ struct Prof {
 #define TP_COUNT(pf, iw, il) do { } while (0)
 #endif
 
+/* V12: the tracker of src_20121113/imctrk2d.f (c2d_config.trk_variant =
+ * C2D_TRK_2012_11; include/compton2d.h): the azimuth update with the path's
+ * r-plane projection f, colmfp kept across cell boundaries, clamps at 1.
+ * V12 = 0 is src/imctrk2d.f bug for bug (hazard H1). */
+template <int V12>
 __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, ComCache& cc, LaneCnt& lc,
                                       Prof& pf) {
-  const double lim8 = 9.9999999e-1, lim9 = 0.999999999;
+  const double lim8 = V12 ? 1.0 : 9.9999999e-1, lim9 = V12 ? 1.0 : 0.999999999;
   const Geo* g = T.g;
 #if C2D_TABLE_COMTOT && C2D_EARLY_LOADS
   /* the step's table reads (comtot interpolation points, n_e, kappa) are
@@ -1080,7 +1087,9 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
 #endif
   /* mode 0 uses mb_ran = 1e-10 (imctrk2d.f:150) but never reads colmfp (dcol below) */
   double colmfp = 0.0;
-  if (p.mode != 0) colmfp = -c2d_log(U(p));   /* Philox uniform is never 0: no `goto 100` redraw */
+  /* src: label 100 every step; 2012-11: only when the track starts (label
+   * 110 after a boundary).  The uniform is never 0: no `goto 100` redraw */
+  if (p.mode != 0) colmfp = (V12 && p.nflight != 0) ? p.cmfp : -c2d_log(U(p));
   if (p.ew < 1.0e-40) return FL_END;
   if (++p.nflight > MAX_FLIGHTS) {
     LC_ADD(lc, C2D_CNT_ABORTED);
@@ -1132,7 +1141,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   double Eta = c2d_cos(p.phi);
   const int eta_switch = (p.phi <= PI_REF && p.phi >= 1.0e-10) ? 1 : -1;
 #endif
-  Eta = clampd(Eta, lim8);
+  if (!V12) Eta = clampd(Eta, lim8);          /* commented out in src_20121113:248-249 */
   const double rpre = p.rpre, zpre = p.zpre, wmu = p.wmu;
   const double disp = Eta * rpre;
   const double psq = rpre * rpre * (1.0 - Eta * Eta);
@@ -1152,6 +1161,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   const double disbr = (double)inout * __builtin_sqrt(dpbsq) - disp;
   const double swmu = __builtin_sqrt(1.0 - wmu * wmu);
   double trldb = disbr / swmu;
+  double fr = disbr;                           /* the reference's f (imctrk2d.f:278,290,380) */
   const double Zr = zpre + wmu * trldb;
   const double zlow = (p.jph == 1) ? P.zmin : g->z[p.jph - 1];
   const double zup = g->z[p.jph];
@@ -1160,6 +1170,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
     knew = p.kph;
     jnew = (Zr > zup) ? p.jph + 1 : p.jph - 1;
     const double f = (Zbnd - zpre) * swmu / wmu;
+    fr = f;
     rbnd = __builtin_sqrt(rpre * rpre + f * f + 2.0 * rpre * f * Eta);
     trldb = __builtin_sqrt(f * f + (Zbnd - zpre) * (Zbnd - zpre));
   } else {
@@ -1178,6 +1189,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
     jnew = p.jph;
     knew = p.kph;
     const double f = trld * swmu;
+    fr = f;
     rnew = __builtin_sqrt(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
     znew = zpre + trld * wmu;
   }
@@ -1221,8 +1233,12 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   }
   p.ew = ewnew;
   p.dcen = p.dcen - trld;
-  Eta = (trld + Eta * rpre) / rnew;          /* hazard H1: trld, not f (imctrk2d.f:472) */
+  if (V12)
+    Eta = (fr + Eta * rpre) / rnew;          /* src_20121113/imctrk2d.f:478 */
+  else
+    Eta = (trld + Eta * rpre) / rnew;        /* hazard H1: trld, not f (imctrk2d.f:472) */
   Eta = clampd(Eta, lim9);
+  if (V12 && ikind == 1) p.cmfp = colmfp - sigsc * trld;   /* src_20121113/imctrk2d.f:505 */
   const bool leaves = (jnew == P.nz + 1 || jnew == 0 || knew == P.nr + 1 || knew == 0);
 #if C2D_TABLE_COMTOT
   p.eta = Eta;
@@ -1689,7 +1705,7 @@ __device__ __forceinline__ void pf_issue(const KParams& P0, CensRec& r, long lon
 __device__ __forceinline__ void pf_apply(const KParams& P0, Pkt& p, const CensRec& r) {
   const KParams& P = cold(P0);
   p.rpre = r.rpre; p.zpre = r.zpre;
-  p.wmu = clampd(r.wmu, 0.99999999);
+  p.wmu = clampd(r.wmu, P.cens_wlim);               /* imcfield2d.f:119-120 (2012-11: +-1) */
   p.ew = r.ew; p.xnu = r.xnu;
 #if C2D_TABLE_COMTOT
   p.eta = r.cphi;                                    /* encoded azimuth (CensusSoA) */
@@ -1765,6 +1781,7 @@ __device__ __forceinline__ void load_source(const KParams& P0, Pkt& p, long long
 /* Every secondary is an imctrk2d(1) track (imctrk2d.f:662-679) from the
  * packet store; generation 0 (census + sources, the split1 probes and the
  * recombined copy) runs as probe bundles (c2d_bundle_kernel below). */
+template <int V12>
 __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kernel)(const KParams* __restrict__ Pg,
                                                                       const GenArgs A) {
   const KParams& P = *Pg;
@@ -1851,7 +1868,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_transport_kerne
 #ifdef C2D_TR_PROF
       pf.acc[TP_LANES] += __popcll(__ballot(1));
 #endif
-      const int out = flight(P, T, p, cc, lc, pf);
+      const int out = flight<V12>(P, T, p, cc, lc, pf);
       TP_MARK(pf, TP_EVENT);
       if (out != FL_CONT) {
         if (out == FL_COLLIDE) push_scat(P, A.q2_out, A.n2_out, make_rec(p, p.key, p.ctr));
@@ -2000,11 +2017,12 @@ __device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bun
 
 /* probe g0 + i collides at dcol inside the shared step: its own partial
  * step to the collision point (flight(), ikind = 3), then the record */
+template <int V12>
 __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, const GenArgs& A,
                                               Bundle& b, int i, double dcol, double sigabs,
                                               double Eta, double swmu, int eta_switch, int cell,
                                               LaneCnt& lc) {
-  const double lim9 = 0.999999999;
+  const double lim9 = V12 ? 1.0 : 0.999999999;
   const Pkt& p = b.p;
   const double rpre = p.rpre, zpre = p.zpre, wmu = p.wmu;
   const double trld = dcol;
@@ -2032,7 +2050,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
     return;
   }
   LC_ADD(lc, C2D_CNT_COLLIDE);
-  double Eta2 = clampd(FDIV_NN(trld + Eta * rpre, rnew), lim9);   /* H1 */
+  double Eta2 = clampd(FDIV_NN((V12 ? f : trld) + Eta * rpre, rnew), lim9);   /* H1 unless 2012-11 */
   double phi = c2d_acos(Eta2);
   if (eta_switch == -1) phi = 2.0 * PI_REF - phi;
   ScatRec r;
@@ -2054,6 +2072,7 @@ __device__ __forceinline__ void probe_collide(const KParams& P, const Tal& T, co
 }
 
 /* one shared step of the bundle (flight() for every copy on the path) */
+template <int V12>
 __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, const GenArgs& A,
                                             Bundle& b, ComCache& cc, LaneCnt& lc, Prof& pf,
                                             CensRec& nr, long long nitem, int& nst) {
@@ -2062,7 +2081,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
 #else
   const KParams& P = P1;
 #endif
-  const double lim8 = 9.9999999e-1, lim9 = 0.999999999;
+  const double lim8 = V12 ? 1.0 : 9.9999999e-1, lim9 = V12 ? 1.0 : 0.999999999;
   const Geo* g = T.g;
   Pkt& p = b.p;
   if (b.alive && b.ewp < 1.0e-40) b.alive = 0;
@@ -2107,7 +2126,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
   double Eta = c2d_cos(p.phi);
   const int eta_switch = (p.phi <= PI_REF && p.phi >= 1.0e-10) ? 1 : -1;
 #endif
-  Eta = clampd(Eta, lim8);
+  if (!V12) Eta = clampd(Eta, lim8);
   const double rpre = p.rpre, zpre = p.zpre, wmu = p.wmu;
   const double disp = Eta * rpre;
   const double psq = rpre * rpre * (1.0 - Eta * Eta);
@@ -2127,6 +2146,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
   const double disbr = (double)inout * FSQRT(dpbsq) - disp;
   const double swmu = FSQRT(1.0 - wmu * wmu);
   double trldb = FDIV_POS(disbr, swmu);
+  double fr = disbr;                    /* V12: the reference's f on a boundary step */
   const double Zr = zpre + wmu * trldb;
   const double zlow = (p.jph == 1) ? P.zmin : g->z[p.jph - 1];
   const double zup = g->z[p.jph];
@@ -2135,6 +2155,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
     knew = p.kph;
     jnew = (Zr > zup) ? p.jph + 1 : p.jph - 1;
     const double f = FDIV_POS((Zbnd - zpre) * swmu, wmu);   /* wmu != 0 on a z crossing */
+    fr = f;
     rbnd = FSQRT(rpre * rpre + f * f + 2.0 * rpre * f * Eta);
     trldb = FSQRT(f * f + (Zbnd - zpre) * (Zbnd - zpre));
   } else {
@@ -2171,7 +2192,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
       const int i = __ffs(m) - 1;
       b.alive &= ~(1u << i);
       n--;
-      probe_collide(P, T, A, b, i, dcol, sigabs, Eta, swmu, eta_switch, cell, lc);
+      probe_collide<V12>(P, T, A, b, i, dcol, sigabs, Eta, swmu, eta_switch, cell, lc);
       dpos = dcol;
       if (n == 0) break;
       b.tau = FDIV_POS(-FLOG(UB(b)), (double)n);
@@ -2217,11 +2238,13 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
       jnew = p.jph;
       knew = p.kph;
       const double f = trld * swmu;
+      fr = f;
       rnew = FSQRT(f * f + rpre * rpre + 2.0 * f * rpre * Eta);
       znew = zpre + trld * wmu;
     }
     p.dcen = p.dcen - trld;
-    double Etan = FDIV_NN(trld + Eta * rpre, rnew);   /* hazard H1: trld, not f (imctrk2d.f:472) */
+    /* hazard H1: trld, not f (imctrk2d.f:472); f in src_20121113:478 */
+    double Etan = FDIV_NN((V12 ? fr : trld) + Eta * rpre, rnew);
     Etan = clampd(Etan, lim9);
     const bool leaves = bnd && (jnew == P.nz + 1 || jnew == 0 || knew == P.nr + 1 || knew == 0);
 #if C2D_TABLE_COMTOT
@@ -2351,6 +2374,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
   TP_MARK(pf, TP_PTS);
 }
 
+template <int V12>
 __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(const KParams* __restrict__ Pg,
                                                                    const GenArgs A) {
   const KParams& P = *Pg;
@@ -2495,7 +2519,7 @@ __global__ void __launch_bounds__(BLOCK) C2D_TR_ATTR C2D_SFX(c2d_bundle_kernel)(
 #ifdef C2D_TR_PROF
       pf.acc[TP_LANES] += __popcll(__ballot(1));
 #endif
-      bundle_step(P, T, A, b, cc, lc, pf, nr, nitem, nst);
+      bundle_step<V12>(P, T, A, b, cc, lc, pf, nr, nitem, nst);
       TP_MARK(pf, TP_EVENT);
       if (!b.alive && !(b.flags & BF_TRACK)) {
         if ((b.flags & (BF_TKILL | BF_RERUN)) == BF_TKILL)
@@ -2607,31 +2631,43 @@ __global__ void __launch_bounds__(256) c2d_comtab_gemm(const double* f_nt, const
 /* ------------------------------------------------------------------ */
 /* launchers (called from capi.cpp)                                    */
 /* ------------------------------------------------------------------ */
+/* trk: c2d_config.trk_variant (0: src/imctrk2d.f, 1: src_20121113) */
 extern "C" int C2D_SFX(c2d_launch_transport)(const c2d::KParams* P_dev, const c2d::GenArgs* A, int grid,
-                                             size_t lds_bytes, hipStream_t stream) {
-  hipLaunchKernelGGL(C2D_SFX(c2d::c2d_transport_kernel), dim3(grid), dim3(c2d::BLOCK), lds_bytes,
-                     stream, P_dev, *A);
+                                             size_t lds_bytes, int trk, hipStream_t stream) {
+  if (trk)
+    hipLaunchKernelGGL(C2D_SFX(c2d::c2d_transport_kernel)<1>, dim3(grid), dim3(c2d::BLOCK), lds_bytes,
+                       stream, P_dev, *A);
+  else
+    hipLaunchKernelGGL(C2D_SFX(c2d::c2d_transport_kernel)<0>, dim3(grid), dim3(c2d::BLOCK), lds_bytes,
+                       stream, P_dev, *A);
   return (int)hipGetLastError();
 }
 
 static int C2D_SFX(bundle_lds_attr)(size_t lds_bytes) {
   if (lds_bytes <= 64 * 1024) return 0;
-  return (int)hipFuncSetAttribute((const void*)C2D_SFX(c2d::c2d_bundle_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  for (const void* k : {(const void*)C2D_SFX(c2d::c2d_bundle_kernel)<0>,
+                        (const void*)C2D_SFX(c2d::c2d_bundle_kernel)<1>})
+    if (hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes))
+      return (int)e;
+  return 0;
 }
 
 extern "C" int C2D_SFX(c2d_launch_bundle)(const c2d::KParams* P_dev, const c2d::GenArgs* A, int grid,
-                                          size_t lds_bytes, hipStream_t stream) {
+                                          size_t lds_bytes, int trk, hipStream_t stream) {
   if (int e = C2D_SFX(bundle_lds_attr)(lds_bytes)) return e;
-  hipLaunchKernelGGL(C2D_SFX(c2d::c2d_bundle_kernel), dim3(grid), dim3(c2d::BLOCK), lds_bytes,
-                     stream, P_dev, *A);
+  if (trk)
+    hipLaunchKernelGGL(C2D_SFX(c2d::c2d_bundle_kernel)<1>, dim3(grid), dim3(c2d::BLOCK), lds_bytes,
+                       stream, P_dev, *A);
+  else
+    hipLaunchKernelGGL(C2D_SFX(c2d::c2d_bundle_kernel)<0>, dim3(grid), dim3(c2d::BLOCK), lds_bytes,
+                       stream, P_dev, *A);
   return (int)hipGetLastError();
 }
 
 extern "C" int C2D_SFX(c2d_bundle_occupancy)(int* blocks_per_cu, size_t lds_bytes) {
   if (C2D_SFX(bundle_lds_attr)(lds_bytes) != 0) { *blocks_per_cu = 0; return 0; }
   return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      blocks_per_cu, C2D_SFX(c2d::c2d_bundle_kernel), c2d::BLOCK, lds_bytes);
+      blocks_per_cu, C2D_SFX(c2d::c2d_bundle_kernel)<0>, c2d::BLOCK, lds_bytes);
 }
 
 extern "C" int C2D_SFX(c2d_launch_source)(const c2d::KParams* P_dev, int grid, hipStream_t stream) {
@@ -2658,7 +2694,7 @@ extern "C" int C2D_SFX(c2d_aux_occupancy)(int which, int* blocks_per_cu) {
 
 extern "C" int C2D_SFX(c2d_transport_occupancy)(int* blocks_per_cu, size_t lds_bytes) {
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      blocks_per_cu, C2D_SFX(c2d::c2d_transport_kernel), c2d::BLOCK, lds_bytes);
+      blocks_per_cu, C2D_SFX(c2d::c2d_transport_kernel)<0>, c2d::BLOCK, lds_bytes);
   return (int)e;
 }
 

@@ -188,6 +188,9 @@ c     hazard H3: census + volume transport see the previous kappa_tot
       cfg%census_capacity = ccap
       cfg%event_capacity = ecap
       cfg%queue_capacity = qcap
+c     the tracker of the host's snapshot: src/ (0, default) or
+c     src_20121113/ (1: the azimuth fix of hazard H1, compton2d.h)
+      cfg%trk_variant = int(c2d_shim_env('C2D_SHIM_TRK_VARIANT', 0_8))
       rc = c2d_init(cfg, ctx)
       if (rc .ne. C2D_OK) call c2d_shim_fail(ctx, 'c2d_init', rc)
       end

@@ -69,6 +69,20 @@ extern "C" {
 #define C2D_COMTOT_EXACT  0   /* 199-term electron-spectrum sum per call (reference)   */
 #define C2D_COMTOT_TABLE  1   /* per-cell cubic table in log(xnu), rebuilt every step  */
 
+/* c2d_config.trk_variant: which snapshot of the reference's tracker
+ * (SURVEY.md §8 hazard H1).  C2D_TRK_SRC (default) is src/imctrk2d.f, bug
+ * for bug: the azimuth update uses the 3-D path, Eta = (trld + Eta*rpre)/rnew
+ * (:472), a fresh colmfp after every cell boundary (`go to 100`, :518-525),
+ * the clamps |wmu| <= 0.99999999 and |Eta| <= 0.999999999 (:161-162,
+ * :243-244, :474-476; imcfield2d.f:119-120).  C2D_TRK_2012_11 is
+ * src_20121113/imctrk2d.f: Eta = (f + Eta*rpre)/rnew with f the path's
+ * projection on the r-plane (:477-479), colmfp kept across boundaries
+ * (`go to 110` with colmfp -= sigsc*trld, :505, :526-533; sigabs reset
+ * after 110, :159), no idead = 4 re-entry (:521-524), and |wmu|, |Eta|
+ * clamped to 1 (:162-167, :481-484; imcfield2d.f:119-124). */
+#define C2D_TRK_SRC       0
+#define C2D_TRK_2012_11   1
+
 typedef struct c2d_array3 { const double* data; int64_t s_i, s_j, s_k; } c2d_array3;
 typedef struct c2d_array2 { const double* data; int64_t s_j, s_k; } c2d_array2;
 typedef struct c2d_iarray2 { const int32_t* data; int64_t s_j, s_k; } c2d_iarray2;
@@ -121,6 +135,7 @@ typedef struct c2d_config {
                                      chunked SoA (64 B per record + 1/16 slack: a
                                      step refills the 1024-record chunks its census
                                      sources have finished with)     */
+  int32_t trk_variant;            /* C2D_TRK_SRC (0, default) | C2D_TRK_2012_11    */
 } c2d_config;
 
 /* Per-step inputs (what imcgen2d/volume_em/file_sp leave in COMMON). */

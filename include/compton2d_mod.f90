@@ -18,6 +18,7 @@ module compton2d
   integer(c_int32_t), parameter :: C2D_FP_EXACT = 0, C2D_FP_FAST = 1
   integer, parameter :: C2D_COMM_ID_BYTES = 128
   integer(c_int32_t), parameter :: C2D_COMTOT_EXACT = 0, C2D_COMTOT_TABLE = 1
+  integer(c_int32_t), parameter :: C2D_TRK_SRC = 0, C2D_TRK_2012_11 = 1
   integer, parameter :: C2D_NCOUNTERS = 16, C2D_CNT_STEPS = 0, C2D_CNT_ESCAPES = 1, &
        C2D_CNT_CENSUS = 2
 
@@ -56,6 +57,7 @@ module compton2d
      integer(c_int64_t) :: census_capacity = 5000000, event_capacity = 5000000, &
           queue_capacity = 262144
      integer(c_int32_t) :: census_inplace = 0
+     integer(c_int32_t) :: trk_variant = 0
   end type c2d_config
 
   type, bind(C) :: c2d_step_in

@@ -320,6 +320,7 @@ typedef struct c2o_ctx {
   int split1, split2, split3, spl3_trg;
   int probe_bundles;            /* lineage mode: split1 probes as bundles (C2O_PROBE_BUNDLES=0: per copy) */
   int spec_switch, cr_sent, pair_switch, kappa_lag, rand_switch;
+  int trk2012;                  /* c2d_config.trk_variant == C2D_TRK_2012_11 */
   int rng_mode, h4_stale;
   /* MPI-worker emulation (c2o_set_dt_lag): the workers receive dt only in
    * z_surf_bcast (src/surf_mpi.f:68), after their census and volume jobs,
@@ -750,17 +751,27 @@ static void collision(c2o_ctx* c, pkt_t* p, int scat_flag, rng_t* g) {
 
 /* one packet copy: label 100 ... 900 of imctrk2d.f; returns 1 if it scattered */
 static int flight_loop(c2o_ctx* c, pkt_t* p, int s, rng_t* g, double wtmin) {
-  const double lim8 = 9.9999999e-1, lim9 = 0.999999999;
+  /* src/imctrk2d.f clamps |wmu| to 0.99999999 at label 110 and |Eta| to
+   * 0.99999999 / 0.999999999; src_20121113 clamps both to 1 (:162-167, :481-484) */
+  const int v12 = c->trk2012;
+  const double lim8 = v12 ? 1.0 : 9.9999999e-1, lim9 = v12 ? 1.0 : 0.999999999;
+  double colmfp = 0.0;
+  int at100 = 1;
   for (;;) {
     double sigabs = 1.0e-40, mb_ran;                   /* label 100 */
-    if (s == 0) {
-      mb_ran = 1.0e-10;
-    } else {
-      mb_ran = U(g);
-      if (c->rand_switch == 2) mb_ran = (double)(int32_t)(mb_ran * 1.0e6) / 1.0e6 + 1.0e-6 * U(g);
+    if (at100) {
+      if (s == 0) {
+        mb_ran = 1.0e-10;
+      } else {
+        mb_ran = U(g);
+        if (c->rand_switch == 2) mb_ran = (double)(int32_t)(mb_ran * 1.0e6) / 1.0e6 + 1.0e-6 * U(g);
+      }
+      if (!(mb_ran > 0.0)) continue;
+      colmfp = -LOG(mb_ran);
     }
-    if (!(mb_ran > 0.0)) continue;
-    double colmfp = -LOG(mb_ran);
+    /* after a cell boundary src re-enters at label 100 (a fresh colmfp,
+     * imctrk2d.f:518-525), src_20121113 at label 110 (:526-533) */
+    at100 = !v12;
     if (p->ew < 1.0e-40) return 0;                     /* label 110 */
     p->wmu = clampd(p->wmu, lim8);
     int cell = CELL(c, p->jph, p->kph);
@@ -793,7 +804,7 @@ static int flight_loop(c2o_ctx* c, pkt_t* p, int s, rng_t* g, double wtmin) {
     /* geometry (imctrk2d.f:228-379) */
     double Eta = COS(p->phi);
     int eta_switch = (p->phi <= PI_REF && p->phi >= 1.0e-10) ? 1 : -1;
-    Eta = clampd(Eta, lim8);
+    if (!v12) Eta = clampd(Eta, lim8);                 /* commented out in src_20121113:248-249 */
     double rpre = p->rpre, zpre = p->zpre, wmu = p->wmu;
     double disp = Eta * rpre;
     double psq = rpre * rpre * (1.0 - Eta * Eta);
@@ -889,13 +900,17 @@ static int flight_loop(c2o_ctx* c, pkt_t* p, int s, rng_t* g, double wtmin) {
     }
     p->ew = ewnew;
     p->dcen = p->dcen - trld;
-    Eta = (trld + Eta * rpre) / rnew;                  /* hazard H1: trld, not f */
+    if (v12)
+      Eta = (f + Eta * rpre) / rnew;                   /* src_20121113/imctrk2d.f:478 */
+    else
+      Eta = (trld + Eta * rpre) / rnew;                /* hazard H1: trld, not f */
     Eta = clampd(Eta, lim9);
     p->phi = ACOS(Eta);
     if (eta_switch == -1) p->phi = 2.0 * PI_REF - p->phi;
     p->rpre = rnew;
     p->zpre = znew;
     if (ikind == 1) {
+      colmfp = colmfp - sigsc * trld;                  /* imctrk2d.f:497 / src_20121113:505 */
       if (jnew == c->nz + 1 || jnew == 0 || knew == c->nr + 1 || knew == 0) {
         p->jph = jnew;
         p->kph = knew;
@@ -944,7 +959,8 @@ static int flight_loop(c2o_ctx* c, pkt_t* p, int s, rng_t* g, double wtmin) {
 #define C2O_BUNDLE_MAX 32
 static int probe_bundle(c2o_ctx* c, const pkt_t* src, double s_ew, double wtmin, int g0, int G,
                         const rng_t* g) {
-  const double lim8 = 9.9999999e-1, lim9 = 0.999999999;
+  const int v12 = c->trk2012;
+  const double lim8 = v12 ? 1.0 : 9.9999999e-1, lim9 = v12 ? 1.0 : 0.999999999;
   rng_t gb = rng_sub(g, C2D_SUB_BUNDLE | (uint32_t)g0);
   uint32_t actr = 0;                                 /* point-stream outputs */
   pkt_t p = *src;
@@ -970,7 +986,7 @@ static int probe_bundle(c2o_ctx* c, const pkt_t* src, double s_ew, double wtmin,
     double xqsqleft = (p.kph == 1) ? c->rmin * c->rmin : c->r[p.kph - 1] * c->r[p.kph - 1];
     double Eta = COS(p.phi);
     int eta_switch = (p.phi <= PI_REF && p.phi >= 1.0e-10) ? 1 : -1;
-    Eta = clampd(Eta, lim8);
+    if (!v12) Eta = clampd(Eta, lim8);
     const double rpre = p.rpre, zpre = p.zpre, wmu = p.wmu;
     double disp = Eta * rpre;
     double psq = rpre * rpre * (1.0 - Eta * Eta);
@@ -989,6 +1005,7 @@ static int probe_bundle(c2o_ctx* c, const pkt_t* src, double s_ew, double wtmin,
     if (dpbsq < 1.0e-6) dpbsq = 1.0e-6;
     double disbr = (double)inout * SQRT(dpbsq) - disp;
     double trldb = disbr / SQRT(1.0 - wmu * wmu);
+    f = disbr;
     double Zr = zpre + wmu * trldb;
     double zlow = (p.jph == 1) ? c->zmin : c->z[p.jph - 1];
     if (Zr > c->z[p.jph] || Zr < zlow) {
@@ -1049,7 +1066,7 @@ static int probe_bundle(c2o_ctx* c, const pkt_t* src, double s_ew, double wtmin,
       } else {
         q.ew = ewnew;
         q.dcen = p.dcen - trc;
-        double Eta2 = clampd((trc + Eta * rpre) / rnew, lim9);   /* H1 */
+        double Eta2 = clampd(((v12 ? fc : trc) + Eta * rpre) / rnew, lim9);   /* H1 unless 2012-11 */
         q.phi = ACOS(Eta2);
         if (eta_switch == -1) q.phi = 2.0 * PI_REF - q.phi;
         q.rpre = rnew;
@@ -1105,7 +1122,7 @@ static int probe_bundle(c2o_ctx* c, const pkt_t* src, double s_ew, double wtmin,
       znew = zpre + trld * wmu;
     }
     p.dcen = p.dcen - trld;
-    Eta = (trld + Eta * rpre) / rnew;                  /* hazard H1 */
+    Eta = ((v12 ? f : trld) + Eta * rpre) / rnew;      /* hazard H1 unless 2012-11 */
     Eta = clampd(Eta, lim9);
     p.phi = ACOS(Eta);
     if (eta_switch == -1) p.phi = 2.0 * PI_REF - p.phi;
@@ -1454,6 +1471,7 @@ c2o_ctx* c2o_create(const c2d_config* cfg, int rng_mode, int rand_switch, int32_
   c->cr_sent = cfg->cr_sent;
   c->pair_switch = cfg->pair_switch;
   c->kappa_lag = cfg->kappa_lag;
+  c->trk2012 = cfg->trk_variant == C2D_TRK_2012_11;
   c->rng_mode = rng_mode;
   c->rand_switch = rand_switch;
   c->rseed = rseed;
@@ -1562,7 +1580,7 @@ int c2o_step(c2o_ctx* c, const c2d_step_in* in) {
       g.ctr = 0;
     }
     P.dcen = C_LIGHT * c->dt;
-    P.wmu = clampd(P.wmu, 0.99999999);
+    P.wmu = clampd(P.wmu, c->trk2012 ? 1.0 : 0.99999999);   /* imcfield2d.f:119-120 (2012-11: 119-124) */
     TALLY(c, counters + C2D_CNT_SOURCES) += 1.0;
     imctrk2d(c, &P, -1, &g);
     if (c->err) return c->err;

@@ -48,6 +48,25 @@ objs=""
 for f in $OBJS; do objs="$objs $OUT/obj/$f.o"; done
 "$FC" -o "$OUT/c2d_refdrv" "$OUT/obj/c2d_refdrv.o" $objs \
   -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
+# the same driver over the 2012-11 snapshot's tracker (c2d_config.trk_variant =
+# C2D_TRK_2012_11): src_20121113/imctrk2d.f and its
+# imcfield2d.f (the census |wmu| clamp) in place of src/'s; every other
+# object, and the COMMON blocks (commonblock.f, general.pa: identical in both
+# snapshots), are src/'s
+SRC12="${C2D_REFERENCE_SRC12:-$(dirname "$SRC")/src_20121113}"
+if [ -d "$SRC12" ]; then
+  mkdir -p "$OUT/obj/v2012"
+  for f in imctrk2d imcfield2d; do
+    "$FC" -c $FFLAGS -I"$MPI_INC" -I"$SRC" -module-dir "$OUT/mod" "$SRC12/$f.f" -o "$OUT/obj/v2012/$f.o"
+  done
+  objs12=""
+  for f in $OBJS; do
+    case $f in imctrk2d|imcfield2d) objs12="$objs12 $OUT/obj/v2012/$f.o" ;; *) objs12="$objs12 $OUT/obj/$f.o" ;; esac
+  done
+  "$FC" -o "$OUT/c2d_refdrv_2012" "$OUT/obj/c2d_refdrv.o" $objs12 \
+    -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi
+  echo "build_ref: $OUT/c2d_refdrv_2012"
+fi
 "$FC" -c $FFLAGS -I"$MPI_INC" -I"$SRC" -module-dir "$OUT/mod" \
   "$HERE/c2d_censdrv.f" -o "$OUT/obj/c2d_censdrv.o"
 "$FC" -o "$OUT/c2d_censdrv" "$OUT/obj/c2d_censdrv.o" "$OUT/obj/census2d.o" \

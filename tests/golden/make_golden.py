@@ -59,6 +59,12 @@ CASES = {
     # 1024-cell indexing, LDS-privatised tallies of 1024 cells (32 KB) and the
     # n_field of 1024 cells; nst = 2e5 so every cell is visited
     "c2_32x32": dict(case=dict(nz=32, nr=32, n_e=80.0, nst=200000), nsteps=2),
+    # the 2012-11 snapshot's tracker (c2d_config.trk_variant = C2D_TRK_2012_11,
+    # SURVEY.md §8 H1): src_20121113/imctrk2d.f + imcfield2d.f linked into
+    # the driver (oracle/ref/build_ref.sh c2d_refdrv_2012) on ssc_tau's deck
+    # (collisions, split3, census) and grid3x4's (12 cells, 2 angular bins)
+    "ssc_tau_2012": dict(case=dict(nz=2, nr=2, n_e=4.0e6, nst=2000), nsteps=3, trk_variant=1),
+    "grid3x4_2012": dict(case=dict(nz=3, nr=4, n_e=1.0e6, nst=1500, nmu=2), nsteps=2, trk_variant=1),
 }
 
 # C3: the Mrk 421 SSC deck src_20121026/input.dat:1-130 +
@@ -106,11 +112,12 @@ def run_case(name: str, spec: dict, out_dir: Path, work: Path, fp: bool = False)
         shutil.rmtree(d)
     refcase.write_input_deck(d, spec["case"])
     refcase.run_reference(d, spec["nsteps"], klag=1, nforceu=spec.get("nforceu", 0),
-                          timeout=7200 if fp else 600)
+                          timeout=7200 if fp else 600, trk_variant=spec.get("trk_variant", 0))
     cfg = refcase.read_config(d)
     arrays = {}
     meta = {k: v for k, v in cfg.items() if not isinstance(v, np.ndarray)}
     meta["nsteps"] = spec["nsteps"]
+    meta["trk_variant"] = spec.get("trk_variant", 0)
     meta["case"] = spec["case"]
     for k, v in cfg.items():
         if isinstance(v, np.ndarray):

@@ -11,7 +11,7 @@ from compton2d_amd import abi
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
 CASES = ("ssc_tau", "ec_lower", "grid3x4", "ec_upper", "bb_upper", "c3_mrk421", "c1_ec1x1",
-         "c2_32x32")
+         "c2_32x32", "ssc_tau_2012", "grid3x4_2012")
 IN_KEYS = ("kappa_tot", "eps_tot", "eps_th", "f_nt", "Pnt", "n_e", "Eloss_th", "Eloss_tot",
            "zsurf", "ewsv", "nsv", "nsurfi", "nsurfo", "ewsurfi", "ewsurfo", "nsurfu", "nsurfl",
            "ewsurfu", "ewsurfl", "tbbi", "tbbo", "tbbu", "tbbl")
@@ -42,7 +42,8 @@ class GoldenCase:
             E_ph=a["E_ph"], E_field=a["cfg_E_field"], gnt=a["cfg_gnt"], hu=a["cfg_hu"],
             Elcmin=a["cfg_Elcmin"], Elcmax=a["cfg_Elcmax"], mu=a["cfg_mu"], split1=m["split1"],
             split2=m["split2"], split3=m["split3"], spl3_trg=m["spl3_trg"],
-            spec_switch=m["spec_switch"], cr_sent=m["cr_sent"], pair_switch=m["pair_switch"])
+            spec_switch=m["spec_switch"], cr_sent=m["cr_sent"], pair_switch=m["pair_switch"],
+            trk_variant=m.get("trk_variant", 0))
         for k, v in over.items():
             setattr(g, k, v)
         return g

@@ -21,6 +21,7 @@ from compton2d_amd import abi
 
 ROOT = Path(__file__).resolve().parents[1]
 REFDRV = ROOT / "oracle" / "_ref" / "c2d_refdrv"
+REFDRV12 = ROOT / "oracle" / "_ref" / "c2d_refdrv_2012"
 REFERENCE = Path(os.environ.get("C2D_REFERENCE", "/root/reference"))
 
 BASE_CASE = dict(
@@ -131,16 +132,18 @@ def write_input_deck(case_dir: Path, case: dict) -> None:
 
 
 def run_reference(case_dir: Path, nsteps: int, klag: int = 1, timeout: int = 600,
-                  nforceu: int = 0) -> None:
+                  nforceu: int = 0, trk_variant: int = 0) -> None:
     """Run c2d_refdrv; nforceu > 0 gives blackbody upper rings (tbbu > 0)
-    nforceu packets each (see oracle/ref/c2d_refdrv.f)."""
-    if not REFDRV.exists():
+    nforceu packets each (see oracle/ref/c2d_refdrv.f).  trk_variant = 1:
+    the driver linked with src_20121113's tracker (c2d_refdrv_2012)."""
+    exe = REFDRV12 if trk_variant else REFDRV
+    if not exe.exists():
         raise FileNotFoundError("reference driver not built: run oracle/ref/build_ref.sh")
     import resource
 
     def big_stack():   # the reference needs `ulimit -s unlimited` (SURVEY.md §5)
         resource.setrlimit(resource.RLIMIT_STACK, (resource.RLIM_INFINITY, resource.RLIM_INFINITY))
-    subprocess.run([str(REFDRV), str(nsteps), str(klag), str(nforceu)], cwd=str(case_dir),
+    subprocess.run([str(exe), str(nsteps), str(klag), str(nforceu)], cwd=str(case_dir),
                    check=True, timeout=timeout, stdout=subprocess.DEVNULL,
                    stderr=subprocess.DEVNULL, preexec_fn=big_stack)
 

@@ -48,6 +48,7 @@ int main(void) {
   P(c2d_fp_step_in, n_field) P(c2d_fp_step_in, ecens) P(c2d_fp_step_in, dt)
   P(c2d_fp_step_out, zone_diag) P(c2d_fp_step_out, dT_max) P(c2d_fp_step_out, p_nth)
   P(c2d_config, seed) P(c2d_config, rank) P(c2d_config, queue_capacity) P(c2d_config, mu)
+  P(c2d_config, census_inplace) P(c2d_config, trk_variant)
   P(c2d_step_in, kappa_tot) P(c2d_step_in, nsv) P(c2d_step_in, tbbl) P(c2d_step_in, spectra)
   P(c2d_step_in, n_spectra) P(c2d_step_in, dt) P(c2d_step_in, device_tables)
   printf("c2d_obs_bins %zu\nc2d_vem_in %zu\nc2d_vem_out %zu\n", sizeof(c2d_obs_bins),
@@ -111,6 +112,15 @@ def test_init_rejects_event_capacity_below_shard_count():
     device call."""
     from golden_io import GoldenCase
     g = GoldenCase("ssc_tau").grid(event_capacity=31)
+    with pytest.raises(engine.C2DError) as e:
+        engine.Engine(g)
+    assert "C2D_E_ARG" in str(e.value)
+
+
+def test_init_rejects_an_unknown_tracker_variant():
+    """c2d_config.trk_variant is C2D_TRK_SRC (0) or C2D_TRK_2012_11 (1)."""
+    from golden_io import GoldenCase
+    g = GoldenCase("ssc_tau").grid(trk_variant=2)
     with pytest.raises(engine.C2DError) as e:
         engine.Engine(g)
     assert "C2D_E_ARG" in str(e.value)

@@ -72,7 +72,7 @@ def test_exact_kernel_bit_parity_with_oracle(name):
         np.testing.assert_array_equal(sort_rows(eg), sort_rows(eo))
 
 
-@pytest.mark.parametrize("name", ["ssc_tau", "c3_mrk421", "c1_ec1x1"])
+@pytest.mark.parametrize("name", ["ssc_tau", "c3_mrk421", "c1_ec1x1", "ssc_tau_2012"])
 def test_exact_kernel_bit_parity_in_place_census(name):
     """The in-place census mode (c2d_config.census_inplace) tracks the same
     histories: counters and census records (by key) equal the oracle's."""
