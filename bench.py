@@ -171,17 +171,33 @@ def cpu_baseline(eng, run, target_s: float = 12.0) -> dict:
     ncell = wl.grid.nz * wl.grid.nr
     step_s = tr_s * stride + fp_s_zone * ncell / cores
     cpu_steps = tr_steps * stride                # the whole step's packet-steps on the CPU
+    # the port's speed against the reference's own Fortran on the same C3
+    # transport work (bitwise-identical histories, one process each; measured
+    # in the build container by tools/fortran_vs_port.py: the Fortran does not
+    # travel to this box)
+    fvp = None
+    fp_path = ROOT / "profiles" / "r06c" / "fortran_vs_port.json"
+    if fp_path.exists():
+        fvp = json.loads(fp_path.read_text())
     return {"value": cpu_steps / step_s, "unit": "packet-steps/s", "cores": cores, "kind": "port",
-            "algorithm": "reference (per-copy split1 probes, lagged-Fibonacci streams reseeded per "
-                         "census packet, exact comtot, glibc libm)",
+            "algorithm": "the reference's algorithm restated in C (oracle/c2d_oracle.c reference mode: "
+                         "per-copy split1 probes, lagged-Fibonacci streams reseeded per census packet, "
+                         "exact comtot, glibc libm); bit-exact results, not the Fortran's code or speed",
+            "port_speed_vs_fortran": None if fvp is None else round(fvp["port_speed_vs_fortran"], 3),
+            "port_speed_source": None if fvp is None else (
+                "profiles/r06c/fortran_vs_port.json: the C3 deck (nst %d, %d steps, %.3g packet-steps), "
+                "Fortran %.3g vs port %.3g packet-steps/s on one core each, bitwise-identical tallies and "
+                "census" % (fvp["nst"], fvp["steps"], fvp["packet_steps"], fvp["fortran_packet_steps_per_s"],
+                            fvp["port_packet_steps_per_s"])),
             "sample": ("the C3 step after this run's last timed step: every %d-th census record "
                        "the GPU left (%d of %d) + 1/%d of the step's volume sources, over %d "
                        "processes = reference workers (census records strided, volume zones "
                        "j*nr+k mod %d; host nproc %d, CPU share %d); C oracle in its reference mode "
-                       "= the reference's algorithm as the Fortran runs it (per-copy split1 probes, "
+                       "= the reference's algorithm restated in C (per-copy split1 probes, "
                        "no bundles; rand_switch=1 lagged-Fibonacci zone streams and the 10000-number "
                        "reseed per census packet, src/imcfield2d.f:115-116; exact 199-term comtot; "
-                       "glibc libm; bit-exact to the Fortran in tests/test_oracle_golden.py): %.0f "
+                       "glibc libm; bit-exact to the Fortran in tests/test_oracle_golden.py; see "
+                       "port_speed_vs_fortran for its speed against the Fortran): %.0f "
                        "packet-steps in %.2f s; FP_calc of %d zones at %.2f s/zone; whole coupled "
                        "step extrapolated = %.2f s x %d + %.2f s/zone x %d zones / %d cores = %.1f s "
                        "for %.3g packet-steps (pool wall %.1f s)"

@@ -189,13 +189,14 @@ def rebalance_census(d6, i5, keys, device=None):
     return _unpack(np.concatenate(parts) if parts else rec[:0])
 
 
-def rebalance_engine_census(engine, threshold: float = 0.1, device=None) -> bool:
+def rebalance_engine_census(engine, threshold: float = 0.1, device=None, packed=None) -> bool:
     """imcredist for an Engine: when the largest census exceeds the mean by
     more than `threshold`, level the census counts (all ranks call it).  On
     the nccl backend (RCCL) the records never leave the GPUs: the surplus tail
     is packed on the device (c2d_census_pack), sent with RCCL send/recv and
     appended on the receiving GPU (c2d_census_append); on gloo they go
-    through the host (export / import)."""
+    through the host (export / import).  `packed` forces either path (the
+    packed one on host tensors: the CPU tests drive it with gloo)."""
     if not is_dist():
         return False
     import torch
@@ -209,7 +210,9 @@ def rebalance_engine_census(engine, threshold: float = 0.1, device=None) -> bool
     mean = float(t.item()) / dist.get_world_size()
     if mean <= 0 or float(mx.item()) <= (1.0 + threshold) * mean:
         return False
-    if device.type == "cuda":
+    if packed is None:
+        packed = device.type == "cuda"
+    if packed:
         _rebalance_device(engine, device)
     else:
         d6, i5, keys = engine.census()
@@ -245,7 +248,8 @@ def _rebalance_device(engine, device) -> None:
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
-    torch.cuda.synchronize(device)
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
     engine.census_truncate(keep)
     for t in recvs:
         engine.census_append(t.data_ptr(), t.shape[0])

@@ -40,7 +40,7 @@ c
       integer seeds_sv(jmax,kmax)
       double precision kap_cur(n_vol,jmax,kmax)
       double precision kap_prev(n_vol,jmax,kmax)
-      double precision t_average
+      double precision t_average, tw0, tw1, tw2, tw3
       character*32 arg
       character*40 fn
       save kap_cur, kap_prev, seeds_sv
@@ -163,11 +163,14 @@ c        census transport with the worker's previous kappa_tot (H3)
          seeds_sv = seeds
          kap_cur = kappa_tot
          if (klag.eq.1) kappa_tot = kap_prev
+         tw0 = MPI_WTIME()
          call field_calc
+         tw1 = MPI_WTIME()
          seeds = seeds_sv
          do 30 zone = 1, nz*nr
             call vol_calc(zone)
  30      continue
+         tw2 = MPI_WTIME()
          kappa_tot = kap_cur
          do 40 js = 1, nz
             call z_surf_calc(js)
@@ -175,7 +178,13 @@ c        census transport with the worker's previous kappa_tot (H3)
          do 50 ks = 1, nr
             call r_surf_calc(ks)
  50      continue
+         tw3 = MPI_WTIME()
          kap_prev = kap_cur
+c        wall time of this step's transport legs (census, volume,
+c        surfaces; tools/fortran_vs_port.py)
+         open(unit=u, file='transport_times.txt', access='append')
+         write(u, '(i6,3(1x,e16.9))') n, tw1 - tw0, tw2 - tw1, tw3 - tw2
+         close(u)
 c
 c        worker tallies of this step
          write(fn, '(a,i3.3,a)') 'out_', n, '.bin'

@@ -188,3 +188,144 @@ def test_rebalanced_census_leaves_tallies_unchanged():
         np.testing.assert_array_equal(got[n][c0:c0 + 8], ref[c0:c0 + 8])
         np.testing.assert_allclose(got[n], ref, rtol=1e-11, atol=1e-13 * np.abs(ref).max())
     o.close()
+
+
+# ---------------------------------------------------------------------------
+# rebalance_engine_census (imcredist for an Engine, src/imcredist.f:18-123),
+# the call an N > 1 run makes, on gloo world 2 with a census skewed first to
+# rank 0 and then to rank 1, so records move in both directions
+# ---------------------------------------------------------------------------
+class _OracleEngine:
+    """The Engine census interface (census_count / census / import_census)
+    over an oracle context: rebalance_engine_census's export/import path."""
+
+    def __init__(self, o):
+        self.o = o
+
+    def census_count(self):
+        return int(self.o.lib.c2o_census_count(self.o.ctx))
+
+    def census(self):
+        return self.o.census()
+
+    def import_census(self, d6, i5, keys):
+        assert self.o.import_census(d6, i5, keys) == 0
+
+
+class _PackedEngine:
+    """The Engine's packed-record interface (census_count / census_pack /
+    census_append / census_truncate on c2d_census_pack's 8-word records,
+    abi.CENSUS_REC_WORDS) over a host array: the device path's plan,
+    offsets, truncation and append order, driven with host tensors."""
+
+    def __init__(self, rec):
+        self.rec = np.array(rec, np.int64).reshape(-1, abi.CENSUS_REC_WORDS)
+
+    def census_count(self):
+        return len(self.rec)
+
+    def census_pack(self, off, m, ptr):
+        import ctypes
+        assert 0 <= off and off + m <= len(self.rec)
+        ctypes.memmove(ptr, self.rec[off:off + m].ctypes.data, m * abi.CENSUS_REC_WORDS * 8)
+
+    def census_truncate(self, keep):
+        assert 0 <= keep <= len(self.rec)
+        self.rec = self.rec[:keep]
+
+    def census_append(self, ptr, m):
+        import ctypes
+        add = np.empty((m, abi.CENSUS_REC_WORDS), np.int64)
+        ctypes.memmove(add.ctypes.data, ptr, m * abi.CENSUS_REC_WORDS * 8)
+        self.rec = np.concatenate([self.rec, add])
+
+
+def _engine_rebalance_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    distributed.init(backend="gloo")
+    out = {}
+    # export/import path: the oracle's own census after a step of ssc_tau
+    # (the ranks' lineage shards), skewed to rank 0, levelled, then the
+    # surplus of a second step skewed to rank 1, levelled again
+    gc = GoldenCase("ssc_tau")
+    o = OL.Oracle(gc.grid(rank=rank, world=world), OL.RNG_LINEAGE, "det")
+    assert o.step(gc.step_inputs(0)) == 0
+    eng = _OracleEngine(o)
+    d6, i5, keys = _skew_to_rank0(*o.census())
+    eng.import_census(d6, i5, keys)
+    before = eng.census()
+    moved0 = distributed.rebalance_engine_census(eng, packed=False)
+    after0 = eng.census()
+    d6, i5, keys = eng.census()
+    if rank == 1:     # rank 1 takes a copy of rank 0's records under fresh keys
+        extra = 3 * len(keys)
+        d6 = np.concatenate([d6] + [d6] * 3)
+        i5 = np.concatenate([i5] + [i5] * 3)
+        keys = np.concatenate([keys] + [keys + np.uint64((i + 1) << 40) for i in range(3)])
+        assert len(keys) == 4 * len(after0[2]) and extra > 0
+    eng.import_census(d6, i5, keys)
+    mid = eng.census()
+    moved1 = distributed.rebalance_engine_census(eng, packed=False)
+    after1 = eng.census()
+    out["oracle"] = (before, after0, mid, after1, moved0, moved1)
+    o.close()
+    # packed path: 8-word records, 900 on rank 0 / 100 on rank 1, then 50 / 2000
+    rng = np.random.default_rng(7 + rank)
+    pe = _PackedEngine(rng.integers(-2 ** 62, 2 ** 62, (900 if rank == 0 else 100, abi.CENSUS_REC_WORDS)))
+    p_before = pe.rec.copy()
+    pm0 = distributed.rebalance_engine_census(pe, packed=True)
+    p_after0 = pe.rec.copy()
+    pe.rec = rng.integers(-2 ** 62, 2 ** 62, (50 if rank == 0 else 2000, abi.CENSUS_REC_WORDS))
+    p_mid = pe.rec.copy()
+    pm1 = distributed.rebalance_engine_census(pe, packed=True)
+    out["packed"] = (p_before, p_after0, p_mid, pe.rec.copy(), pm0, pm1)
+    q.put((rank, out))
+    distributed.barrier()
+    dist.destroy_process_group()
+
+
+def _records(cens):
+    d6, i5, keys = cens
+    return sorted((int(k), tuple(d), tuple(i)) for d, i, k in zip(d6, i5, keys))
+
+
+def test_rebalance_engine_census_both_directions_gloo():
+    """rebalance_engine_census on 2 gloo ranks: a census skewed to rank 0 is
+    levelled (0 -> 1), then one skewed to rank 1 (1 -> 0), through both
+    paths -- export/import (oracle census records) and the packed-record
+    path of the nccl backend (census_pack / truncate / append, here on host
+    tensors).  Every record arrives whole, exactly once, and the counts end
+    level; the rank that keeps records keeps its first ones in order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engine_rebalance_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    # export / import
+    b = {r: res[r]["oracle"] for r in (0, 1)}
+    assert all(b[r][4] and b[r][5] for r in (0, 1))          # both calls moved records
+    assert len(b[1][0][2]) == 0 < len(b[0][0][2])            # first skew: all on rank 0
+    assert len(b[1][2][2]) > len(b[0][2][2])                 # second skew: rank 1 heavier
+    for phase_in, phase_out in ((0, 1), (2, 3)):
+        assert _records(tuple(np.concatenate([b[r][phase_in][i] for r in (0, 1)]) for i in range(3))) == \
+            _records(tuple(np.concatenate([b[r][phase_out][i] for r in (0, 1)]) for i in range(3)))
+        n0, n1 = len(b[0][phase_out][2]), len(b[1][phase_out][2])
+        assert abs(n0 - n1) <= 1
+    # packed records
+    p = {r: res[r]["packed"] for r in (0, 1)}
+    assert all(p[r][4] and p[r][5] for r in (0, 1))
+    for phase_in, phase_out, keeper in ((0, 1, 1), (2, 3, 0)):
+        before = np.concatenate([p[0][phase_in], p[1][phase_in]])
+        after = np.concatenate([p[0][phase_out], p[1][phase_out]])
+        assert sorted(map(tuple, before)) == sorted(map(tuple, after))
+        assert len(p[0][phase_out]) == len(p[1][phase_out]) == len(before) // 2
+        # the deficit rank keeps its own records first, the surplus rank its head
+        np.testing.assert_array_equal(p[keeper][phase_out][:len(p[keeper][phase_in])], p[keeper][phase_in])
+        donor = 1 - keeper
+        np.testing.assert_array_equal(p[donor][phase_out], p[donor][phase_in][:len(p[donor][phase_out])])

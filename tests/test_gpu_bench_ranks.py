@@ -27,8 +27,12 @@ def _last_json(out: str) -> dict:
     return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
 
 
-def test_two_ranks_on_one_gpu_match_one_rank():
-    common = ["--workload", "c3", "--spinup", "1", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+@pytest.mark.parametrize("workload,spinup", [("c3", 1), ("c4", 2)])
+def test_two_ranks_on_one_gpu_match_one_rank(workload, spinup):
+    """c4 is the N > 1 default shape: the 32x32 C2 medium, FP off, the
+    in-place chunked census (bench.py INPLACE) carried through spin-up steps."""
+    common = ["--workload", workload, "--spinup", str(spinup), "--steps", "2", "--warmup", "1",
+              "--no-cpu-baseline"]
     one = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--sources", "8000000"] + common,
                          capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert one.returncode == 0, one.stderr[-2000:]
@@ -42,3 +46,7 @@ def test_two_ranks_on_one_gpu_match_one_rank():
     a, b = _last_json(one.stdout), _last_json(two.stdout)
     assert b["n_gpus"] == 2 and a["n_gpus"] == 1
     assert b["config"]["packet_steps_timed"] == a["config"]["packet_steps_timed"] > 0
+    if workload == "c4":
+        assert a["config"]["census"]["layout"].startswith("chunked")
+        assert b["config"]["census"]["layout"].startswith("chunked")
+        assert a["config"]["census"]["records_after_spinup"] > 0
