@@ -206,6 +206,68 @@ def cpu_baseline(eng, run, target_s: float = 12.0) -> dict:
                           cpu_steps, wall))}
 
 
+def fp_offclamp(device: int, cpu: bool) -> dict:
+    """One FP update off the temperature clamp, outside the timed steps (C3's
+    zones all sit on the reference's 1000 keV clamp, so the coupled step's FP
+    is the cheap case).  The workload of tools/fp_bench.py --vary: the
+    reference's fp_pick FP inputs tiled over 30x9 with n_e and tea varied per
+    zone, so no two zones share a temperature-search chain (2 391 implicit
+    sub-steps per zone).  On fresh contexts, i.e. with an empty gamma_bar
+    memo: the fast mode's first update (zones in index order), a second with
+    the memo emptied again (zones in the measured, costliest-first order) and
+    a third with the memo warm; the exact mode's first update.  cpu: the C
+    oracle's FP_calc on 8 zones of the same tile, one process each (the
+    bench's cpu_baseline leg)."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    import fp_bench
+    from compton2d_amd import abi
+    from compton2d_amd.engine import Engine
+    c, g, tile = fp_bench.tiled_case(30, 9, "fp_pick", vary=True)
+    g.device = device
+    out = {"workload": "tools/fp_bench.py --nz 30 --nr 9 --vary: the reference's fp_pick FP inputs "
+                       "(tests/golden/fp_pick.npz) tiled over 30x9, n_e and tea varied per zone",
+           "zones": 30 * 9, "timed_in_value": False}
+    call = (tile["ncycle"], tile["time"], tile["dt"], tile, tile)
+    for mode in ("fast", "exact"):
+        eng = Engine(g)
+        try:
+            eng.fp_set_config(c.constants())
+            eng.fp_set_mode(abi.FP_FAST if mode == "fast" else abi.FP_EXACT)
+            r = eng.fp_step(*call)
+            leg = {"ms_cold_index_order": eng.last_fp_ms(),
+                   "implicit_substeps": float(np.sum(r["zone_diag"][..., 5])),
+                   "Te_new_range": [float(r["Te_new"].min()), float(r["Te_new"].max())]}
+            if mode == "fast":
+                os.environ["C2D_FPF_MEMO_RESET"] = "1"
+                try:
+                    eng.fp_step(*call)
+                    leg["ms_cold_measured_order"] = eng.last_fp_ms()
+                finally:
+                    del os.environ["C2D_FPF_MEMO_RESET"]
+                eng.fp_step(*call)
+                leg["ms_warm"] = eng.last_fp_ms()
+                leg["kernel"] = "c2d_fp_fast_kernel<256> (C2D_FP_FAST; stated tolerance)"
+            else:
+                leg["kernel"] = "c2d_fp_kernel (C2D_FP_EXACT; bit for bit)"
+            out[mode] = leg
+        finally:
+            eng.close()
+    if cpu:
+        import multiprocessing as mp
+        cores = min(8, cpu_share()[0])
+        jobs = [(30, 9, (i, i + 1), "fp_pick", True) for i in range(cores)]
+        t0 = time.perf_counter()
+        with mp.get_context("spawn").Pool(cores) as pool:
+            res = pool.map(fp_bench._cpu_zone, jobs)
+        wall = time.perf_counter() - t0
+        per_zone = float(np.mean([x[0] for x in res]))
+        out["cpu_baseline"] = {"s_per_zone": per_zone, "zones_per_s_per_core": 1.0 / per_zone,
+                               "cores": cores, "kind": "port",
+                               "sample": "FP_calc of zones (0, 0..%d) of the tile, one process each "
+                                         "(C oracle, det math), pool wall %.1f s" % (cores - 1, wall)}
+    return out
+
+
 def load_pmc(workload_key: str):
     """Per-packet-step counters of the generation-0 transport launch and the
     FP kernel's issue figures, from the committed rocprofv3 PMC summary
@@ -407,6 +469,8 @@ def main():
     ap.add_argument("--host-tables", action="store_true",
                     help="c3: move tables/electrons through host arrays every step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fp-offclamp", action="store_true",
+                    help="c3: skip the untimed off-clamp FP update (kernels.fp_offclamp)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -609,6 +673,8 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline and wk == "c3":
         out["cpu_baseline"] = cpu_baseline(eng, run, args.cpu_seconds)
+    if world == 1 and wk == "c3" and not args.no_fp_offclamp:
+        kernels["fp_offclamp"] = fp_offclamp(local, cpu=not args.no_cpu_baseline)
     print(json.dumps(out))
     eng.close()
 

@@ -56,7 +56,7 @@ for r in "$@"; do
       run 300 smoke python -c "import __graft_entry__ as g; g.smoke()"; tail -2 "$O/smoke.out" ;;
     bench)
       run 600 bench python bench.py; line "$O/bench.out" ;;
-    c3)      run 500 c3 python bench.py --steps $STEPS --warmup $WARMUP --no-cpu-baseline; line "$O/c3.out" ;;
+    c3)      run 500 c3 python bench.py --steps $STEPS --warmup $WARMUP --no-cpu-baseline --no-fp-offclamp; line "$O/c3.out" ;;
     c3chunk) run 500 c3chunk python bench.py --steps $STEPS --warmup $WARMUP --no-cpu-baseline --census-inplace 1
              line "$O/c3chunk.out" ;;
     c4)      run 600 c4 python bench.py --workload c4 --steps $STEPS --warmup $WARMUP --no-cpu-baseline; line "$O/c4.out" ;;
@@ -65,7 +65,7 @@ for r in "$@"; do
       for t in $(echo "${r#ab:}" | tr ',' ' '); do
         lib=""; [ "$t" = base ] || lib=$PWD/compton2d_amd/sweep/$t/libcompton2d.so
         C2D_LIBRARY=$lib run 400 "ab_$t" python bench.py --spinup "${SPINUP:-0}" --steps "${STEPS}" \
-            --warmup "${WARMUP}" --no-cpu-baseline
+            --warmup "${WARMUP}" --no-cpu-baseline --no-fp-offclamp
         line "$O/ab_$t.out"
       done ;;
     profile)
