@@ -51,6 +51,10 @@ struct SpecDev {             /* file_sp table (imcsurf2d_para.f:544-685) */
  * with the same c2d_acos / c2d_cos (c2d_census_export / _import), so the
  * records it sees are the ones the fast kernel wrote before this encoding. */
 #define C2D_CENS_ESW (1u << 24)
+/* a volume source of this step written in census format by the source
+ * kernel (KParams.vol_cens_base): its dcen is c dt U, U the first draw of
+ * its own stream (vol_source, imcvol2d_para.f:206), not the census's c dt */
+#define C2D_CENS_VOL (1u << 25)
 /* Double-buffered census: a wave's unused tail of its last append chunk is
  * marked dead (bins = C2D_CENS_DEAD) and closed by the host's compaction
  * (capi.cpp census_compact). */
@@ -73,9 +77,23 @@ struct SpecDev {             /* file_sp table (imcsurf2d_para.f:544-685) */
 #define C2D_CCHUNK (1 << C2D_CCHUNK_LOG)
 #define C2D_CT_TRACK 16      /* census chunks a wave counts down at once (pow 2) */
 #define C2D_CT_STACK 8       /* freed chunks a wave holds for its next appends */
+/* A census record's jk word: kph | ie << 7 | jph << 16 | efl << 23 (jph, kph
+ * <= 99: 7 bits each; ie, efl <= 400: 9 bits each).  ie is the E_ph bin of
+ * xnu (the kappa_tot column, imctrk2d.f:382-384) and efl its E_field bin (the
+ * n_field row, imctrk2d.f:547-549): xnu does not change between a census
+ * write and the next step's read, so a census packet looks neither up
+ * again.  ie, efl = 0: not known (the reader looks them up). */
+__host__ __device__ __forceinline__ uint32_t c2d_cens_jk(int jph, int kph, int ie, int efl) {
+  return (uint32_t)kph | ((uint32_t)ie << 7) | ((uint32_t)jph << 16) | ((uint32_t)efl << 23);
+}
+__host__ __device__ __forceinline__ int c2d_cens_j(uint32_t jk) { return (int)((jk >> 16) & 0x7fu); }
+__host__ __device__ __forceinline__ int c2d_cens_k(uint32_t jk) { return (int)(jk & 0x7fu); }
+__host__ __device__ __forceinline__ int c2d_cens_ie(uint32_t jk) { return (int)((jk >> 7) & 0x1ffu); }
+__host__ __device__ __forceinline__ int c2d_cens_efl(uint32_t jk) { return (int)(jk >> 23); }
+
 struct CensusSoA {
   double* rpre; double* zpre; double* wmu; double* phi; double* ew; double* xnu;
-  uint32_t* jk;      /* jph << 16 | kph (1-based)                  */
+  uint32_t* jk;      /* c2d_cens_jk: jph, kph (1-based) + the E_ph / E_field bins */
   uint32_t* bins;    /* jgpsp | jgplc << 8 | jgpmu << 16 (| C2D_CENS_ESW) */
   uint64_t* key;
 };
@@ -236,6 +254,10 @@ struct KParams {
   int64_t cap_pk;
   /* this step's work */
   int64_t n_cens_items, n_vol_items, n_surf_items;
+  /* >= 0: the source kernel writes the volume sources in census format into
+   * cin at slots [vol_cens_base, + n_vol_items) and generation 0 takes them
+   * as census items (prefetched like them); -1: the packet store */
+  int64_t vol_cens_base;
   int64_t n_vol_global, n_surf_global;
   /* tallies */
   double* T;

@@ -107,6 +107,7 @@ struct DevCensus {
 }  // namespace
 
 struct c2d_ctx {
+  Geo geo_h;                  /* host copy of the grids (census import's bin lookups) */
   c2d_config cfg;
   int nz = 0, nr = 0, ncell = 0, nmu = 0, nslot = 0;
   std::string err;
@@ -171,6 +172,13 @@ struct c2d_ctx {
   double* ev = nullptr;
   int64_t n_ev = 0;
   int64_t ev_cnt[C2D_EV_SHARDS] = {};   /* events in each shard of the buffer (last step) */
+  /* the context's own escapes binned on a second stream (c2d_obs_accumulate
+   * with no events): it overlaps the next step's FP / tables / sources, and
+   * the next generation-0 launch, which rewrites the event buffer, waits
+   * for it (obs_settle reads its time when the host needs the result) */
+  hipStream_t obs_stream = nullptr;
+  hipEvent_t ev_obs_src = nullptr, ev_obs_a = nullptr, ev_obs_b = nullptr;
+  bool obs_inflight = false;
   int64_t ev_cap_sh = 0;                /* per-shard capacity                             */
   ScatRec *q2[2] = {nullptr, nullptr}, *q3[2] = {nullptr, nullptr};
   DevPk pk;
@@ -316,6 +324,10 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
 
   HIPCHK(c, hipSetDevice(cfg->device));
   HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(c, hipStreamCreateWithFlags(&c->obs_stream, hipStreamNonBlocking));
+  HIPCHK(c, hipEventCreateWithFlags(&c->ev_obs_src, hipEventDisableTiming));
+  HIPCHK(c, hipEventCreate(&c->ev_obs_a));
+  HIPCHK(c, hipEventCreate(&c->ev_obs_b));
   HIPCHK(c, hipEventCreate(&c->ev_g0a));
   HIPCHK(c, hipEventCreate(&c->ev_g0b));
   HIPCHK(c, hipEventCreate(&c->ev_g0t));
@@ -345,6 +357,7 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
   for (int n = 0; n < cfg->nmu; n++) g.mu[n + 1] = cfg->mu[n];
   HIPCHK(c, dalloc(&c->geo, 1));
   HIPCHK(c, hipMemcpy(c->geo, &g, sizeof g, hipMemcpyHostToDevice));
+  c->geo_h = g;
   HIPCHK(c, dalloc(&c->gnt, C2D_NUM_NT));
   HIPCHK(c, hipMemcpy(c->gnt, cfg->gnt, sizeof(double) * C2D_NUM_NT, hipMemcpyHostToDevice));
 
@@ -473,6 +486,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->obs_stream) (void)hipStreamSynchronize(c->obs_stream);   /* it reads the event buffer */
   if (c->mono_flag) (void)hipFree(c->mono_flag);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   void* ptrs[] = {c->geo, c->gnt, c->kappa_cur, c->kappa_prev, c->eps_tot, c->eps_th, c->f_nt,
@@ -507,6 +521,11 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
   if (c->ev_g0b) (void)hipEventDestroy(c->ev_g0b);
   if (c->ev_g0t) (void)hipEventDestroy(c->ev_g0t);
   if (c->ev_end) (void)hipEventDestroy(c->ev_end);
+  if (c->obs_stream) (void)hipStreamSynchronize(c->obs_stream);
+  if (c->ev_obs_src) (void)hipEventDestroy(c->ev_obs_src);
+  if (c->ev_obs_a) (void)hipEventDestroy(c->ev_obs_a);
+  if (c->ev_obs_b) (void)hipEventDestroy(c->ev_obs_b);
+  if (c->obs_stream) (void)hipStreamDestroy(c->obs_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1269,10 +1288,24 @@ static int run_step_body(c2d_ctx* c) {
   P.n_vol_items = share(c->n_vol_global);
   P.n_surf_items = share(c->n_surf_global);
   const int64_t n_src = P.n_vol_items + P.n_surf_items;
+  /* double-buffered census with room behind the previous census: the source
+   * kernel writes the volume sources there in census format, and generation
+   * 0 reads them as census items (the next-source prefetch covers them; no
+   * packet-store round trip).  C2D_VOL_CENSUS=0: the packet store. */
+  P.vol_cens_base = -1;
+  {
+    const char* e = getenv("C2D_VOL_CENSUS");
+    if (!c->chunked && !(e && e[0] == '0') && P.n_vol_items > 0 &&
+        c->n_census + P.n_vol_items <= c->cens_phys) {
+      P.vol_cens_base = c->n_census;
+      P.n_cens_items = c->n_census + P.n_vol_items;
+    }
+  }
+  const int64_t n_pk_src = n_src - (P.vol_cens_base >= 0 ? P.n_vol_items : 0);
   {
     /* packet store: all of this step's sources, and secondaries in chunks */
     const int64_t want = std::max<int64_t>(
-        n_src, std::min<int64_t>(int64_t(1) << 22,
+        n_pk_src, std::min<int64_t>(int64_t(1) << 22,
                                  std::max<int64_t>(65536, cfg.queue_capacity *
                                                               std::max(cfg.split2, cfg.split3))));
     if (c->pk.cap < want) {
@@ -1318,6 +1351,9 @@ static int run_step_body(c2d_ctx* c) {
   unsigned long long nq[CTL_CNT + C2D_CNT_PATHS_INT + 1 - CTL_N2];
   /* ---- generation 0: census + sampled sources ---- */
   {
+    /* the last step's events may still be binned on obs_stream: they are
+     * rewritten from here on (the tables, FP and budgets ran beside it) */
+    if (c->obs_inflight) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_obs_b, 0));
     HIPCHK(c, hipEventRecord(c->ev_g0a, c->stream));
     if (n_src > 0) {
       int rc = launch_src(c->dP, aux_grid(n_src, c->src_grid), c->stream);
@@ -1326,7 +1362,7 @@ static int run_step_body(c2d_ctx* c) {
     }
     GenArgs A = {};
     A.gen = 0;
-    A.n_items = P.n_cens_items + n_src;
+    A.n_items = P.n_cens_items + n_pk_src;
     A.q2_out = c->q2[1]; A.q3_out = c->q3[1];
     A.n2_out = c->ctl + CTL_N2; A.n3_out = c->ctl + CTL_N3;
     A.n_pk = c->ctl + CTL_NPK;
@@ -1624,8 +1660,8 @@ static int census_download(c2d_ctx* c, int64_t first, int64_t stride, int64_t m,
         i5[5 * o + 0] = (int32_t)(bins & 0xff);
         i5[5 * o + 1] = (int32_t)((bins >> 8) & 0xff);
         i5[5 * o + 2] = (int32_t)((bins >> 16) & 0xff);
-        i5[5 * o + 3] = (int32_t)(jk >> 16);
-        i5[5 * o + 4] = (int32_t)(jk & 0xffff);
+        i5[5 * o + 3] = (int32_t)c2d_cens_j(jk);
+        i5[5 * o + 4] = (int32_t)c2d_cens_k(jk);
       }
       if (keys) keys[o] = r[7];
     }
@@ -1685,7 +1721,12 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
       const double ph = d6[6 * i + 3];
       if (!(ph <= C2D_PI_REF && ph >= 1.0e-10)) bins[i] |= C2D_CENS_ESW;
     }
-    jk[i] = ((uint32_t)q[3] << 16) | (uint32_t)q[4];
+    /* the E_ph / E_field bins of xnu the record carries (c2d_cens_jk), with
+     * the kernels' semantics (grid_lookup = the bisection, build_lookup) */
+    const double xnu = d6[6 * i + 5];
+    const int ie = grid_bin_host(c->geo_h.E_ph, C2D_N_VOL, xnu);
+    const int efl = xnu > c->egg_min ? grid_bin_host(c->geo_h.E_field, C2D_NPHFIELD, xnu) : 0;
+    jk[i] = c2d_cens_jk(q[3], q[4], ie, efl);
   }
   if (n) {
     HIPCHK(c, hipMemcpy(d.jk, jk.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -2274,6 +2315,8 @@ extern "C" int c2d_last_vem_ms(c2d_ctx* c, double* ms) {
 /* ------------------------------------------------------------------ */
 /* observer-frame binning (postprocessing/pspt.c, plcm.c)               */
 /* ------------------------------------------------------------------ */
+static int obs_settle(c2d_ctx* c);
+
 extern "C" int c2d_obs_begin(c2d_ctx* c, const c2d_obs_bins* b) {
   if (!c || !b) return C2D_E_ARG;
   if ((b->mode != C2D_OBS_SED && b->mode != C2D_OBS_LC) || b->n_t < 1 || b->n_t > C2D_OBS_MAX_T ||
@@ -2286,6 +2329,7 @@ extern "C" int c2d_obs_begin(c2d_ctx* c, const c2d_obs_bins* b) {
   c->pspt_on = false;
   c->obs_ready = false;
   HIPCHK(c, hipSetDevice(c->cfg.device));
+  { const int rc = obs_settle(c); if (rc) return rc; }   /* the histogram is about to go */
   if (c->obs_edges) (void)hipFree(c->obs_edges);
   if (c->obs_hist) (void)hipFree(c->obs_hist);
   c->obs_edges = c->obs_hist = nullptr;
@@ -2334,6 +2378,18 @@ extern "C" int c2d_obs_begin(c2d_ctx* c, const c2d_obs_bins* b) {
   return C2D_OK;
 }
 
+/* Wait for an asynchronous binning of the context's own events (obs_stream)
+ * and add its kernel time. */
+static int obs_settle(c2d_ctx* c) {
+  if (!c->obs_inflight) return C2D_OK;
+  c->obs_inflight = false;
+  HIPCHK(c, hipEventSynchronize(c->ev_obs_b));
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, c->ev_obs_a, c->ev_obs_b);
+  c->obs_ms += ms;
+  return C2D_OK;
+}
+
 /* Bin `nseg` event segments (device pointer, count) back to back on the
  * context's stream; one event pair and one synchronisation around them all. */
 static int obs_launch_segments(c2d_ctx* c, const double* const* ev, const int64_t* m, int nseg) {
@@ -2365,14 +2421,33 @@ extern "C" int c2d_obs_accumulate(c2d_ctx* c, const double* events, int64_t n) {
   if (!c) return C2D_E_ARG;
   if (!c->obs_ready) return fail(c, C2D_E_STATE, "c2d_obs_begin must precede c2d_obs_accumulate");
   HIPCHK(c, hipSetDevice(c->cfg.device));
+  { const int rc = obs_settle(c); if (rc) return rc; }
   if (!events) {
     const double* seg[C2D_EV_SHARDS];
     int64_t cnt[C2D_EV_SHARDS];
+    int64_t tot = 0;
     for (int sh = 0; sh < C2D_EV_SHARDS; sh++) {
       seg[sh] = c->ev + (size_t)sh * c->ev_cap_sh * C2D_EVENT_WORDS;
       cnt[sh] = c->ev_cnt[sh];
+      tot += cnt[sh];
     }
-    return obs_launch_segments(c, seg, cnt, C2D_EV_SHARDS);
+    const char* e = getenv("C2D_OBS_ASYNC");
+    if ((e && e[0] == '0') || tot == 0) return obs_launch_segments(c, seg, cnt, C2D_EV_SHARDS);
+    /* on obs_stream, after the step that wrote the events; the next
+     * generation-0 launch waits for it (run_step_body) */
+    HIPCHK(c, hipEventRecord(c->ev_obs_src, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->obs_stream, c->ev_obs_src, 0));
+    const int64_t bs = c2d_obs_block();
+    HIPCHK(c, hipEventRecord(c->ev_obs_a, c->obs_stream));
+    for (int s = 0; s < C2D_EV_SHARDS; s++) {
+      if (cnt[s] == 0) continue;
+      const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * c->obs_wg_per_cu, (cnt[s] + bs - 1) / bs));
+      int rc = c2d_launch_obs(&c->obs, seg[s], cnt[s], grid, c->obs_stream);
+      if (rc) return fail(c, C2D_E_HIP, "obs launch: %s", hipGetErrorString((hipError_t)rc));
+    }
+    HIPCHK(c, hipEventRecord(c->ev_obs_b, c->obs_stream));
+    c->obs_inflight = true;
+    return C2D_OK;
   }
   if (n < 0) return C2D_E_ARG;
   if (n > c->obs_ev_cap) {
@@ -2390,6 +2465,7 @@ extern "C" int c2d_obs_accumulate_device(c2d_ctx* c, const double* d_events, int
   if (!c || !d_events || n < 0) return C2D_E_ARG;
   if (!c->obs_ready) return fail(c, C2D_E_STATE, "c2d_obs_begin must precede c2d_obs_accumulate_device");
   HIPCHK(c, hipSetDevice(c->cfg.device));
+  { const int rc = obs_settle(c); if (rc) return rc; }
   return obs_launch(c, d_events, n);
 }
 
@@ -2397,6 +2473,7 @@ extern "C" int c2d_obs_result(c2d_ctx* c, double* F, double* F2, double* count, 
   if (!c) return C2D_E_ARG;
   if (!c->obs_ready) return fail(c, C2D_E_STATE, "c2d_obs_begin must precede c2d_obs_result");
   HIPCHK(c, hipSetDevice(c->cfg.device));
+  { const int rc = obs_settle(c); if (rc) return rc; }
   const size_t nh = (size_t)c->obs.n_t * c->obs.n_mu * c->obs.n_e;
   if (F) HIPCHK(c, hipMemcpy(F, c->obs.F, nh * sizeof(double), hipMemcpyDeviceToHost));
   if (F2) HIPCHK(c, hipMemcpy(F2, c->obs.F2, nh * sizeof(double), hipMemcpyDeviceToHost));
@@ -2435,6 +2512,7 @@ extern "C" int c2d_obs_begin_pspt(c2d_ctx* c, const char* deck) {
 extern "C" int c2d_obs_write_pspt(c2d_ctx* c, const char* path, int32_t factor, int32_t world_sum) {
   if (!c) return C2D_E_ARG;
   if (!c->pspt_on || !c->obs_ready) return fail(c, C2D_E_STATE, "c2d_obs_write_pspt: c2d_obs_begin_pspt first");
+  { const int rc = obs_settle(c); if (rc) return rc; }
   if (c->obs.mode != C2D_OBS_SED || c->obs.n_mu != 1 || c->obs.n_t != c->pspt.n_t || c->obs.n_e != c->pspt.n_e ||
       !c->pspt_red)
     return fail(c, C2D_E_STATE, "c2d_obs_write_pspt: the binning is not the pspt deck's");

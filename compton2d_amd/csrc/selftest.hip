@@ -68,6 +68,74 @@ extern "C" int c2d_selftest_math(int device, int fn, const double* x_host, doubl
   return rc;
 }
 
+/* The r-boundary distance of a flight step (src/imctrk2d.f:251-277) with the
+ * fast build's reciprocal / square-root sequences after NR Newton steps --
+ * the same sequences as transport.hip rcp_pos / fsqrt_nn -- or (NR = 0) IEEE
+ * sqrt and division as the exact build. */
+namespace c2d {
+template <int NR>
+__device__ __forceinline__ double st_rcp(double b) {
+  double y = __builtin_amdgcn_rcp(b);
+#pragma unroll
+  for (int k = 0; k < NR; k++) y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+  return y;
+}
+template <int NR>
+__device__ __forceinline__ double st_sqrt(double x) {
+  x = fmax(x, 1.0e-300);
+  const double h = 0.5 * x;
+  double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+  for (int k = 0; k < NR; k++) y = y * __builtin_fma(-h, y * y, 1.5);
+  return x * y;
+}
+template <int NR>
+__global__ void c2d_selftest_geom_kernel(const double* in, double* out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  /* rbnd < 0: the inner boundary |rbnd| (inout = -1, imctrk2d.f:254-264) */
+  const double rpre = in[4 * i], Eta = in[4 * i + 1], wmu = in[4 * i + 2];
+  const double rbnd = fabs(in[4 * i + 3]);
+  const double inout = in[4 * i + 3] < 0.0 ? -1.0 : 1.0;
+  const double disp = Eta * rpre;
+  const double psq = rpre * rpre * (1.0 - Eta * Eta);
+  double dpbsq = rbnd * rbnd - psq;
+  if (dpbsq < 1.0e-6) dpbsq = 1.0e-6;
+  double disbr, trldb;
+  if (NR == 0) {
+    disbr = inout * __builtin_sqrt(dpbsq) - disp;
+    trldb = disbr / __builtin_sqrt(1.0 - wmu * wmu);
+  } else {
+    disbr = inout * st_sqrt<NR>(dpbsq) - disp;
+    trldb = disbr * st_rcp<NR>(st_sqrt<NR>(1.0 - wmu * wmu));
+  }
+  out[2 * i] = disbr;
+  out[2 * i + 1] = trldb;
+}
+}  // namespace c2d
+
+extern "C" int c2d_selftest_geom(int device, int nr, const double* in_host, double* out_host, int64_t n) {
+  if (n <= 0) return 0;
+  if (nr < 0 || nr > 2) return -1;
+  if (hipSetDevice(device) != hipSuccess) return -2;
+  double *in = nullptr, *out = nullptr;
+  if (hipMalloc((void**)&in, 4 * n * sizeof(double)) != hipSuccess) return -2;
+  if (hipMalloc((void**)&out, 2 * n * sizeof(double)) != hipSuccess) { (void)hipFree(in); return -2; }
+  int rc = 0;
+  if (hipMemcpy(in, in_host, 4 * n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) rc = -2;
+  if (!rc) {
+    const dim3 g((unsigned)((n + 255) / 256)), b(256);
+    if (nr == 0) hipLaunchKernelGGL(c2d::c2d_selftest_geom_kernel<0>, g, b, 0, 0, in, out, n);
+    else if (nr == 1) hipLaunchKernelGGL(c2d::c2d_selftest_geom_kernel<1>, g, b, 0, 0, in, out, n);
+    else hipLaunchKernelGGL(c2d::c2d_selftest_geom_kernel<2>, g, b, 0, 0, in, out, n);
+    if (hipDeviceSynchronize() != hipSuccess) rc = -2;
+  }
+  if (!rc && hipMemcpy(out_host, out, 2 * n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) rc = -2;
+  (void)hipFree(in);
+  (void)hipFree(out);
+  return rc;
+}
+
 /* McDonald K2, K3 at n arguments z (one wavefront each, c2d_wave.hpp's
  * mcdonald23_w) and the shader cycles each evaluation took: parity with the
  * oracle's sequential McDonald (src/volume2d.f:598-626) and a latency probe. */

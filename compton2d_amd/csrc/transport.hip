@@ -262,7 +262,8 @@ struct Pkt {
   int32_t jph, kph, mode;
   uint32_t bins;      /* jgpsp | jgplc << 8 | jgpmu << 16 | kap << 24 (PktSoA layout): the
                          spectral bins (imcleak2d.f) and the kappa phase (H3) in one register */
-  int32_t ie;         /* E_ph bin of xnu (imctrk2d.f:382-384), cached per xnu     */
+  int32_t ie;         /* E_ph bin of xnu (imctrk2d.f:382-384), cached per xnu, in the low
+                         16 bits; its E_field bin + 1 above them (0: not known yet) */
   uint64_t key;
   uint32_t sub;       /* lineage sub-stream: split1 copies of a source (c2d_rng.h) */
   uint32_t ctr;
@@ -922,9 +923,12 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
 #if defined(C2D_ABLATE_NFIELD) && C2D_ABLATE_NFIELD == 1   /* profiling ablations only */
   if (p.xnu < 0.0) {
 #else
+  int efl = 0;                          /* the record's E_field bin (c2d_cens_jk) */
   if (p.xnu > P.egg_min) {              /* Egg_min = E_field(1)^2/E_field(2), host-computed */
 #endif
-    const int i = grid_lookup(g->E_field, C2D_NPHFIELD, g->efl_start, g->efl_k0, p.xnu);
+    const int known = (p.ie >> 16) - 1;
+    const int i = known >= 0 ? known : grid_lookup(g->E_field, C2D_NPHFIELD, g->efl_start, g->efl_k0, p.xnu);
+    efl = i;
     const double v = FDIV_POS(6.25e8 * p.ew, p.xnu);
 #if defined(C2D_ABLATE_NFIELD) && C2D_ABLATE_NFIELD == 2   /* the lookup without the add */
     if (v == 1.25e300)
@@ -949,7 +953,7 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
 #endif
     gst(P.cout.ew + slot, p.ew);
     gst(P.cout.xnu + slot, p.xnu);
-    gst(P.cout.jk + slot, ((uint32_t)p.jph << 16) | (uint32_t)p.kph);
+    gst(P.cout.jk + slot, c2d_cens_jk(p.jph, p.kph, p.ie & 0xffff, efl));
     gst(P.cout.bins + slot, (p.bins & 0x00ffffffu)
 #if C2D_TABLE_COMTOT
                                 | (p.esw == -1 ? C2D_CENS_ESW : 0u)
@@ -997,8 +1001,8 @@ __device__ __forceinline__ void load_rec(Pkt& p, const ScatRec& r) {
 /* ------------------------------------------------------------------ */
 /* E_ph bin and comtot-table position depend on xnu only: computed when a
  * packet starts (source, probe restart, secondary) instead of every step. */
-__device__ __forceinline__ void cache_energy(const KParams& P, const Geo* g, Pkt& p) {
-  p.ie = grid_lookup(g->E_ph, C2D_N_VOL, g->eph_start, g->eph_k0, p.xnu);
+__device__ __forceinline__ void cache_energy(const KParams& P, const Geo* g, Pkt& p, bool have_ie = false) {
+  if (!have_ie) p.ie = grid_lookup(g->E_ph, C2D_N_VOL, g->eph_start, g->eph_k0, p.xnu);
 #if C2D_TABLE_COMTOT
   const double s = (FLOG(p.xnu) - C2D_COMTAB_U0) * P.comtab_du_inv;
   if (s >= 1.0 && s < (double)(C2D_COMTAB_N - 3)) {
@@ -1083,7 +1087,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   const double* tb_e = P.comtab + (int64_t)cell_e * C2D_COMTAB_N + (p.tg > 0 ? p.tg - 1 : 0);
   const double ey0 = gld(tb_e), ey1 = gld(tb_e + 1), ey2 = gld(tb_e + 2), ey3 = gld(tb_e + 3);
   const double ene = gld(P.n_e + cell_e);
-  const double ekap = gld((KAP(p) ? P.kappa_s : P.kappa_cv) + (int64_t)cell_e * C2D_N_VOL + (p.ie - 1));
+  const double ekap = gld((KAP(p) ? P.kappa_s : P.kappa_cv) + (int64_t)cell_e * C2D_N_VOL + ((p.ie & 0xffff) - 1));
 #endif
   /* mode 0 uses mb_ran = 1e-10 (imctrk2d.f:150) but never reads colmfp (dcol below) */
   double colmfp = 0.0;
@@ -1199,7 +1203,7 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
   double sigabs = 1.0e-40 + 1.0 * ekap;
 #else
   const double* kap = KAP(p) ? P.kappa_s : P.kappa_cv;
-  double sigabs = 1.0e-40 + 1.0 * gld(kap + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
+  double sigabs = 1.0e-40 + 1.0 * gld(kap + (int64_t)cell * C2D_N_VOL + ((p.ie & 0xffff) - 1));
 #endif
   if (sigabs < 1.0e-40) sigabs = 1.0e-40;
   const double xabs = sigabs * trld;
@@ -1596,7 +1600,34 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_source_kernel)(const KPara
       surf_source(P, g, p, side, s1, slot);
     }
     p.ctr = 0;   /* a source's own draws are done: its copies use sub-streams */
-    store_pk(P.pk, it, p);
+    if (P.vol_cens_base >= 0) {
+      if (it < P.n_vol_items) {
+        /* census format (pf_apply reads it back; C2D_CENS_VOL: dcen from the key) */
+        const int64_t s = P.vol_cens_base + it;
+        gst(P.cin.rpre + s, p.rpre);
+        gst(P.cin.zpre + s, p.zpre);
+        gst(P.cin.wmu + s, p.wmu);
+#if C2D_TABLE_COMTOT
+        const double eta = c2d_cos(p.phi);           /* set_phi's encoding (CensusSoA) */
+        const bool esw_neg = !(p.phi <= PI_REF && p.phi >= 1.0e-10);
+        gst(P.cin.phi + s, eta);
+#else
+        const bool esw_neg = false;
+        gst(P.cin.phi + s, p.phi);
+#endif
+        gst(P.cin.ew + s, p.ew);
+        gst(P.cin.xnu + s, p.xnu);
+        const int ie = grid_lookup(g->E_ph, C2D_N_VOL, g->eph_start, g->eph_k0, p.xnu);
+        const int efl = p.xnu > P.egg_min ? grid_lookup(g->E_field, C2D_NPHFIELD, g->efl_start, g->efl_k0, p.xnu) : 0;
+        gst(P.cin.jk + s, c2d_cens_jk(p.jph, p.kph, ie, efl));
+        gst(P.cin.bins + s, (p.bins & 0x00ffffffu) | C2D_CENS_VOL | (esw_neg ? C2D_CENS_ESW : 0u));
+        gst(P.cin.key + s, p.key);
+      } else {
+        store_pk(P.pk, it - P.n_vol_items, p);
+      }
+    } else {
+      store_pk(P.pk, it, p);
+    }
   }
 }
 
@@ -1714,11 +1745,13 @@ __device__ __forceinline__ void pf_apply(const KParams& P0, Pkt& p, const CensRe
 #else
   p.phi = r.cphi;
 #endif
-  p.jph = (int32_t)(r.jk >> 16); p.kph = (int32_t)(r.jk & 0xffffu);
+  p.jph = c2d_cens_j(r.jk); p.kph = c2d_cens_k(r.jk);
+  p.ie = c2d_cens_ie(r.jk) | ((c2d_cens_efl(r.jk) + 1) << 16);   /* the bins the record carries */
   p.bins = r.bn & 0x00ffffffu;                       /* kap = 0 (census phase, H3) */
   p.key = r.key;
   p.sub = 0;
   p.dcen = P.cdt;                                    /* imcfield2d.f:117 */
+  if (r.bn & C2D_CENS_VOL) p.dcen = P.cdt * c2d_draw_s(r.key, 0u, 0u);   /* vol_source's first draw */
 }
 
 /* C2D_PF_LDS: the prefetched record goes straight to LDS (gfx950 global ->
@@ -2012,7 +2045,7 @@ __device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bun
     p.ctr = 0;
     b.flags = BF_TRACK | (G > 0 ? BF_SPEC : 0);
   }
-  cache_energy(P, T.g, p);          /* azimuth: set by load_source */
+  cache_energy(P, T.g, p, b.src >= 0);   /* census records carry ie; azimuth: set by load_source */
 }
 
 /* probe g0 + i collides at dcol inside the shared step: its own partial
@@ -2098,7 +2131,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
   const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
   /* the step's absorption coefficient: issued before the comtot lookup and
    * the geometry, used after them */
-  const double kap_cell = gld((KAP(p) ? P.kappa_s : P.kappa_cv) + (int64_t)cell * C2D_N_VOL + (p.ie - 1));
+  const double kap_cell = gld((KAP(p) ? P.kappa_s : P.kappa_cv) + (int64_t)cell * C2D_N_VOL + ((p.ie & 0xffff) - 1));
   double sigsc = 1.0;
   if (b.alive) {
 #if C2D_TABLE_COMTOT

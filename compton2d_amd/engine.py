@@ -95,6 +95,9 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_selftest_math.restype = C.c_int
     lib.c2d_selftest_math.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double), C.c_int64]
+    lib.c2d_selftest_geom.restype = C.c_int
+    lib.c2d_selftest_geom.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double),
+                                      C.POINTER(C.c_double), C.c_int64]
     lib.c2d_last_gen0_steps.restype = C.c_int
     lib.c2d_last_gen0_steps.argtypes = [vp, C.POINTER(C.c_int64)]
     lib.c2d_last_path_steps.restype = C.c_int
@@ -488,6 +491,20 @@ def device_mcdonald(z: np.ndarray, device: int = 0):
     if rc != 0:
         raise C2DError(rc, "c2d_selftest_mcdonald failed")
     return out[:, 0], out[:, 1], out[:, 2]
+
+
+def device_geom(nr: int, rays: np.ndarray, device: int = 0) -> np.ndarray:
+    """(disbr, trldb) of the flight step's r-boundary distance for rays
+    (rpre, Eta, wmu, rbnd) on the GPU, with the fast build's sqrt / reciprocal
+    after `nr` Newton steps, or IEEE (nr = 0) (c2d_selftest_geom)."""
+    lib = load_library()
+    rays = np.ascontiguousarray(rays, np.float64).reshape(-1, 4)
+    out = np.zeros((rays.shape[0], 2))
+    rc = lib.c2d_selftest_geom(device, nr, rays.ctypes.data_as(abi.PD), out.ctypes.data_as(abi.PD),
+                               rays.shape[0])
+    if rc != 0:
+        raise C2DError(rc, "c2d_selftest_geom failed")
+    return out
 
 
 def device_math(fn: int, x: np.ndarray, device: int = 0) -> np.ndarray:

@@ -536,6 +536,14 @@ int  c2d_device_count(int32_t* n);
  * device (fn 0 log, 1 exp, 2 cos, 3 acos, 4 cbrt-by-pow, 5 sqrt, 6 x/3,
  * 7 Philox draw with key=x, counter=index) for bit-parity checks. */
 int  c2d_selftest_math(int device, int fn, const double* x, double* y, int64_t n);
+/* Diagnostics: the r-boundary distance of the flight step (src/imctrk2d.f:
+ * 251-277: psq, dpbsq, disbr = inout*sqrt(dpbsq) - Eta*rpre, trldb =
+ * disbr/sqrt(1 - wmu^2)) for n rays in[4n] = (rpre, Eta, wmu, rbnd; rbnd < 0:
+ * the inner boundary |rbnd|, inout = -1) with
+ * the fast build's square root / reciprocal sequences after `nr` Newton
+ * steps (nr 1: the fast build, 2: its former default) and with IEEE sqrt
+ * and division (nr 0: the exact build); out[2n] = (disbr, trldb). */
+int  c2d_selftest_geom(int device, int nr, const double* in, double* out, int64_t n);
 
 #ifdef __cplusplus
 }
