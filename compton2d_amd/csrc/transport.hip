@@ -115,6 +115,33 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 #ifndef C2D_PT_SERIES
 #define C2D_PT_SERIES 1
 #endif
+/* fast build: the survivors' absorption points in f32 (C2D_PT_F32=1; 0:
+ * f64).  They only weight prdep (delpr = deleabs * wmustar * c,
+ * imctrk2d.f:454-462: radiation pressure, read by no other part of the
+ * reference); f32 keeps wmustar to ~1e-7, far inside the fast build's 1e-3
+ * tally tolerance */
+#ifndef C2D_PT_F32
+#define C2D_PT_F32 1
+#endif
+/* fast build: the probe bundle's optical depth to its next collision,
+ * tau = -log(u)/n, with v_log_f32 (C2D_TAU_F32=1; 0: the f64 log).  tau only
+ * decides where the exponential collision process puts the next collision,
+ * so a ~1e-7 relative error leaves the process's statistics unchanged */
+#ifndef C2D_TAU_F32
+#define C2D_TAU_F32 1
+#endif
+/* fast build: the comtot table coordinate ln(xnu) of a source with
+ * v_log_f32 (C2D_LNX_F32=1).  An absolute error of ~1e-7 in ln(xnu) moves
+ * the cubic interpolation point by 4e-6 of a table step (ln 1e25 / 2047),
+ * ~1e-7 relative in comtot: the table's own interpolation error */
+#ifndef C2D_LNX_F32
+#define C2D_LNX_F32 0
+#endif
+#if C2D_TABLE_COMTOT && C2D_TAU_F32
+#define TAU_LOG(u) ((double)(0.69314718f * __builtin_amdgcn_logf((float)(u))))
+#else
+#define TAU_LOG(u) FLOG(u)
+#endif
 
 /* Fast build only (the exact build keeps the oracle's c2d_math and IEEE
  * division bit for bit):
@@ -1004,7 +1031,11 @@ __device__ __forceinline__ void load_rec(Pkt& p, const ScatRec& r) {
 __device__ __forceinline__ void cache_energy(const KParams& P, const Geo* g, Pkt& p, bool have_ie = false) {
   if (!have_ie) p.ie = grid_lookup(g->E_ph, C2D_N_VOL, g->eph_start, g->eph_k0, p.xnu);
 #if C2D_TABLE_COMTOT
+#if C2D_LNX_F32
+  const double s = ((double)(0.69314718f * __builtin_amdgcn_logf((float)p.xnu)) - C2D_COMTAB_U0) * P.comtab_du_inv;
+#else
   const double s = (FLOG(p.xnu) - C2D_COMTAB_U0) * P.comtab_du_inv;
+#endif
   if (s >= 1.0 && s < (double)(C2D_COMTAB_N - 3)) {
     p.tg = (int32_t)s;
     p.tt = s - (double)p.tg;
@@ -2034,7 +2065,7 @@ __device__ __forceinline__ void bundle_begin(const KParams& P, const Tal& T, Bun
   b.flags = 0;
   b.tsteps = 0;
   b.tau = 0.0;
-  if (G > 0) b.tau = FDIV_POS(-FLOG(UB(b)), (double)G);
+  if (G > 0) b.tau = FDIV_POS(-TAU_LOG(UB(b)), (double)G);
   p.nflight = 0;
   p.mode = 0;
   if (b.g0 + G == P.split1 && P.split1 - b.nscat > 0) {
@@ -2228,7 +2259,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
       probe_collide<V12>(P, T, A, b, i, dcol, sigabs, Eta, swmu, eta_switch, cell, lc);
       dpos = dcol;
       if (n == 0) break;
-      b.tau = FDIV_POS(-FLOG(UB(b)), (double)n);
+      b.tau = FDIV_POS(-TAU_LOG(UB(b)), (double)n);
     }
     if (n > 0) {
       b.tau = b.tau - sigsc * (trld - dpos);
@@ -2347,6 +2378,37 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
       /* two 32-bit uniforms per output of the bundle's point stream
        * (c2d_abspt), fresh outputs per shared step */
       const uint32_t sub = C2D_SUB_ABSPT | (uint32_t)b.g0;
+#if C2D_TABLE_COMTOT && C2D_PT_F32
+      /* wmustar = (wmu*rpre + s) / |r + s d| with |r + s d|^2 written as
+       * (s + wmu*rpre)^2 + rpre^2 (1 - wmu^2): a sum of non-negative terms,
+       * no cancellation near the axis in f32.  u: the top 24 bits of each
+       * 32-bit half of the point stream's output, (u + 1/2) 2^-24 in (0,1)
+       * exactly in f32; -log(1-x) by its series below 1e-2 (truncation
+       * < x^4/5), else by v_log_f32 */
+      {
+        const float isig = (float)FDIV_POS(1.0, sigabs);
+        const float Aw = (float)(wmu * rpre);
+        const float Cw = (float)(rpre * rpre * (1.0 - wmu * wmu));
+        const float qf = (float)qabs;
+        float wsum = 0.0f;
+        for (int t = 0; t < nabs; t += 2) {
+          const uint64_t wo = c2d_abspt(p.key, sub, b.actr++);
+#pragma unroll
+          for (int j = 0; j < 2; j++) {
+            if (t + j < nabs) {
+              const uint32_t u = j == 0 ? (uint32_t)(wo >> 32) : (uint32_t)wo;
+              const float x = ((float)(u >> 8) + 0.5f) * (5.9604644775390625e-8f * qf);
+              const float L = (x < 1.0e-2f)
+                  ? x * __builtin_fmaf(x, __builtin_fmaf(x, __builtin_fmaf(x, 0.25f, 0.33333334f), 0.5f), 1.0f)
+                  : -0.69314718f * __builtin_amdgcn_logf(1.0f - x);
+              const float tt = __builtin_fmaf(L, isig, Aw);          /* s + wmu*rpre */
+              wsum += tt * __builtin_amdgcn_rsqf(__builtin_fmaf(tt, tt, Cw));
+            }
+          }
+        }
+        sum_prdep = dabs * (double)wsum * C_LIGHT;
+      }
+#else
 #if C2D_TABLE_COMTOT
       const double isig = FDIV_POS(1.0, sigabs);
       const double Aw = wmu * rpre, Bw = rpre * rpre;
@@ -2398,6 +2460,7 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
         }
       }
 #endif
+#endif   /* C2D_PT_F32 */
     } else {
       sum_prdep = (double)nabs * (dabs * wmu * C_LIGHT);
     }
