@@ -620,7 +620,11 @@ def main():
             "fp": wk == "c3",
             "comtot": ("table (cubic in ln E, 2048 pts per cell, f64)" if mode == abi.COMTOT_TABLE
                        else "exact 199-term sum"),
-            "arithmetic": "f64 throughout (comtot table stored in f64)",
+            "arithmetic": ("f64 (positions, weights, tallies, comtot table stored in f64); the fast build "
+                           "samples the probes' absorption points, which weight only prdep, and draws the "
+                           "probe bundle's optical depth to its next collision, -log(u)/n, in f32 "
+                           "(transport.hip C2D_PT_F32, C2D_TAU_F32)" if mode == abi.COMTOT_TABLE
+                           else "f64 throughout (exact build, bit for bit with the oracle)"),
             "tables": ("device-resident (C2D_DEV_EMISSION | C2D_DEV_ELECTRONS)"
                        if wk == "c3" and not args.host_tables else "host arrays"),
             "parallelism": "lineage-sharded sources, %d rank(s), no data-path collective" % world,

@@ -135,7 +135,7 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
  * the cubic interpolation point by 4e-6 of a table step (ln 1e25 / 2047),
  * ~1e-7 relative in comtot: the table's own interpolation error */
 #ifndef C2D_LNX_F32
-#define C2D_LNX_F32 0
+#define C2D_LNX_F32 1
 #endif
 #if C2D_TABLE_COMTOT && C2D_TAU_F32
 #define TAU_LOG(u) ((double)(0.69314718f * __builtin_amdgcn_logf((float)(u))))

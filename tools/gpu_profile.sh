@@ -11,7 +11,7 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-B="$ROOT/bench.py --no-cpu-baseline $*"
+B="$ROOT/bench.py --no-cpu-baseline --no-fp-offclamp $*"
 # every pass runs the bench's own configuration (the driver's default K/W)
 K=${STEPS:-5}; W=${WARMUP:-2}
 echo "== kernel trace $(date +%T)"
