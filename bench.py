@@ -15,9 +15,12 @@ src/xec2d.f:67-87):
     c2d_fp_step         FP_calc for every zone, photon field read on the device
 
 with tables and electron spectra resident in HBM across steps and the census
-carried from step to step.  `--workload c2` is the 32x32 FP-off transport
-workload of round 1; `--workload c4` is C2's medium at C4's 1.25e8
-sources per GPU (1e9 per step on 8 GPUs).
+carried from step to step.  `--gpus N` runs the same per-GPU workload on every
+rank (weak scaling: 1e8 sources per GPU per step, lineage-sharded, one RCCL
+all-reduce of the tally buffer per step), so the per-N lines compare.
+`--workload c2` is the 32x32 FP-off transport workload of round 1;
+`--workload c4` is C2's medium at C4's 1.25e8 sources per GPU (1e9 per step
+on 8 GPUs, BASELINE configs[3]).
 
     python bench.py [--gpus N --steps K --warmup W] [--workload c3|c2|c4]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
@@ -455,7 +458,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=("c3", "c2", "c4", "c5"), default=None,
-                    help="default: c3 on one GPU, c4 (BASELINE configs[3]) on N > 1")
+                    help="default: c3 at every N (weak scaling: the same per-GPU workload, so the "
+                         "driver's per-N values compare); c4 = BASELINE configs[3]'s 1.25e8 per GPU "
+                         "on the 32x32 medium")
     ap.add_argument("--sources", type=int, default=None, help="volume packets/step/GPU (c5: nst/GPU)")
     ap.add_argument("--spinup", type=int, default=None,
                     help="untimed steps before the warm-up that bring the census to its steady "
@@ -485,7 +490,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    wk = args.workload or ("c3" if world == 1 else "c4")
+    wk = args.workload or "c3"
     args.workload = wk
     sources = args.sources or DEFAULT_SOURCES[wk]
     spinup = SPINUP.get(wk, 0) if args.spinup is None else args.spinup

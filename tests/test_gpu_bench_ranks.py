@@ -29,8 +29,9 @@ def _last_json(out: str) -> dict:
 
 @pytest.mark.parametrize("workload,spinup", [("c3", 1), ("c4", 2)])
 def test_two_ranks_on_one_gpu_match_one_rank(workload, spinup):
-    """c4 is the N > 1 default shape: the 32x32 C2 medium, FP off, the
-    in-place chunked census (bench.py INPLACE) carried through spin-up steps."""
+    """c3 is the default at every N; c4 (BASELINE configs[3]'s per-GPU
+    load) the 32x32 C2 medium, FP off, the in-place chunked census
+    (bench.py INPLACE) carried through spin-up steps."""
     common = ["--workload", workload, "--spinup", str(spinup), "--steps", "2", "--warmup", "1",
               "--no-cpu-baseline"]
     one = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--sources", "8000000"] + common,
