@@ -218,7 +218,9 @@ def fp_offclamp(device: int, cpu: bool) -> dict:
     sub-steps per zone).  On fresh contexts, i.e. with an empty gamma_bar
     memo: the fast mode's first update (zones in index order), a second with
     the memo emptied again (zones in the measured, costliest-first order) and
-    a third with the memo warm; the exact mode's first update.  cpu: the C
+    a third with the memo warm; the exact mode's first update.  The fast mode
+    takes McDonald pairs from its moment table (fp_fast.hip mcd_mtab, built in
+    c2d_fp_set_config: config_wall_ms), so a cold memo costs it little.  cpu: the C
     oracle's FP_calc on 8 zones of the same tile, one process each (the
     bench's cpu_baseline leg)."""
     sys.path.insert(0, str(ROOT / "tools"))
@@ -234,10 +236,13 @@ def fp_offclamp(device: int, cpu: bool) -> dict:
     for mode in ("fast", "exact"):
         eng = Engine(g)
         try:
+            t0 = time.perf_counter()
             eng.fp_set_config(c.constants())
+            setup_ms = 1e3 * (time.perf_counter() - t0)
             eng.fp_set_mode(abi.FP_FAST if mode == "fast" else abi.FP_EXACT)
             r = eng.fp_step(*call)
             leg = {"ms_cold_index_order": eng.last_fp_ms(),
+                   "config_wall_ms": setup_ms,
                    "implicit_substeps": float(np.sum(r["zone_diag"][..., 5])),
                    "Te_new_range": [float(r["Te_new"].min()), float(r["Te_new"].max())]}
             if mode == "fast":

@@ -318,6 +318,17 @@ enum : int32_t { FPERR_STEPS = 1, FPERR_GUARD = 2 };
 
 /* McDonald abscissa table: n < C2D_FP_MCD_N -> {t_n, ts_n, (ts_n^2-1)^1.5, (ts_n^2-1)^2.5} */
 #define C2D_FP_MCD_N 16384
+/* the fast kernel's McDonald moment table (fp_fast.hip, C2D_FPF_MTAB): z0 on
+ * a geometric grid of C2D_FPF_MT_Q points per octave from 2^C2D_FPF_MT_LO to
+ * 2^C2D_FPF_MT_HI; per entry C2D_FPF_MT_W doubles: z0, 1/z0, the two series'
+ * stopping indices f at z0, C2D_FPF_MT_K moments of each series, and each
+ * series' abscissa rows (t, ts, p) at n = f-1 .. f+2 */
+#define C2D_FPF_MT_Q 1024
+#define C2D_FPF_MT_LO (-17)
+#define C2D_FPF_MT_HI 3
+#define C2D_FPF_MT_N ((C2D_FPF_MT_HI - C2D_FPF_MT_LO) * C2D_FPF_MT_Q + 1)
+#define C2D_FPF_MT_K 7
+#define C2D_FPF_MT_W (4 + 2 * C2D_FPF_MT_K + 24)
 
 struct FpParams {
   int32_t nz, nr, pick_sw, inj_switch, inj_dis, g2var_switch, cf_sentinel, pair_sw;
@@ -347,6 +358,10 @@ struct FpParams {
   const int32_t* zorder;   /* [ncell] or null: q-th zone = q                  */
   int32_t* zq;             /* queue head, zeroed before the launch            */
   int32_t ncell;
+  /* fast kernel: the McDonald moment table (null: every pair by its series),
+   * and whether the shared gamma_bar memo is still consulted beside it */
+  const double* mom;       /* [C2D_FPF_MT_N][C2D_FPF_MT_W]                    */
+  int32_t mt_glob;
 };
 
 /* ---- observer-frame binning (observe.hip) ---- */

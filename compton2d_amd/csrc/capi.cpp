@@ -47,6 +47,7 @@ extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, con
 extern "C" int c2d_launch_fp(const FpParams* P, int ncell, int waves, hipStream_t s);
 extern "C" int c2d_launch_fp_fast(const FpParams* dP, int ncell, int block, int grid, hipStream_t s);
 extern "C" int c2d_fp_fast_block(int ncell, int n_simd);
+extern "C" int c2d_fp_mom_build(const double* mcd, double* mom, hipStream_t stream);
 extern "C" int c2d_fp_waves(int ncell, int n_simd);
 extern "C" int c2d_launch_vem(const VemParams* P, int ncell, hipStream_t s);
 extern "C" int c2d_launch_obs(const ObsDev* O, const double* ev, int64_t n, int grid,
@@ -220,6 +221,7 @@ struct c2d_ctx {
   double* fpf_gb_val = nullptr;
   FpParams* fp_dP = nullptr;                 /* FpParams in device memory (fast kernel) */
   int32_t* fpf_zq = nullptr;                 /* fast kernel: zone queue head + order [1 + ncell] */
+  double* fpf_mom = nullptr;                 /* fast kernel: McDonald moment table              */
   std::vector<int32_t> fpf_order;            /* zones by the last update's sub-steps, costliest first */
   bool fpf_ordered = false;                  /* fpf_order holds a measured order */
   float last_fp_ms = 0.f;
@@ -513,7 +515,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
     if (q) (void)hipFree(q);
   void* fptrs[] = {c->fp_FT, c->fp_mcd, c->fp_zin, c->fp_fin, c->fp_Pin, c->fp_nf, c->fp_fout, c->fp_Pout,
                    c->fp_zout, c->fp_err, c->fp_gb_key, c->fp_gb_val, c->fpf_gb_key, c->fpf_gb_val,
-                   c->fp_dP, c->fpf_zq};
+                   c->fp_dP, c->fpf_zq, c->fpf_mom};
   for (void* p : fptrs)
     if (p) (void)hipFree(p);
   c->pk.release();
@@ -1929,6 +1931,20 @@ static int ensure_mcd(c2d_ctx* c) {
   }
   if (!c->fp_dP) HIPCHK(c, dalloc(&c->fp_dP, 1));
   if (!c->fpf_zq) HIPCHK(c, dalloc(&c->fpf_zq, (size_t)c->ncell + 1));
+  /* the fast kernel's McDonald moment table (fp_fast.hip mcd_mtab): 6.9 MB,
+   * built on the device once (~1 ms); C2D_FPF_MTAB=0 leaves it out (A/B) */
+  const char* mt = getenv("C2D_FPF_MTAB");
+  if (!(mt && mt[0] == '0') && !c->fpf_mom) {
+    double* m = nullptr;
+    HIPCHK(c, dalloc(&m, (size_t)C2D_FPF_MT_N * C2D_FPF_MT_W));
+    const int rb = c2d_fp_mom_build(c->fp_mcd, m, c->stream);
+    const hipError_t e = rb ? (hipError_t)rb : hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+      (void)hipFree(m);
+      HIPCHK(c, e);
+    }
+    c->fpf_mom = m;
+  }
   if ((int)c->fpf_order.size() != c->ncell) {
     c->fpf_order.resize(c->ncell);
     for (int q = 0; q < c->ncell; q++) c->fpf_order[q] = q;
@@ -2074,6 +2090,11 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
      * 0 = one workgroup per zone) */
     P.zq = c->fpf_zq;
     P.zorder = c->fpf_zq + 1;
+    /* McDonald pairs from the moment table; C2D_FPF_MTAB=2 keeps consulting
+     * the shared gamma_bar memo as well */
+    const char* mt = getenv("C2D_FPF_MTAB");
+    P.mom = (mt && mt[0] == '0') ? nullptr : c->fpf_mom;
+    P.mt_glob = (mt && mt[0] == '2') ? 1 : 0;
     P.ncell = (int32_t)nc;
     HIPCHK(c, hipMemcpyAsync(c->fpf_zq + 1, c->fpf_order.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, st));
     HIPCHK(c, hipMemsetAsync(c->fpf_zq, 0, sizeof(int32_t), st));

@@ -58,7 +58,7 @@ __shared__ double f_bigW[NT + 2], f_bigC[NT + 2], f_em[NT + 2], f_Pnt[NT + 2], f
 __shared__ double f_pcr[2][4][256];          /* PCR rows a, b, c, d (double-buffered) */
 __shared__ double f_red[2][2][WMAXF];        /* block reductions: [slot][value][wave] */
 __shared__ int f_ired[2][2][WMAXF];          /* block integer min/max                 */
-__shared__ double f_eg[2];                   /* exp(gammln(2.5)), exp(gammln(3.5))    */
+__shared__ double f_eg[3];                   /* exp(gammln(2.5)), exp(gammln(3.5)), their ratio */
 constexpr int ZMEMO = 64;                    /* the zone's gamma_bar memo (direct-mapped) */
 __shared__ double f_mth[ZMEMO], f_mgv[ZMEMO];
 
@@ -492,17 +492,224 @@ __device__ void mcdonald23_fast(Blk<BS>& B, double z, const double* __restrict__
 #endif
 }
 
+/* 1/x: v_rcp_f64 and two Newton steps (fast mode: < 1 ulp) */
+__device__ __forceinline__ double rcp_nr(double x) {
+  double q = __builtin_amdgcn_rcp(x);
+  q = __builtin_fma(__builtin_fma(-x, q, 1.0), q, q);
+  return __builtin_fma(__builtin_fma(-x, q, 1.0), q, q);
+}
+
+/* McDonald moment table (C2D_FPF_MTAB).  Both series are sums over one fixed
+ * abscissa lattice, S(z) = sum_{n <= f(z)} w_n exp(-z ts_n), so around a grid
+ * point z0 (y_n = z0 ts_n, eta = z/z0 - 1)
+ *   S(z) = sum_k (-eta)^k N_k(z0),   N_k = sum_{n <= f(z0)} w_n e^{-y_n} y_n^k / k!
+ * as long as the stopping index is the same; the terms between f(z0) and
+ * f(z) (f moves by ~0.5 term per grid step) are added or removed one by one,
+ * each found by the reference's own stopping test at z.  With 1024 points per
+ * octave |eta| <= 3.4e-4, and the terms that carry the sums have y < ~30: 7
+ * moments leave (eta y)^7/7! < 1e-17 of a term.  The abscissa rows around
+ * f(z0) ride in the entry, so a pair is one load of an entry (336 B), two
+ * Horner chains and four exps per series, instead of ~8000 terms; the sum
+ * differs from the term-by-term one by rounding (the moments are compensated
+ * sums in n order; 1.1e-15, tests/test_gpu_fp.py).  Entries whose series
+ * would run past the abscissa table are marked f = -1: the series instead. */
+constexpr int MT_K = C2D_FPF_MT_K, MT_W = C2D_FPF_MT_W, MT_N = C2D_FPF_MT_N;
+constexpr int MT_ROWS = 4 + 2 * MT_K;           /* the rows of series 2, then 3 */
+
+/* the reference's term of one series at z and its stopping test
+ * (volume2d.f:608-620), as mcd_pass computes them, for one abscissa row */
+__device__ __forceinline__ double mt_term(double z, double t, double ts, double p, bool& stop) {
+  const double y = z * ts;
+  double ny[1] = {-(y < 2.25e2 ? y : 2.25e2)}, em[1];
+  exp_nonpos_tab<1>(ny, em);
+  if (!(ny[0] > -2.25e2)) em[0] = 0.0;
+  const double v = p * em[0];
+  stop = !(t * 1.001 < 2.0 || v > 1.0e-8);
+  return (1.001 - 1.0) * t * v;
+}
+template <int SER>
+__device__ __forceinline__ double mt_term_tab(const double* __restrict__ tab, double z, int n, bool& stop) {
+  const double4 x = gld4(tab + (size_t)n * 4);
+  return mt_term(z, x.x, x.y, SER == 2 ? x.z : x.w, stop);
+}
+
+/* s: the series at z from the moments at z0 (stopping index f0); tm[], st[]:
+ * the terms and stopping tests at z of the rows f0-1 .. f0+2.  Moves the
+ * stopping index to z's.  False: more than 4 terms apart, or past the table */
+template <int SER>
+__device__ __forceinline__ bool mt_fix(const double* __restrict__ tab, double z, int f0, const double (&tm)[4],
+                                       const bool (&st)[4], double& s) {
+  if (st[1]) {                                /* f(z) <= f0 */
+    if (!st[0]) return true;                  /* f(z) = f0 */
+    double sub = tm[1], t1 = tm[0];           /* drop f0; f0-1 stops too: look further down */
+    int f = f0 - 1;
+    for (int it = 0;; it++) {
+      if (f == 0) break;
+      bool sp;
+      const double tp = mt_term_tab<SER>(tab, z, f - 1, sp);
+      if (!sp) break;
+      if (it == 3) return false;
+      sub = sub + t1;
+      t1 = tp;
+      f--;
+    }
+    s = s - sub;
+    return true;
+  }
+  s = s + tm[2];                              /* f(z) > f0 */
+  if (st[2]) return true;
+  s = s + tm[3];
+  if (st[3]) return true;
+  for (int n = f0 + 3, it = 0;; n++, it++) {
+    if (n >= C2D_FP_MCD_N || it == 2) return false;
+    bool sn;
+    s = s + mt_term_tab<SER>(tab, z, n, sn);
+    if (sn) return true;
+  }
+}
+
+/* both sums at z from the table (every thread alike: same bits, uniform) */
+__device__ __forceinline__ bool mcd_mtab(const double* __restrict__ mom, const double* __restrict__ tab, double z,
+                                         double& S2, double& S3, long long* tmr = nullptr) {
+  if (!mom || !(z >= 0x1p-17 && z <= 0x1p3)) return false;
+  const float l2 = __builtin_amdgcn_logf((float)z);           /* log2 z, ~1e-7 */
+  int j = (int)__builtin_rintf((l2 - (float)C2D_FPF_MT_LO) * (float)C2D_FPF_MT_Q);
+  j = j < 0 ? 0 : (j > MT_N - 1 ? MT_N - 1 : j);
+  const double* e = mom + (size_t)j * MT_W;
+  /* the whole entry at once: every address is known before any value */
+  const C2D_GLOBAL double* eg = (const C2D_GLOBAL double*)e;
+  double w[MT_W];
+#pragma unroll
+  for (int q = 0; q < MT_W; q++) w[q] = eg[q];
+  const int f2 = (int)w[2], f3 = (int)w[3];
+  if (f2 < 1 || f3 < 1) return false;
+  /* the eight rows' terms at z (both series side by side: one exp chain of
+   * eight interleaved), and the two Horner chains beside them */
+  double ny[8], em[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const double y = z * w[MT_ROWS + 3 * q + 1];
+    ny[q] = -(y < 2.25e2 ? y : 2.25e2);
+  }
+  exp_nonpos_tab<8>(ny, em);
+  const double ne = -__builtin_fma(z, w[1], -1.0);            /* -eta */
+  double s2 = w[4 + MT_K - 1], s3 = w[4 + 2 * MT_K - 1];
+#pragma unroll
+  for (int k = MT_K - 2; k >= 0; k--) {
+    s2 = __builtin_fma(s2, ne, w[4 + k]);
+    s3 = __builtin_fma(s3, ne, w[4 + MT_K + k]);
+  }
+  double tm2[4], tm3[4];
+  bool st2[4], st3[4];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    if (!(ny[q] > -2.25e2)) em[q] = 0.0;
+    const double t = w[MT_ROWS + 3 * q], v = w[MT_ROWS + 3 * q + 2] * em[q];
+    const bool st = !(t * 1.001 < 2.0 || v > 1.0e-8);
+    const double tm = (1.001 - 1.0) * t * v;
+    if (q < 4) { tm2[q] = tm; st2[q] = st; } else { tm3[q - 4] = tm; st3[q - 4] = st; }
+  }
+  if (tmr) tmr[0] = clock64() + (long long)(s2 + s3 + tm2[0] + tm3[0] == 1.2345 ? 1 : 0);
+  if (!mt_fix<2>(tab, z, f2, tm2, st2, s2) || !mt_fix<3>(tab, z, f3, tm3, st3, s3)) return false;
+  if (tmr) tmr[1] = tmr[2] = clock64() + (long long)(s2 + s3 == 1.2345 ? 1 : 0);
+  S2 = s2;
+  S3 = s3;
+  return true;
+}
+
+/* Neumaier's compensated sum */
+__device__ __forceinline__ void nsum(double& s, double& c, double w) {
+  const double t = s + w;
+  c = c + ((fabs(s) >= fabs(w)) ? (s - t) + w : (w - t) + s);
+  s = t;
+}
+
+/* the table: one entry per thread, the series in n order at z0 */
+__global__ void __launch_bounds__(64) c2d_fp_mom_kernel(const double* __restrict__ tab, double* __restrict__ mom) {
+  f_e64[threadIdx.x] = c_exp2_64[threadIdx.x];
+  __syncthreads();
+  const int j = blockIdx.x * 64 + threadIdx.x;
+  if (j >= MT_N) return;
+  const double z0 = c2d_exp_bf(((double)j / C2D_FPF_MT_Q + C2D_FPF_MT_LO) * 6.93147180559945309417e-01);
+  double a2[MT_K], c2[MT_K], a3[MT_K], c3[MT_K];
+#pragma unroll
+  for (int k = 0; k < MT_K; k++) a2[k] = c2[k] = a3[k] = c3[k] = 0.0;
+  bool run2 = true, run3 = true;
+  int f2 = -1, f3 = -1;
+  for (int n = 0; n < C2D_FP_MCD_N && (run2 || run3); n++) {
+    const double4 x = gld4(tab + (size_t)n * 4);
+    const double y = z0 * x.y;
+    double ny[1] = {-(y < 2.25e2 ? y : 2.25e2)}, em[1];
+    exp_nonpos_tab<1>(ny, em);
+    if (!(ny[0] > -2.25e2)) em[0] = 0.0;
+    const double v2 = x.z * em[0], v3 = x.w * em[0];
+    const double tn = x.x * 1.001, dtt = (1.001 - 1.0) * x.x;
+    if (run2) {
+      double w = dtt * v2;
+#pragma unroll
+      for (int k = 0; k < MT_K; k++) {
+        nsum(a2[k], c2[k], w);
+        w = w * y / (double)(k + 1);
+      }
+      if (!(tn < 2.0 || v2 > 1.0e-8)) {
+        run2 = false;
+        f2 = n;
+      }
+    }
+    if (run3) {
+      double w = dtt * v3;
+#pragma unroll
+      for (int k = 0; k < MT_K; k++) {
+        nsum(a3[k], c3[k], w);
+        w = w * y / (double)(k + 1);
+      }
+      if (!(tn < 2.0 || v3 > 1.0e-8)) {
+        run3 = false;
+        f3 = n;
+      }
+    }
+  }
+  /* usable: stopped at least one row into the table and 3 rows before its end */
+  const bool ok2 = f2 >= 1 && f2 < C2D_FP_MCD_N - 3, ok3 = f3 >= 1 && f3 < C2D_FP_MCD_N - 3;
+  double* e = mom + (size_t)j * MT_W;
+  e[0] = z0;
+  e[1] = 1.0 / z0;
+  e[2] = ok2 ? (double)f2 : -1.0;
+  e[3] = ok3 ? (double)f3 : -1.0;
+#pragma unroll
+  for (int k = 0; k < MT_K; k++) {
+    e[4 + k] = a2[k] + c2[k];
+    e[4 + MT_K + k] = a3[k] + c3[k];
+  }
+  for (int q = 0; q < 4; q++) {
+    const int n2 = ok2 ? f2 - 1 + q : 0, n3 = ok3 ? f3 - 1 + q : 0;
+    e[MT_ROWS + 3 * q] = tab[(size_t)n2 * 4];
+    e[MT_ROWS + 3 * q + 1] = tab[(size_t)n2 * 4 + 1];
+    e[MT_ROWS + 3 * q + 2] = tab[(size_t)n2 * 4 + 2];
+    e[MT_ROWS + 12 + 3 * q] = tab[(size_t)n3 * 4];
+    e[MT_ROWS + 12 + 3 * q + 1] = tab[(size_t)n3 * 4 + 1];
+    e[MT_ROWS + 12 + 3 * q + 2] = tab[(size_t)n3 * 4 + 3];
+  }
+}
+
 template <int BS>
-__device__ double gamma_bar_fast(Blk<BS>& B, double Theta, const double* tab, long long& guard) {
+__device__ double gamma_bar_fast(Blk<BS>& B, double Theta, const double* tab, const double* mom, long long& guard) {
   double g;
   if (Theta < F32(0.2)) {
     g = (1. + F32(4.375) * Theta + F32(7.383) * (Theta * Theta) + F32(3.384) * (Theta * Theta * Theta)) /
             (1. + F32(1.875) * Theta + F32(.8203) * (Theta * Theta)) -
         Theta;
   } else {
-    double K2, K3;
-    mcdonald23_fast<BS>(B, 1.0 / Theta, tab, K2, K3, guard);
-    g = K3 / K2 - Theta;
+    double K2, K3, S2, S3;
+    const double z = rcp_nr(Theta);
+    if (mcd_mtab(mom, tab, z, S2, S3)) {
+      /* K3/K2 = (z/2) (S3/S2) exp(gammln(2.5))/exp(gammln(3.5)) (volume2d.f:623-624):
+       * the normalisations' powers of z/2 cancel but one */
+      g = (5.0e-1 * z) * (S3 * rcp_nr(S2)) * f_eg[2] - Theta;
+    } else {
+      mcdonald23_fast<BS>(B, z, tab, K2, K3, guard);
+      g = K3 / K2 - Theta;
+    }
   }
   if (g < 1.0) g = 1.0;
   return g;
@@ -549,13 +756,6 @@ __device__ double pcr_solve(Blk<BS>& B, double a, double b, double c, double dd)
     buf ^= 1;
   }
   return own ? dd / b : 0.0;
-}
-
-/* 1/x: v_rcp_f64 and two Newton steps (fast mode: < 1 ulp) */
-__device__ __forceinline__ double rcp_nr(double x) {
-  double q = __builtin_amdgcn_rcp(x);
-  q = __builtin_fma(__builtin_fma(-x, q, 1.0), q, q);
-  return __builtin_fma(__builtin_fma(-x, q, 1.0), q, q);
 }
 
 /* The same system, rows 1..NT (row i in thread i-1, rows past NT identity
@@ -767,6 +967,7 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
 #endif
     if (f_mth[slot] == th) return f_mgv[slot];
     double g = 0.0;
+    glob = glob && (!P.mom || P.mt_glob);
     if (glob) {
       /* read by thread 0 and broadcast, so every thread takes the same branch */
       if (tid == 0) {
@@ -781,7 +982,7 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
 #endif
     }
     if (g == 0.0) {
-      g = gamma_bar_fast<BS>(B, th, P.mcd, guard);
+      g = gamma_bar_fast<BS>(B, th, P.mcd, P.mom, guard);
 #ifdef C2D_FP_PROF
       if (th >= F32(0.2)) pf_mcd++;
 #endif
@@ -1125,6 +1326,7 @@ __global__ void __launch_bounds__(BS) c2d_fp_fast_kernel(const FpParams* __restr
     f_eg[0] = c2d_exp_bf(gammln(5.0e-1 + 2.0));
     for (int j = 0; j < 64; j++) f_e64[j] = c_exp2_64[j];
     f_eg[1] = c2d_exp_bf(gammln(5.0e-1 + 3.0));
+    f_eg[2] = f_eg[0] / f_eg[1];
   }
   /* one zone after another from the queue: a zone's time is its sub-step
    * count x one latency chain, and the costliest zones come first, each on a
@@ -1162,5 +1364,64 @@ extern "C" int c2d_launch_fp_fast(const c2d::FpParams* dP, int ncell, int block,
   if (block != C2D_FPF_BS || grid <= 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(c2d::c2d_fp_fast_kernel<C2D_FPF_BS>, dim3(grid < ncell ? grid : ncell), dim3(C2D_FPF_BS), 0,
                      stream, dP);
+  return (int)hipGetLastError();
+}
+
+/* the McDonald moment table for the fast kernel (C2D_FPF_MT_N x C2D_FPF_MT_W
+ * doubles at `mom`), from the abscissa table `mcd`; once per context */
+extern "C" int c2d_fp_mom_build(const double* mcd, double* mom, hipStream_t stream) {
+  hipLaunchKernelGGL(c2d::c2d_fp_mom_kernel, dim3((C2D_FPF_MT_N + 63) / 64), dim3(64), 0, stream, mcd, mom);
+  return (int)hipGetLastError();
+}
+
+namespace c2d {
+namespace {
+/* selftest: K2, K3 at z from the table and from the series (one block per z),
+ * with the shader cycles each took */
+__global__ void __launch_bounds__(256) c2d_fp_mtab_test_kernel(const double* __restrict__ tab,
+                                                               const double* __restrict__ mom,
+                                                               const double* __restrict__ zs, double* out) {
+  Blk<256> B;
+  B.tid = threadIdx.x;
+  B.lane = B.tid & (FPB - 1);
+  B.wave = B.tid / FPB;
+  if (B.tid < 64) f_e64[B.tid] = c_exp2_64[B.tid];
+  if (B.tid == 0) {
+    f_eg[0] = c2d_exp_bf(gammln(5.0e-1 + 2.0));
+    f_eg[1] = c2d_exp_bf(gammln(5.0e-1 + 3.0));
+    f_eg[2] = f_eg[0] / f_eg[1];
+  }
+  __syncthreads();
+  const double z = zs[blockIdx.x];
+  double S2 = 0.0, S3 = 0.0, K2t = 0.0, K3t = 0.0, K2s, K3s;
+  long long guard = 0;
+  /* timed: what gamma_bar_fast does with the table (from z) */
+  long long tmr[3] = {0, 0, 0};
+  const long long t0 = clock64();
+  const bool ok = mcd_mtab(mom, tab, z, S2, S3, tmr);
+  const double gq = ok ? (5.0e-1 * z) * (S3 * rcp_nr(S2)) * f_eg[2] - rcp_nr(z) : 0.0;
+  const long long t1 = clock64();
+  if (ok) mcdonald23_finish_c(z, S2, S3, f_eg[0], f_eg[1], K2t, K3t);
+  __syncthreads();
+  const long long t2 = clock64();
+  mcdonald23_fast<256>(B, z, tab, K2s, K3s, guard);
+  const long long t3 = clock64();
+  if (B.tid == 0) {
+    double* o = out + (size_t)blockIdx.x * 8;
+    o[0] = K2t; o[1] = K3t; o[2] = K2s; o[3] = K3s; o[4] = ok ? 1.0 : 0.0;
+    o[5] = (double)(t1 - t0); o[6] = (double)(t3 - t2); o[7] = gq;
+#ifdef C2D_MTAB_TIMERS
+    o[0] = (double)(tmr[0] - t0); o[1] = (double)(tmr[1] - tmr[0]); o[2] = (double)(tmr[2] - tmr[1]);
+    o[3] = (double)(t1 - tmr[2]);
+#endif
+  }
+}
+}  // namespace
+}  // namespace c2d
+
+extern "C" int c2d_fp_mtab_test(const double* mcd, const double* mom, const double* z, double* out, int n,
+                                hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(c2d::c2d_fp_mtab_test_kernel, dim3((unsigned)n), dim3(256), 0, stream, mcd, mom, z, out);
   return (int)hipGetLastError();
 }

@@ -160,9 +160,8 @@ __global__ void __launch_bounds__(64) c2d_selftest_mcd_kernel(const double* z, c
 }
 }  // namespace c2d
 
-extern "C" int c2d_selftest_mcdonald(int device, const double* z_host, int n, double* out_host) {
-  if (n <= 0) return 0;
-  if (hipSetDevice(device) != hipSuccess) return -2;
+/* the abscissa table as capi.cpp ensure_mcd builds it */
+static std::vector<double> mcd_abscissae() {
   std::vector<double> mt((size_t)C2D_FP_MCD_N * 4);
   const double dtm = 1.001, sm = 5.0e-1 * (1.0 + dtm);
   double t = 1.0;
@@ -174,6 +173,13 @@ extern "C" int c2d_selftest_mcdonald(int device, const double* z_host, int n, do
     mt[(size_t)k * 4 + 3] = c2d_pow(ts * ts - 1.0, 2.5);
     t = t * dtm;
   }
+  return mt;
+}
+
+extern "C" int c2d_selftest_mcdonald(int device, const double* z_host, int n, double* out_host) {
+  if (n <= 0) return 0;
+  if (hipSetDevice(device) != hipSuccess) return -2;
+  const std::vector<double> mt = mcd_abscissae();
   double *z = nullptr, *tab = nullptr, *out = nullptr;
   int rc = 0;
   if (hipMalloc((void**)&z, n * sizeof(double)) != hipSuccess ||
@@ -191,6 +197,38 @@ extern "C" int c2d_selftest_mcdonald(int device, const double* z_host, int n, do
     rc = -2;
   if (z) (void)hipFree(z);
   if (tab) (void)hipFree(tab);
+  if (out) (void)hipFree(out);
+  return rc;
+}
+
+/* The fast FP kernel's McDonald pair from its moment table against the same
+ * kernel's term-by-term series (fp_fast.hip mcd_mtab / mcdonald23_fast), per
+ * z: K2, K3 (table), K2, K3 (series), 1 if the table answered, and the
+ * shader cycles of each. */
+extern "C" int c2d_fp_mom_build(const double* mcd, double* mom, hipStream_t stream);
+extern "C" int c2d_fp_mtab_test(const double* mcd, const double* mom, const double* z, double* out, int n,
+                                hipStream_t stream);
+extern "C" int c2d_selftest_mcd_fast(int device, const double* z_host, int n, double* out_host) {
+  if (n <= 0) return 0;
+  if (hipSetDevice(device) != hipSuccess) return -2;
+  const std::vector<double> mt = mcd_abscissae();
+  double *z = nullptr, *tab = nullptr, *mom = nullptr, *out = nullptr;
+  int rc = 0;
+  if (hipMalloc((void**)&z, n * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&tab, mt.size() * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&mom, (size_t)C2D_FPF_MT_N * C2D_FPF_MT_W * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&out, 8 * (size_t)n * sizeof(double)) != hipSuccess)
+    rc = -2;
+  if (!rc && (hipMemcpy(z, z_host, n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemcpy(tab, mt.data(), mt.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess))
+    rc = -2;
+  if (!rc && (c2d_fp_mom_build(tab, mom, 0) != 0 || c2d_fp_mtab_test(tab, mom, z, out, n, 0) != 0)) rc = -2;
+  if (!rc && hipDeviceSynchronize() != hipSuccess) rc = -2;
+  if (!rc && hipMemcpy(out_host, out, 8 * (size_t)n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+    rc = -2;
+  if (z) (void)hipFree(z);
+  if (tab) (void)hipFree(tab);
+  if (mom) (void)hipFree(mom);
   if (out) (void)hipFree(out);
   return rc;
 }

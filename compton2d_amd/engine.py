@@ -493,6 +493,22 @@ def device_mcdonald(z: np.ndarray, device: int = 0):
     return out[:, 0], out[:, 1], out[:, 2]
 
 
+def device_mcd_fast(z: np.ndarray, device: int = 0) -> np.ndarray:
+    """The fast FP kernel's McDonald pair at z from its moment table and from
+    its term-by-term series (c2d_selftest_mcd_fast): rows (K2, K3 table, K2,
+    K3 series, table answered, cycles of the table's gamma_bar, cycles of the
+    series, gamma_bar from the table as the fast kernel forms it)."""
+    lib = load_library()
+    lib.c2d_selftest_mcd_fast.restype = C.c_int
+    lib.c2d_selftest_mcd_fast.argtypes = [C.c_int, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double)]
+    z = np.ascontiguousarray(z, np.float64)
+    out = np.zeros((len(z), 8))
+    rc = lib.c2d_selftest_mcd_fast(device, z.ctypes.data_as(abi.PD), len(z), out.ctypes.data_as(abi.PD))
+    if rc != 0:
+        raise C2DError(rc, "c2d_selftest_mcd_fast failed")
+    return out
+
+
 def device_geom(nr: int, rays: np.ndarray, device: int = 0) -> np.ndarray:
     """(disbr, trldb) of the flight step's r-boundary distance for rays
     (rpre, Eta, wmu, rbnd) on the GPU, with the fast build's sqrt / reciprocal

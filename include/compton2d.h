@@ -544,6 +544,12 @@ int  c2d_selftest_math(int device, int fn, const double* x, double* y, int64_t n
  * steps (nr 1: the fast build, 2: its former default) and with IEEE sqrt
  * and division (nr 0: the exact build); out[2n] = (disbr, trldb). */
 int  c2d_selftest_geom(int device, int nr, const double* in, double* out, int64_t n);
+/* Diagnostics: the fast FP kernel's McDonald pair (volume2d.f:598-626) at n
+ * arguments z from its moment table and from its term-by-term series;
+ * out[8n] = (K2, K3 from the table, K2, K3 from the series, 1 if the table
+ * answered, shader cycles of the table's gamma_bar and of the series,
+ * gamma_bar = K3/K2 - 1/z as the fast kernel forms it from the table). */
+int  c2d_selftest_mcd_fast(int device, const double* z, int n, double* out);
 
 #ifdef __cplusplus
 }

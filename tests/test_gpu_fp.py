@@ -129,3 +129,33 @@ def test_gpu_fp_fast_within_tolerance(name, capsys):
     with pytest.raises(Exception, match="C2D_E_ARG"):
         eng.fp_set_mode(7)
     eng.close()
+
+
+def test_gpu_fp_fast_mcdonald_moment_table(capsys):
+    """The fast kernel's McDonald pair from its moment table (fp_fast.hip
+    mcd_mtab: 7 moments per series at 1024 grid points per octave of z, the
+    stopping index moved to z's term by term) against the same kernel's
+    term-by-term series, at random z over the table's range and on and half-way
+    between its grid points: K2, K3 and gamma_bar = K3/K2 - 1/z (formed as the
+    kernel does, (z/2) (S3/S2) Gamma(2.5)/Gamma(3.5) - 1/z) within 1e-13
+    relative.  The table answers wherever the series stops inside the abscissa
+    table (z >= 2^-16 here; below, both take the series)."""
+    from compton2d_amd.engine import device_mcd_fast
+    rng = np.random.default_rng(5)
+    z = np.concatenate([2.0 ** rng.uniform(-17.0, np.log2(5.0), 3000),
+                        2.0 ** (np.arange(-17 * 1024, 3 * 1024 + 1, 37) / 1024.0),
+                        2.0 ** ((np.arange(-17 * 1024, 3 * 1024, 41) + 0.5) / 1024.0),
+                        [5.0, 0.2, 1.0, 2.0 ** -16]])
+    out = device_mcd_fast(z)
+    ok = out[:, 4] == 1.0
+    assert np.all(ok[z >= 2.0 ** -16]), z[(z >= 2.0 ** -16) & ~ok][:5]
+    d2 = np.abs(out[ok, 0] / out[ok, 2] - 1.0)
+    d3 = np.abs(out[ok, 1] / out[ok, 3] - 1.0)
+    gs = out[ok, 3] / out[ok, 2] - 1.0 / z[ok]
+    dg = np.abs(out[ok, 7] / gs - 1.0)
+    with capsys.disabled():
+        print("\nmoment table: %d of %d z answered; max rel dev K2 %.1e K3 %.1e gamma_bar %.1e; "
+              "shader cycles table %.0f (median) vs series %.0f"
+              % (ok.sum(), len(z), d2.max(), d3.max(), dg.max(), np.median(out[ok, 5]),
+                 np.median(out[ok, 6])))
+    assert d2.max() <= 1e-13 and d3.max() <= 1e-13 and dg.max() <= 1e-13

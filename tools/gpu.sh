@@ -15,6 +15,7 @@
 #   profile        rocprofv3 kernel trace + PMC passes of the C3 bench (tools/gpu_profile.sh)
 #   fp             tools/fp_bench.py off the clamp: 30x9, varied zones, memo on and off
 #   fpab:<t1>,..   the fp run for each build (as ab:)
+#   fpfast         the fast FP off the clamp, McDonald moment table on/off, memo warm/cold
 #   fppmc          rocprofv3 kernel trace + SQ counters of that FP run (memo on)
 #   fpprof         FP section timers off the clamp (sweep build "fpprof", tools/fp_prof.py)
 #   trprof[:t,..]  wave section timers of the C3 run (sweep builds, default "prof"; tools/tr_prof.py)
@@ -74,6 +75,14 @@ for r in "$@"; do
       for m in 1 0; do
         C2D_FP_MEMO=$m run 300 "fp_memo$m" python tools/fp_bench.py --nz 30 --nr 9 --vary --reps 3 --cpu-zones 8
         tail -1 "$O/fp_memo$m.out"
+      done ;;
+    fpfast)  # the fast FP off the clamp: McDonald moment table on / off / with the shared memo
+             # (C2D_FPF_MTAB 1 / 0 / 2), gamma_bar memo warm or emptied before every update
+      for v in 1:0 1:1 0:0 0:1 2:1; do
+        mt=${v%%:*}; rs=${v##*:}
+        C2D_FPF_MTAB=$mt C2D_FPF_MEMO_RESET=$rs run 300 "fpfast_mt${mt}_cold${rs}" \
+          python tools/fp_bench.py --nz 30 --nr 9 --vary --reps 3 --cpu-zones 8 --mode fast
+        echo "fpfast mtab=$mt cold=$rs: $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('%.2f ms (first call %.2f), f_nt dev %.1e, Te equal %s' % (d['kernel_ms'], d['kernel_ms_first_call'], d['f_nt_max_dev_vs_oracle_on_sample'], d['Te_new_equal_on_sample']))" "$O/fpfast_mt${mt}_cold${rs}.out")"
       done ;;
     fpab:*)  # tools/fp_bench.py off the clamp for each build (as ab:, memo on)
       for t in $(echo "${r#fpab:}" | tr ',' ' '); do
