@@ -267,7 +267,12 @@ struct KParams {
   int32_t* err;
   int32_t lds_cells;        /* 1: cell tallies privatised in LDS */
   unsigned long long* prof;  /* [C2D_TR_PROF_WORDS] section counters (-DC2D_TR_PROF builds) */
+  /* guide rows of the emission CDFs (eps_linear == 0): cdf_guide[(t * ncell + cell) *
+   * (C2D_CDF_GUIDE + 1) + q] = the smallest i in [1, 400] with cdf(i) >= q / C2D_CDF_GUIDE
+   * (400 if none), t 0: eps_tot, 1: eps_th; null: the full binary search */
+  const uint16_t* cdf_guide;
 };
+#define C2D_CDF_GUIDE 256
 
 /* Per-launch arguments (passed by value; KParams stays constant over a step). */
 struct GenArgs {

@@ -200,6 +200,8 @@ struct c2d_ctx {
   int comm_rank = 0, comm_world = 1;
   int64_t n_vol_global = 0, n_surf_global = 0;
   int eps_linear = 0;
+  uint16_t* cdf_guide = nullptr;   /* [2][ncell][C2D_CDF_GUIDE + 1] (c2d_cdf_guide) */
+  bool cdf_guide_on = false;
   std::vector<double> h_stage;
   double last_g0_ms = 0.0, last_all_ms = 0.0;
   float last_src_ms = 0.f;
@@ -507,7 +509,7 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
     if (c->cens[b].key) (void)hipFree(c->cens[b].key);
   }
   for (double* p : c->spec_bufs) (void)hipFree(p);
-  void* optrs[] = {c->obs_edges, c->obs_hist, c->obs_ev, c->pspt_red};
+  void* optrs[] = {c->obs_edges, c->obs_hist, c->obs_ev, c->pspt_red, c->cdf_guide};
   for (void* p : optrs)
     if (p) (void)hipFree(p);
   void* vptrs[] = {c->vem_zin, c->vem_fnt, c->vem_eph, c->vem_kap, c->vem_et, c->vem_eh, c->vem_zout};
@@ -571,6 +573,30 @@ __global__ void __launch_bounds__(256) c2d_check_monotone(const double* __restri
        t += (int64_t)gridDim.x * blockDim.x) {
     const int i = (int)(t % n);
     if (i > 0 && !(a[t] >= a[t - 1])) atomicOr(flag, 1);
+  }
+}
+
+/* guide rows of the emission CDFs (KParams.cdf_guide): row (t, cell), entry q
+ * = the smallest i in [1, n] with cdf(i) >= q / C2D_CDF_GUIDE, n if none --
+ * cdf_index's own predicate, so its search restricted to [guide[q],
+ * guide[q+1]] returns the same index as over [1, n] */
+__global__ void __launch_bounds__(256) c2d_cdf_guide(const double* __restrict__ eps_tot,
+                                                     const double* __restrict__ eps_th, int ncell, int n,
+                                                     uint16_t* __restrict__ guide) {
+  const int64_t rows = 2 * (int64_t)ncell, per = C2D_CDF_GUIDE + 1;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < rows * per;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = t / per;
+    const int q = (int)(t % per);
+    const double* cdf = (row < ncell ? eps_tot : eps_th) + (row % ncell) * (int64_t)n;
+    const double thr = (double)q * (1.0 / C2D_CDF_GUIDE);
+    int lo = 1, hi = n;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cdf[mid - 1] < thr) lo = mid + 1;
+      else hi = mid;
+    }
+    guide[t] = (uint16_t)lo;
   }
 }
 
@@ -734,6 +760,19 @@ extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
     HIPCHK(c, hipMemcpy(c->spectra, hs.data(), hs.size() * sizeof(SpecDev), hipMemcpyHostToDevice));
   }
 
+  /* the CDFs' guide rows (used while they are monotone; C2D_CDF_GUIDE_OFF=1: A/B) */
+  {
+    const char* go = getenv("C2D_CDF_GUIDE_OFF");
+    c->cdf_guide_on = !(go && go[0] == '1');
+    if (c->cdf_guide_on) {
+      if (!c->cdf_guide) HIPCHK(c, dalloc(&c->cdf_guide, (size_t)2 * nc * (C2D_CDF_GUIDE + 1)));
+      const int64_t nt = (int64_t)2 * nc * (C2D_CDF_GUIDE + 1);
+      const int grid = (int)std::min<int64_t>((nt + 255) / 256, (int64_t)c->n_cu * 4);
+      hipLaunchKernelGGL(c2d_cdf_guide, dim3(grid), dim3(256), 0, c->stream, c->eps_tot, c->eps_th, nc, C2D_N_VOL,
+                         c->cdf_guide);
+      HIPCHK(c, hipGetLastError());
+    }
+  }
   if (c->cfg.comtot_mode == C2D_COMTOT_TABLE) {
     int rc = c2d_launch_comtab_gemm(c->f_nt, c->gnt, c->comS, c->comtab, nc, c->stream);
     if (rc) return fail(c, C2D_E_HIP, "comtab_gemm launch: %d", rc);
@@ -1231,6 +1270,7 @@ static int run_step_body(c2d_ctx* c) {
   P.split1 = cfg.split1; P.split2 = cfg.split2; P.split3 = cfg.split3; P.spl3_trg = cfg.spl3_trg;
   P.spec_switch = cfg.spec_switch; P.rank = cfg.rank; P.world = cfg.world;
   P.eps_linear = c->eps_linear;
+  P.cdf_guide = (c->cdf_guide_on && !c->eps_linear) ? c->cdf_guide : nullptr;
   P.rmin = cfg.rmin; P.zmin = cfg.zmin;
   P.geo = c->geo; P.gnt = c->gnt;
   P.kappa_cv = cfg.kappa_lag ? c->kappa_prev : c->kappa_cur;

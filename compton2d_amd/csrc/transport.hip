@@ -587,13 +587,22 @@ __device__ __forceinline__ int grid_lookup(const double* E, int n, const int16_t
 }
 /* `i=0; do i=i+1 while (cdf(i) < rnum .and. i < n)` (imcvol2d_para.f:170-172) */
 __device__ __forceinline__ int cdf_index(const double* cdf /*0-based*/, int n, double rnum,
-                                         int linear) {
+                                         int linear, const uint16_t* guide = nullptr) {
   if (linear) {
     int i = 0;
     do { i = i + 1; } while (cdf[i - 1] < rnum && i < n);
     return i;
   }
   int lo = 1, hi = n;   /* smallest i with cdf(i) >= rnum, capped at n */
+  if (guide) {
+    /* the answer lies in [guide[q], guide[q+1]] for q = floor(rnum G)
+     * (rnum G is exact, G a power of two): the same index in ~2 probes
+     * instead of ~9 dependent loads */
+    int q = (int)(rnum * (double)C2D_CDF_GUIDE);
+    q = q < 0 ? 0 : (q > C2D_CDF_GUIDE - 1 ? C2D_CDF_GUIDE - 1 : q);
+    lo = guide[q];
+    hi = guide[q + 1];
+  }
   while (lo < hi) {
     int mid = (lo + hi) >> 1;
     if (cdf[mid - 1] < rnum) lo = mid + 1;
@@ -1380,7 +1389,8 @@ __device__ __forceinline__ void vol_source(const KParams& P, const Geo* g, Pkt& 
   double rnum = U(p), psi;
   if (rnum < f_thermal) {
     rnum = U(p);
-    int i = cdf_index(P.eps_th + (int64_t)cell * C2D_N_VOL, C2D_N_VOL, rnum, P.eps_linear);
+    int i = cdf_index(P.eps_th + (int64_t)cell * C2D_N_VOL, C2D_N_VOL, rnum, P.eps_linear,
+                      P.cdf_guide ? P.cdf_guide + (int64_t)(P.ncell + cell) * (C2D_CDF_GUIDE + 1) : nullptr);
     if (i < C2D_N_VOL) p.xnu = g->E_ph[i] + U(p) * (g->E_ph[i + 1] - g->E_ph[i]);
     else p.xnu = g->E_ph[i];
     double rnum0 = U(p);
@@ -1430,7 +1440,8 @@ __device__ __forceinline__ void vol_source(const KParams& P, const Geo* g, Pkt& 
     }
   } else {
     rnum = U(p);
-    int i = cdf_index(P.eps_tot + (int64_t)cell * C2D_N_VOL, C2D_N_VOL, rnum, P.eps_linear);
+    int i = cdf_index(P.eps_tot + (int64_t)cell * C2D_N_VOL, C2D_N_VOL, rnum, P.eps_linear,
+                      P.cdf_guide ? P.cdf_guide + (int64_t)cell * (C2D_CDF_GUIDE + 1) : nullptr);
     if (i < C2D_N_VOL) p.xnu = g->E_ph[i] + U(p) * (g->E_ph[i + 1] - g->E_ph[i]);
     else p.xnu = g->E_ph[i];
     p.wmu = 2.0 * U(p) - 1.0;
