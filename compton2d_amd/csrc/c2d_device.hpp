@@ -91,11 +91,18 @@ __host__ __device__ __forceinline__ int c2d_cens_k(uint32_t jk) { return (int)(j
 __host__ __device__ __forceinline__ int c2d_cens_ie(uint32_t jk) { return (int)((jk >> 7) & 0x1ffu); }
 __host__ __device__ __forceinline__ int c2d_cens_efl(uint32_t jk) { return (int)(jk >> 23); }
 
+/* The 64-B record as four 16-B columns, so a lane writes and reads a record
+ * with four dwordx4 accesses (a wave's access to one column is contiguous):
+ *   rz (rpre, zpre), wp (wmu, phi), ex (ew, xnu), tg (jk, bins, key low, key high)
+ * jk: c2d_cens_jk (jph, kph 1-based + the E_ph / E_field bins); bins: jgpsp |
+ * jgplc << 8 | jgpmu << 16 (| C2D_CENS_ESW | C2D_CENS_VOL | C2D_CENS_DEAD). */
+typedef double __attribute__((ext_vector_type(2))) c2d_d2;
+typedef uint32_t __attribute__((ext_vector_type(4))) c2d_u4;
 struct CensusSoA {
-  double* rpre; double* zpre; double* wmu; double* phi; double* ew; double* xnu;
-  uint32_t* jk;      /* c2d_cens_jk: jph, kph (1-based) + the E_ph / E_field bins */
-  uint32_t* bins;    /* jgpsp | jgplc << 8 | jgpmu << 16 (| C2D_CENS_ESW) */
-  uint64_t* key;
+  c2d_d2* rz;
+  c2d_d2* wp;
+  c2d_d2* ex;
+  c2d_u4* tg;
 };
 
 /* Collision record: packet state after the move to the collision point
@@ -161,6 +168,25 @@ template <class T>
 __device__ __forceinline__ T gld(const T* p) { return *(const C2D_GLOBAL T*)p; }
 template <class T>
 __device__ __forceinline__ void gst(T* p, T v) { *(C2D_GLOBAL T*)p = v; }
+/* census columns (CensusSoA): one 16-B global access each */
+__device__ __forceinline__ void cst2(c2d_d2* p, double a, double b) {
+  const c2d_d2 v = {a, b};
+  *(C2D_GLOBAL c2d_d2*)p = v;
+}
+__device__ __forceinline__ c2d_d2 cld2(const c2d_d2* p) { return *(const C2D_GLOBAL c2d_d2*)p; }
+__device__ __forceinline__ void cst4(c2d_u4* p, uint32_t jk, uint32_t bins, uint64_t key) {
+  const c2d_u4 v = {jk, bins, (uint32_t)key, (uint32_t)(key >> 32)};
+  *(C2D_GLOBAL c2d_u4*)p = v;
+}
+__device__ __forceinline__ c2d_u4 cld4(const c2d_u4* p) { return *(const C2D_GLOBAL c2d_u4*)p; }
+__device__ __forceinline__ uint64_t c2d_tg_key(c2d_u4 t) { return ((uint64_t)t.w << 32) | (uint64_t)t.z; }
+/* a record's bins word alone (compaction scans, dead marks) */
+__device__ __forceinline__ uint32_t cens_bins(const c2d_u4* tg, int64_t s) {
+  return gld(reinterpret_cast<const uint32_t*>(tg + s) + 1);
+}
+__device__ __forceinline__ void cens_set_bins(c2d_u4* tg, int64_t s, uint32_t b) {
+  gst(reinterpret_cast<uint32_t*>(tg + s) + 1, b);
+}
 __device__ __forceinline__ void gadd(double* p, double v) {
   __hip_atomic_fetch_add((C2D_GLOBAL double*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

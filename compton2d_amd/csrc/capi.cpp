@@ -93,14 +93,11 @@ struct DevPk {
 };
 
 struct DevCensus {
-  double* d[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  uint32_t* jk = nullptr;
-  uint32_t* bins = nullptr;
-  uint64_t* key = nullptr;
+  c2d_d2* d[3] = {nullptr, nullptr, nullptr};   /* rz, wp, ex (CensusSoA) */
+  c2d_u4* tg = nullptr;
   CensusSoA soa() const {
     CensusSoA s;
-    s.rpre = d[0]; s.zpre = d[1]; s.wmu = d[2]; s.phi = d[3]; s.ew = d[4]; s.xnu = d[5];
-    s.jk = jk; s.bins = bins; s.key = key;
+    s.rz = d[0]; s.wp = d[1]; s.ex = d[2]; s.tg = tg;
     return s;
   }
 };
@@ -476,10 +473,8 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
       HIPCHK(c, dalloc(&c->cscan, 2 * (size_t)c->cscan_cap));
     }
     for (int b = 0; b < (c->chunked ? 1 : 2); b++) {
-      for (int f = 0; f < 6; f++) HIPCHK(c, dalloc(&c->cens[b].d[f], (size_t)c->cens_phys));
-      HIPCHK(c, dalloc(&c->cens[b].jk, (size_t)c->cens_phys));
-      HIPCHK(c, dalloc(&c->cens[b].bins, (size_t)c->cens_phys));
-      HIPCHK(c, dalloc(&c->cens[b].key, (size_t)c->cens_phys));
+      for (int f = 0; f < 3; f++) HIPCHK(c, dalloc(&c->cens[b].d[f], (size_t)c->cens_phys));
+      HIPCHK(c, dalloc(&c->cens[b].tg, (size_t)c->cens_phys));
     }
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -502,11 +497,9 @@ extern "C" void c2d_finalize(c2d_ctx* c) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int b = 0; b < 2; b++) {
-    for (int f = 0; f < 6; f++)
+    for (int f = 0; f < 3; f++)
       if (c->cens[b].d[f]) (void)hipFree(c->cens[b].d[f]);
-    if (c->cens[b].jk) (void)hipFree(c->cens[b].jk);
-    if (c->cens[b].bins) (void)hipFree(c->cens[b].bins);
-    if (c->cens[b].key) (void)hipFree(c->cens[b].key);
+    if (c->cens[b].tg) (void)hipFree(c->cens[b].tg);
   }
   for (double* p : c->spec_bufs) (void)hipFree(p);
   void* optrs[] = {c->obs_edges, c->obs_hist, c->obs_ev, c->pspt_red, c->cdf_guide};
@@ -807,17 +800,17 @@ __global__ void __launch_bounds__(256) c2d_nf_reduce(const double* __restrict__ 
 #endif
 constexpr int CT_TILE = C2D_CT_TILE, CT_BLOCK = 256;
 
-__device__ __forceinline__ void census_class(const uint32_t* bins, int64_t i, int64_t R, int64_t W,
+__device__ __forceinline__ void census_class(const c2d_u4* tg, int64_t i, int64_t R, int64_t W,
                                              bool& hole, bool& src) {
   hole = src = false;
   if (i < R) {
-    const bool dead = (bins[i] & C2D_CENS_DEAD) != 0u;
+    const bool dead = (cens_bins(tg, i) & C2D_CENS_DEAD) != 0u;
     hole = dead && i < W;
     src = !dead && i >= W;
   }
 }
 
-__global__ void __launch_bounds__(CT_BLOCK) c2d_census_count(const uint32_t* __restrict__ bins, int64_t R,
+__global__ void __launch_bounds__(CT_BLOCK) c2d_census_count(const c2d_u4* __restrict__ tg, int64_t R,
                                                              int64_t W, const uint8_t* __restrict__ flag,
                                                              uint32_t* __restrict__ cnt) {
   __shared__ uint32_t sh[2][CT_BLOCK / 64];
@@ -832,7 +825,7 @@ __global__ void __launch_bounds__(CT_BLOCK) c2d_census_count(const uint32_t* __r
   uint32_t nh = 0, ns = 0;
   for (int j = 0; j < CT_TILE / CT_BLOCK; j++) {
     bool h, s;
-    census_class(bins, base + j * CT_BLOCK + threadIdx.x, R, W, h, s);
+    census_class(tg, base + j * CT_BLOCK + threadIdx.x, R, W, h, s);
     nh += (uint32_t)__popcll(__ballot(h));
     ns += (uint32_t)__popcll(__ballot(s));
   }
@@ -878,7 +871,7 @@ __global__ void __launch_bounds__(1024) c2d_census_scan(uint32_t* __restrict__ c
   }
 }
 
-__global__ void __launch_bounds__(CT_BLOCK) c2d_census_emit(const uint32_t* __restrict__ bins, int64_t R,
+__global__ void __launch_bounds__(CT_BLOCK) c2d_census_emit(const c2d_u4* __restrict__ tg, int64_t R,
                                                             int64_t W, const unsigned long long* __restrict__ off,
                                                             int64_t cap, int64_t* __restrict__ holes,
                                                             int64_t* __restrict__ srcs) {
@@ -893,7 +886,7 @@ __global__ void __launch_bounds__(CT_BLOCK) c2d_census_emit(const uint32_t* __re
   for (int j = 0; j < CT_TILE / CT_BLOCK; j++) {
     const int64_t i = base + j * CT_BLOCK + threadIdx.x;
     bool h, s;
-    census_class(bins, i, R, W, h, s);
+    census_class(tg, i, R, W, h, s);
     const unsigned long long mh = __ballot(h), ms = __ballot(s);
     if (lane == 0) { sh[0][w] = (uint32_t)__popcll(mh); sh[1][w] = (uint32_t)__popcll(ms); }
     __syncthreads();
@@ -920,34 +913,34 @@ __global__ void __launch_bounds__(256) c2d_census_fill(CensusSoA c, const int64_
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < m;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t d = holes[t], s = srcs[t];
-    c.rpre[d] = c.rpre[s]; c.zpre[d] = c.zpre[s]; c.wmu[d] = c.wmu[s]; c.phi[d] = c.phi[s];
-    c.ew[d] = c.ew[s]; c.xnu[d] = c.xnu[s]; c.jk[d] = c.jk[s]; c.bins[d] = c.bins[s];
-    c.key[d] = c.key[s];
-    c.bins[s] = C2D_CENS_DEAD;          /* moved: the next round must not list it again */
+    const c2d_d2 rz = cld2(c.rz + s), wp = cld2(c.wp + s), ex = cld2(c.ex + s);
+    const c2d_u4 tg = cld4(c.tg + s);
+    cst2(c.rz + d, rz.x, rz.y);
+    cst2(c.wp + d, wp.x, wp.y);
+    cst2(c.ex + d, ex.x, ex.y);
+    cst4(c.tg + d, tg.x, tg.y, c2d_tg_key(tg));
+    cens_set_bins(c.tg, s, C2D_CENS_DEAD);   /* moved: the next round must not list it again */
   }
 }
 
 /* ---- census records: packed 8-word form (C2D_CENSUS_REC_WORDS), bit-exact ---- */
 __device__ __forceinline__ void rec_pack(const CensusSoA& cs, int64_t s, uint64_t* r) {
-  r[0] = __double_as_longlong(cs.rpre[s]);
-  r[1] = __double_as_longlong(cs.zpre[s]);
-  r[2] = __double_as_longlong(cs.wmu[s]);
-  r[3] = __double_as_longlong(cs.phi[s]);
-  r[4] = __double_as_longlong(cs.ew[s]);
-  r[5] = __double_as_longlong(cs.xnu[s]);
-  r[6] = (uint64_t)cs.jk[s] | ((uint64_t)cs.bins[s] << 32);
-  r[7] = cs.key[s];
+  const c2d_d2 rz = cld2(cs.rz + s), wp = cld2(cs.wp + s), ex = cld2(cs.ex + s);
+  const c2d_u4 tg = cld4(cs.tg + s);
+  r[0] = __double_as_longlong(rz.x);
+  r[1] = __double_as_longlong(rz.y);
+  r[2] = __double_as_longlong(wp.x);
+  r[3] = __double_as_longlong(wp.y);
+  r[4] = __double_as_longlong(ex.x);
+  r[5] = __double_as_longlong(ex.y);
+  r[6] = (uint64_t)tg.x | ((uint64_t)tg.y << 32);
+  r[7] = c2d_tg_key(tg);
 }
 __device__ __forceinline__ void rec_unpack(const CensusSoA& cs, int64_t d, const uint64_t* r) {
-  cs.rpre[d] = __longlong_as_double(r[0]);
-  cs.zpre[d] = __longlong_as_double(r[1]);
-  cs.wmu[d] = __longlong_as_double(r[2]);
-  cs.phi[d] = __longlong_as_double(r[3]);
-  cs.ew[d] = __longlong_as_double(r[4]);
-  cs.xnu[d] = __longlong_as_double(r[5]);
-  cs.jk[d] = (uint32_t)(r[6] & 0xffffffffull);
-  cs.bins[d] = (uint32_t)(r[6] >> 32);
-  cs.key[d] = r[7];
+  cst2(cs.rz + d, __longlong_as_double(r[0]), __longlong_as_double(r[1]));
+  cst2(cs.wp + d, __longlong_as_double(r[2]), __longlong_as_double(r[3]));
+  cst2(cs.ex + d, __longlong_as_double(r[4]), __longlong_as_double(r[5]));
+  cst4(cs.tg + d, (uint32_t)(r[6] & 0xffffffffull), (uint32_t)(r[6] >> 32), r[7]);
 }
 /* census record i -> its slot (chunked: through the chunk list) */
 __device__ __forceinline__ int64_t cens_slot(const int32_t* clist, int64_t i) {
@@ -990,12 +983,12 @@ __global__ void __launch_bounds__(256) c2d_chunk_select(const int32_t* __restric
 /* double-buffered census after the step: the unused tail of each wave
  * slot's last chunk (one workgroup per slot) is marked dead and counted */
 __global__ void __launch_bounds__(256) c2d_chunk_tails(const int64_t* __restrict__ cstate, uint32_t chunk,
-                                                       int64_t cap, uint32_t* __restrict__ bins,
+                                                       int64_t cap, c2d_u4* __restrict__ tg,
                                                        unsigned long long* __restrict__ dead) {
   const int64_t base = cstate[2 * blockIdx.x], used = cstate[2 * blockIdx.x + 1];
   if (base < 0 || used <= 0 || used >= (int64_t)chunk || base >= cap) return;
   const int64_t t1 = base + chunk < cap ? base + chunk : cap;
-  for (int64_t s = base + used + threadIdx.x; s < t1; s += blockDim.x) bins[s] = C2D_CENS_DEAD;
+  for (int64_t s = base + used + threadIdx.x; s < t1; s += blockDim.x) cens_set_bins(tg, s, C2D_CENS_DEAD);
   if (threadIdx.x == 0 && t1 > base + used) atomicAdd(dead, (unsigned long long)(t1 - base - used));
 }
 
@@ -1209,11 +1202,11 @@ static int census_compact(c2d_ctx* c, const DevCensus& cb, int64_t R, int64_t W)
   int64_t* srcs = c->cscan + c->cscan_cap;
   for (int round = 0;; round++) {
     hipLaunchKernelGGL(c2d_census_count, dim3((unsigned)ntiles), dim3(CT_BLOCK), 0, c->stream,
-                       cb.bins, R, W, c->ctile_flag, c->ctile_cnt);
+                       cb.tg, R, W, c->ctile_flag, c->ctile_cnt);
     hipLaunchKernelGGL(c2d_census_scan, dim3(1), dim3(1024), 0, c->stream, c->ctile_cnt, ntiles,
                        c->ctile_off);
     hipLaunchKernelGGL(c2d_census_emit, dim3((unsigned)ntiles), dim3(CT_BLOCK), 0, c->stream,
-                       cb.bins, R, W, c->ctile_off, c->cscan_cap, holes, srcs);
+                       cb.tg, R, W, c->ctile_off, c->cscan_cap, holes, srcs);
     HIPCHK(c, hipGetLastError());
     unsigned long long nn[2];
     HIPCHK(c, hipMemcpyAsync(nn, c->ctile_off + 2 * ntiles, sizeof nn, hipMemcpyDeviceToHost, c->stream));
@@ -1472,7 +1465,7 @@ static int run_step_body(c2d_ctx* c) {
   {
     if (!c->chunked && c->n_ws > 0) {
       hipLaunchKernelGGL(c2d_chunk_tails, dim3((unsigned)c->n_ws), dim3(256), 0, c->stream, c->cstate,
-                         c->cens_chunk, c->cens_phys, c->cens[out_buf].bins,
+                         c->cens_chunk, c->cens_phys, c->cens[out_buf].tg,
                          c->ctl + CTL_CNT + C2D_CNT_DEAD_INT);
       HIPCHK(c, hipGetLastError());
     }
@@ -1743,14 +1736,14 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
   HIPCHK(c, hipStreamSynchronize(c->stream));
   /* records [0, n) of the SoA (chunked: the list's chunks 0, 1, ...) */
   const DevCensus& d = c->cens[c->cur];
-  std::vector<double> col(n);
+  std::vector<c2d_d2> col(n);
   const bool enc = cens_encoded(c);
-  for (int f = 0; f < 6; f++) {
+  for (int f = 0; f < 3; f++) {
     for (int64_t i = 0; i < n; i++) {
-      col[i] = d6[6 * i + f];
-      if (f == 3 && enc) col[i] = c2d_cos(col[i]);
+      col[i].x = d6[6 * i + 2 * f];
+      col[i].y = (f == 1 && enc) ? c2d_cos(d6[6 * i + 3]) : d6[6 * i + 2 * f + 1];
     }
-    if (n) HIPCHK(c, hipMemcpy(d.d[f], col.data(), n * sizeof(double), hipMemcpyHostToDevice));
+    if (n) HIPCHK(c, hipMemcpy(d.d[f], col.data(), n * sizeof(c2d_d2), hipMemcpyHostToDevice));
   }
   std::vector<uint32_t> jk(n), bins(n);
   for (int64_t i = 0; i < n; i++) {
@@ -1771,9 +1764,14 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
     jk[i] = c2d_cens_jk(q[3], q[4], ie, efl);
   }
   if (n) {
-    HIPCHK(c, hipMemcpy(d.jk, jk.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(d.bins, bins.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(d.key, keys, n * sizeof(uint64_t), hipMemcpyHostToDevice));
+    std::vector<c2d_u4> tg(n);
+    for (int64_t i = 0; i < n; i++) {
+      tg[i].x = jk[i];
+      tg[i].y = bins[i];
+      tg[i].z = (uint32_t)keys[i];
+      tg[i].w = (uint32_t)(keys[i] >> 32);
+    }
+    HIPCHK(c, hipMemcpy(d.tg, tg.data(), n * sizeof(c2d_u4), hipMemcpyHostToDevice));
   }
   if (c->chunked) {
     const int64_t k = (n + C2D_CCHUNK - 1) / C2D_CCHUNK;

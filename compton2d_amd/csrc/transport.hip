@@ -979,23 +979,19 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
   }
   const unsigned long long slot = census_slot_chunk(P);
   if (slot < (unsigned long long)P.cap_cout) {
-    gst(P.cout.rpre + slot, p.rpre);
-    gst(P.cout.zpre + slot, p.zpre);
-    gst(P.cout.wmu + slot, p.wmu);
+    cst2(P.cout.rz + slot, p.rpre, p.zpre);
 #if C2D_TABLE_COMTOT
-    gst(P.cout.phi + slot, p.eta);                   /* encoded azimuth (CensusSoA) */
+    cst2(P.cout.wp + slot, p.wmu, p.eta);            /* encoded azimuth (CensusSoA) */
 #else
-    gst(P.cout.phi + slot, p.phi);
+    cst2(P.cout.wp + slot, p.wmu, p.phi);
 #endif
-    gst(P.cout.ew + slot, p.ew);
-    gst(P.cout.xnu + slot, p.xnu);
-    gst(P.cout.jk + slot, c2d_cens_jk(p.jph, p.kph, p.ie & 0xffff, efl));
-    gst(P.cout.bins + slot, (p.bins & 0x00ffffffu)
+    cst2(P.cout.ex + slot, p.ew, p.xnu);
+    cst4(P.cout.tg + slot, c2d_cens_jk(p.jph, p.kph, p.ie & 0xffff, efl),
+         (p.bins & 0x00ffffffu)
 #if C2D_TABLE_COMTOT
-                                | (p.esw == -1 ? C2D_CENS_ESW : 0u)
+             | (p.esw == -1 ? C2D_CENS_ESW : 0u)
 #endif
-    );
-    gst(P.cout.key + slot, c2d_census_key(p.key, p.ctr, p.sub));
+         , c2d_census_key(p.key, p.ctr, p.sub));
   } else {
     gor(P.err, ERR_CENSUS);
   }
@@ -1646,24 +1642,20 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_source_kernel)(const KPara
       if (it < P.n_vol_items) {
         /* census format (pf_apply reads it back; C2D_CENS_VOL: dcen from the key) */
         const int64_t s = P.vol_cens_base + it;
-        gst(P.cin.rpre + s, p.rpre);
-        gst(P.cin.zpre + s, p.zpre);
-        gst(P.cin.wmu + s, p.wmu);
+        cst2(P.cin.rz + s, p.rpre, p.zpre);
 #if C2D_TABLE_COMTOT
         const double eta = c2d_cos(p.phi);           /* set_phi's encoding (CensusSoA) */
         const bool esw_neg = !(p.phi <= PI_REF && p.phi >= 1.0e-10);
-        gst(P.cin.phi + s, eta);
+        cst2(P.cin.wp + s, p.wmu, eta);
 #else
         const bool esw_neg = false;
-        gst(P.cin.phi + s, p.phi);
+        cst2(P.cin.wp + s, p.wmu, p.phi);
 #endif
-        gst(P.cin.ew + s, p.ew);
-        gst(P.cin.xnu + s, p.xnu);
+        cst2(P.cin.ex + s, p.ew, p.xnu);
         const int ie = grid_lookup(g->E_ph, C2D_N_VOL, g->eph_start, g->eph_k0, p.xnu);
         const int efl = p.xnu > P.egg_min ? grid_lookup(g->E_field, C2D_NPHFIELD, g->efl_start, g->efl_k0, p.xnu) : 0;
-        gst(P.cin.jk + s, c2d_cens_jk(p.jph, p.kph, ie, efl));
-        gst(P.cin.bins + s, (p.bins & 0x00ffffffu) | C2D_CENS_VOL | (esw_neg ? C2D_CENS_ESW : 0u));
-        gst(P.cin.key + s, p.key);
+        cst4(P.cin.tg + s, c2d_cens_jk(p.jph, p.kph, ie, efl),
+             (p.bins & 0x00ffffffu) | C2D_CENS_VOL | (esw_neg ? C2D_CENS_ESW : 0u), p.key);
       } else {
         store_pk(P.pk, it - P.n_vol_items, p);
       }
@@ -1767,12 +1759,13 @@ struct CensRec {
 
 __device__ __forceinline__ void pf_issue(const KParams& P0, CensRec& r, long long i) {
   const KParams& P = cold(P0);
-  r.rpre = gld(P.cin.rpre + i); r.zpre = gld(P.cin.zpre + i);
-  r.wmu = gld(P.cin.wmu + i);
-  r.ew = gld(P.cin.ew + i); r.xnu = gld(P.cin.xnu + i);
-  r.jk = gld(P.cin.jk + i); r.bn = gld(P.cin.bins + i);
-  r.cphi = gld(P.cin.phi + i);
-  r.key = gld(P.cin.key + i);
+  const c2d_d2 rz = cld2(P.cin.rz + i), wp = cld2(P.cin.wp + i), ex = cld2(P.cin.ex + i);
+  const c2d_u4 tg = cld4(P.cin.tg + i);
+  r.rpre = rz.x; r.zpre = rz.y;
+  r.wmu = wp.x; r.cphi = wp.y;
+  r.ew = ex.x; r.xnu = ex.y;
+  r.jk = tg.x; r.bn = tg.y;
+  r.key = c2d_tg_key(tg);
 }
 
 __device__ __forceinline__ void pf_apply(const KParams& P0, Pkt& p, const CensRec& r) {
@@ -1812,17 +1805,13 @@ __device__ __forceinline__ void pf_dword(const void* src, int w, int f) {
 __device__ __forceinline__ void pf_issue_lds(const KParams& P0, long long i) {
   const KParams& P = cold(P0);
   const int w = (int)(threadIdx.x >> 6);
-  const double* d[6] = {P.cin.rpre + i, P.cin.zpre + i, P.cin.wmu + i, P.cin.phi + i, P.cin.ew + i,
-                        P.cin.xnu + i};
+  /* dwords 0-3 (rpre, zpre), 4-7 (wmu, phi), 8-11 (ew, xnu), 12-15 (jk, bins, key) */
+  const uint32_t* d[4] = {reinterpret_cast<const uint32_t*>(P.cin.rz + i),
+                          reinterpret_cast<const uint32_t*>(P.cin.wp + i),
+                          reinterpret_cast<const uint32_t*>(P.cin.ex + i),
+                          reinterpret_cast<const uint32_t*>(P.cin.tg + i)};
 #pragma unroll
-  for (int f = 0; f < 6; f++) {
-    pf_dword(d[f], w, 2 * f);
-    pf_dword(reinterpret_cast<const uint32_t*>(d[f]) + 1, w, 2 * f + 1);
-  }
-  pf_dword(P.cin.jk + i, w, 12);
-  pf_dword(P.cin.bins + i, w, 13);
-  pf_dword(P.cin.key + i, w, 14);
-  pf_dword(reinterpret_cast<const uint32_t*>(P.cin.key + i) + 1, w, 15);
+  for (int f = 0; f < 16; f++) pf_dword(d[f >> 2] + (f & 3), w, f);
 }
 __device__ __forceinline__ void pf_read_lds(CensRec& r) {
   /* the loads' LDS writes complete in vmcnt order: wait for all of them */
