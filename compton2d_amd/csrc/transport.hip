@@ -103,7 +103,13 @@ constexpr double RAD_CP = 3.333564097e-11;     /* general.pa:23 */
 constexpr double EMASSKEV = 5.11e2;
 constexpr double SIGTHOM = 6.6516e-25;
 constexpr int BLOCK = C2D_TR_BLOCK;   /* transport and bundle kernels */
-constexpr int SBLOCK = 256;       /* source / scatter kernels */
+constexpr int SBLOCK = 256;       /* scatter kernel */
+/* source kernel: its LDS (the Geo image and the volume prefix, ~26 KB) per
+ * workgroup limits a CU to 6 of them; 512 threads make that 8 waves per SIMD */
+#ifndef C2D_SRC_BLOCK
+#define C2D_SRC_BLOCK 512
+#endif
+constexpr int SRCBLOCK = C2D_SRC_BLOCK;
 /* generation-0 items a wave takes per fetch (one returning atomic on a work
  * shard counter: 64 -> 256 -> 1024 items, +6 %, +2 %) */
 #ifndef C2D_WORK_CHUNK
@@ -1585,7 +1591,7 @@ __device__ __forceinline__ void load_pk(Pkt& p, const PktSoA& s, int64_t i) {
 /* generation-0 sources: volume (imcvol2d_para.f:90-414) and surface     */
 /* (imcsurf2d_para.f:228-534) packets, one lane per packet               */
 /* ------------------------------------------------------------------ */
-__global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_source_kernel)(const KParams* __restrict__ Pg) {
+__global__ void __launch_bounds__(SRCBLOCK) C2D_SFX(c2d_source_kernel)(const KParams* __restrict__ Pg) {
   const KParams& P = *Pg;
   __shared__ double geo_lds[GEO_DOUBLES];
   /* the volume-source prefix over cells, for the per-packet cell search
@@ -1595,15 +1601,15 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_source_kernel)(const KPara
   const bool pref_in_lds = P.ncell + 1 <= PREF_LDS;
   {
     const double* gsrc = reinterpret_cast<const double*>(P.geo);
-    for (int i = threadIdx.x; i < GEO_DOUBLES; i += SBLOCK) geo_lds[i] = gsrc[i];
+    for (int i = threadIdx.x; i < GEO_DOUBLES; i += SRCBLOCK) geo_lds[i] = gsrc[i];
     if (pref_in_lds)
-      for (int i = threadIdx.x; i <= P.ncell; i += SBLOCK) pref_lds[i] = P.vol_prefix[i];
+      for (int i = threadIdx.x; i <= P.ncell; i += SRCBLOCK) pref_lds[i] = P.vol_prefix[i];
   }
   __syncthreads();
   const Geo* g = reinterpret_cast<const Geo*>(geo_lds);
   const int64_t n = P.n_vol_items + P.n_surf_items;
-  const int64_t stride = (int64_t)gridDim.x * SBLOCK;
-  for (int64_t it = (int64_t)blockIdx.x * SBLOCK + threadIdx.x; it < n; it += stride) {
+  const int64_t stride = (int64_t)gridDim.x * SRCBLOCK;
+  for (int64_t it = (int64_t)blockIdx.x * SRCBLOCK + threadIdx.x; it < n; it += stride) {
     Pkt p;
     p.ctr = 0;
     p.sub = 0;
@@ -2767,7 +2773,7 @@ extern "C" int C2D_SFX(c2d_bundle_occupancy)(int* blocks_per_cu, size_t lds_byte
 }
 
 extern "C" int C2D_SFX(c2d_launch_source)(const c2d::KParams* P_dev, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(C2D_SFX(c2d::c2d_source_kernel), dim3(grid), dim3(c2d::SBLOCK), 0, stream, P_dev);
+  hipLaunchKernelGGL(C2D_SFX(c2d::c2d_source_kernel), dim3(grid), dim3(c2d::SRCBLOCK), 0, stream, P_dev);
   return (int)hipGetLastError();
 }
 
@@ -2783,7 +2789,7 @@ extern "C" int C2D_SFX(c2d_launch_scatter)(const c2d::KParams* P_dev, const c2d:
  * plain CUs x 8 grid would assume, leaving a second partial round */
 extern "C" int C2D_SFX(c2d_aux_occupancy)(int which, int* blocks_per_cu) {
   hipError_t e = which == 0
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, C2D_SFX(c2d::c2d_source_kernel), c2d::SBLOCK, 0)
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, C2D_SFX(c2d::c2d_source_kernel), c2d::SRCBLOCK, 0)
       : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, C2D_SFX(c2d::c2d_scatter_kernel), c2d::SBLOCK, 0);
   return (int)e;
 }
