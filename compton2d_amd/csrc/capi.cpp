@@ -1734,44 +1734,45 @@ extern "C" int c2d_census_import(c2d_ctx* c, const double* d6, const int32_t* i5
     return fail(c, C2D_E_CENSUS_OVERFLOW, "census import %lld > capacity", (long long)n);
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  /* records [0, n) of the SoA (chunked: the list's chunks 0, 1, ...) */
+  /* records [0, n) of the SoA (chunked: the list's chunks 0, 1, ...), in
+   * batches so the host staging stays bounded */
   const DevCensus& d = c->cens[c->cur];
-  std::vector<c2d_d2> col(n);
   const bool enc = cens_encoded(c);
-  for (int f = 0; f < 3; f++) {
-    for (int64_t i = 0; i < n; i++) {
-      col[i].x = d6[6 * i + 2 * f];
-      col[i].y = (f == 1 && enc) ? c2d_cos(d6[6 * i + 3]) : d6[6 * i + 2 * f + 1];
+  const int64_t B = std::min<int64_t>(n, int64_t(1) << 20);
+  std::vector<c2d_d2> col((size_t)B);
+  std::vector<c2d_u4> tg((size_t)B);
+  for (int64_t i0 = 0; i0 < n; i0 += B) {
+    const int64_t nb = std::min(B, n - i0);
+    for (int f = 0; f < 3; f++) {
+      for (int64_t t = 0; t < nb; t++) {
+        const double* r = d6 + 6 * (i0 + t);
+        col[t].x = r[2 * f];
+        col[t].y = (f == 1 && enc) ? c2d_cos(r[3]) : r[2 * f + 1];
+      }
+      HIPCHK(c, hipMemcpy(d.d[f] + i0, col.data(), nb * sizeof(c2d_d2), hipMemcpyHostToDevice));
     }
-    if (n) HIPCHK(c, hipMemcpy(d.d[f], col.data(), n * sizeof(c2d_d2), hipMemcpyHostToDevice));
-  }
-  std::vector<uint32_t> jk(n), bins(n);
-  for (int64_t i = 0; i < n; i++) {
-    const int32_t* q = i5 + 5 * i;
-    if (q[3] < 1 || q[3] > c->nz || q[4] < 1 || q[4] > c->nr || q[0] < 0 || q[0] > 255 ||
-        q[1] < 0 || q[1] > 255 || q[2] < 0 || q[2] > 255)
-      return fail(c, C2D_E_ARG, "census record %lld out of range", (long long)i);
-    bins[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16);
-    if (enc) {
-      const double ph = d6[6 * i + 3];
-      if (!(ph <= C2D_PI_REF && ph >= 1.0e-10)) bins[i] |= C2D_CENS_ESW;
+    for (int64_t t = 0; t < nb; t++) {
+      const int64_t i = i0 + t;
+      const int32_t* q = i5 + 5 * i;
+      if (q[3] < 1 || q[3] > c->nz || q[4] < 1 || q[4] > c->nr || q[0] < 0 || q[0] > 255 ||
+          q[1] < 0 || q[1] > 255 || q[2] < 0 || q[2] > 255)
+        return fail(c, C2D_E_ARG, "census record %lld out of range", (long long)i);
+      uint32_t bins = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16);
+      if (enc) {
+        const double ph = d6[6 * i + 3];
+        if (!(ph <= C2D_PI_REF && ph >= 1.0e-10)) bins |= C2D_CENS_ESW;
+      }
+      /* the E_ph / E_field bins of xnu the record carries (c2d_cens_jk), with
+       * the kernels' semantics (grid_lookup = the bisection, build_lookup) */
+      const double xnu = d6[6 * i + 5];
+      const int ie = grid_bin_host(c->geo_h.E_ph, C2D_N_VOL, xnu);
+      const int efl = xnu > c->egg_min ? grid_bin_host(c->geo_h.E_field, C2D_NPHFIELD, xnu) : 0;
+      tg[t].x = c2d_cens_jk(q[3], q[4], ie, efl);
+      tg[t].y = bins;
+      tg[t].z = (uint32_t)keys[i];
+      tg[t].w = (uint32_t)(keys[i] >> 32);
     }
-    /* the E_ph / E_field bins of xnu the record carries (c2d_cens_jk), with
-     * the kernels' semantics (grid_lookup = the bisection, build_lookup) */
-    const double xnu = d6[6 * i + 5];
-    const int ie = grid_bin_host(c->geo_h.E_ph, C2D_N_VOL, xnu);
-    const int efl = xnu > c->egg_min ? grid_bin_host(c->geo_h.E_field, C2D_NPHFIELD, xnu) : 0;
-    jk[i] = c2d_cens_jk(q[3], q[4], ie, efl);
-  }
-  if (n) {
-    std::vector<c2d_u4> tg(n);
-    for (int64_t i = 0; i < n; i++) {
-      tg[i].x = jk[i];
-      tg[i].y = bins[i];
-      tg[i].z = (uint32_t)keys[i];
-      tg[i].w = (uint32_t)(keys[i] >> 32);
-    }
-    HIPCHK(c, hipMemcpy(d.tg, tg.data(), n * sizeof(c2d_u4), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(d.tg + i0, tg.data(), nb * sizeof(c2d_u4), hipMemcpyHostToDevice));
   }
   if (c->chunked) {
     const int64_t k = (n + C2D_CCHUNK - 1) / C2D_CCHUNK;
