@@ -617,6 +617,28 @@ __device__ __forceinline__ bool mcd_mtab(const double* __restrict__ mom, const d
   return true;
 }
 
+/* C2D_FPF_MT_PF: the table entries of the next search's first candidates
+ * (Theta 1.005^{+-1}) fetched into the caches at the top of the sub-step,
+ * by 12 lanes of wave 0 through global -> LDS loads into a scratch row (no
+ * registers held, nothing waits for them): the search then finds them in L2 */
+#ifndef C2D_FPF_MT_PF
+#define C2D_FPF_MT_PF 1
+#endif
+__shared__ uint32_t f_mtpf[64];
+typedef const __attribute__((address_space(1))) void* fpf_gptr_t;
+typedef __attribute__((address_space(3))) void* fpf_lptr_t;
+__device__ __forceinline__ void mt_prefetch(const double* __restrict__ mom, double th, int lane) {
+  if (!mom || lane >= 12) return;
+  const double t = lane < 6 ? th * F32(1.005) : th / F32(1.005);     /* the search's own lattice */
+  const double z = rcp_nr(t);
+  if (!(z >= 0x1p-17 && z <= 0x1p3)) return;
+  int j = (int)__builtin_rintf((__builtin_amdgcn_logf((float)z) - (float)C2D_FPF_MT_LO) * (float)C2D_FPF_MT_Q);
+  j = j < 0 ? 0 : (j > MT_N - 1 ? MT_N - 1 : j);
+  /* an entry spans 336 B: one dword every 64 B touches each of its cache lines */
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(mom + (size_t)j * MT_W) + (lane % 6) * 16;
+  __builtin_amdgcn_global_load_lds((fpf_gptr_t)a, (fpf_lptr_t)&f_mtpf[0], 4, 0, 0);
+}
+
 /* Neumaier's compensated sum */
 __device__ __forceinline__ void nsum(double& s, double& c, double w) {
   const double t = s + w;
@@ -1040,6 +1062,9 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
   }
   for (;;) {
     /* label 200 (:577) */
+#if C2D_FPF_MT_PF
+    if (B.wave == 0 && Th_e >= F32(0.2)) mt_prefetch(P.mom, Th_e, B.lane);
+#endif
     PF_BEGIN();
     const double g_av0 = (fp_steps == 0) ? gamma_bar_m(Th_e, true) : g_av_next;
     PF_END(pf_gb);
