@@ -2397,13 +2397,24 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
         const float Cw = (float)(rpre * rpre * (1.0 - wmu * wmu));
         const float qf = (float)qabs;
         float wsum = 0.0f;
+        /* c2d_abspt(key, sub, n) = mix64(key + gamma ((sub << 32 | n) + 1)):
+         * the argument advances by gamma per output (an add, not a 64-bit
+         * multiply per output); the same outputs */
+        uint64_t zst = p.key + 0x9E3779B97F4A7C15ull * ((((uint64_t)sub << 32) | (uint64_t)b.actr) + 1ull);
         for (int t = 0; t < nabs; t += 2) {
-          const uint64_t wo = c2d_abspt(p.key, sub, b.actr++);
+          const uint64_t wo = c2d_mix64(zst);
+          zst += 0x9E3779B97F4A7C15ull;
+          b.actr++;
 #pragma unroll
           for (int j = 0; j < 2; j++) {
             if (t + j < nabs) {
               const uint32_t u = j == 0 ? (uint32_t)(wo >> 32) : (uint32_t)wo;
-              const float x = ((float)(u >> 8) + 0.5f) * (5.9604644775390625e-8f * qf);
+              /* the top 24 bits by one v_cvt_f32_u32: written as (float)(u >> 8),
+               * the high half's conversion was widened to a 64-bit shift and a
+               * u64 -> f32 expansion (7 more instructions) */
+              float fu;
+              __asm__("v_cvt_f32_u32 %0, %1" : "=v"(fu) : "v"(u >> 8));
+              const float x = (fu + 0.5f) * (5.9604644775390625e-8f * qf);
               const float L = (x < 1.0e-2f)
                   ? x * __builtin_fmaf(x, __builtin_fmaf(x, __builtin_fmaf(x, 0.25f, 0.33333334f), 0.5f), 1.0f)
                   : -0.69314718f * __builtin_amdgcn_logf(1.0f - x);
