@@ -190,21 +190,19 @@ def upper_surface_budget(r: np.ndarray, rmin: float, nst: int, dt: float, tbbu: 
 def volume_budget(nst: int, fas: np.ndarray):
     """nsv, ewsv of every zone (src/imcgen2d.f:406-413, :446-456):
     Emiss_tot sums fas in (j, k) order; nsv = int(0.5*nst*fas/Emiss_tot)
-    (Fortran truncation), ewsv = fas/nsv (0 for an empty zone)."""
-    fas = np.asarray(fas, np.float64)
+    (Fortran truncation), ewsv = fas/nsv (0 for an empty zone).  Vectorised
+    with the same operations: cumsum adds in order (a left fold, as the
+    reference's loop), then the same multiply, divide and truncation."""
+    fas = np.ascontiguousarray(fas, np.float64)
     nz, nr = fas.shape
-    emiss_tot = 0.0
-    for j in range(nz):
-        for k in range(nr):
-            emiss_tot = emiss_tot + float(fas[j, k])
-    nsv = np.zeros((nz, nr), np.int32)
-    ewsv = np.zeros((nz, nr))
+    emiss_tot = float(np.cumsum(fas.ravel())[-1]) if fas.size else 0.0
+    if emiss_tot == 0.0:
+        return np.zeros((nz, nr), np.int32), np.zeros((nz, nr))
     half = 0.5 * float(nst)
-    for j in range(nz):
-        for k in range(nr):
-            n = int(half * float(fas[j, k]) / emiss_tot) if emiss_tot != 0.0 else 0
-            nsv[j, k] = n
-            ewsv[j, k] = float(fas[j, k]) / float(n) if n > 0 else 0.0
+    nsv = np.trunc(half * fas / emiss_tot).astype(np.int32)
+    ewsv = np.zeros((nz, nr))
+    pos = nsv > 0
+    ewsv[pos] = fas[pos] / nsv[pos].astype(np.float64)
     return nsv, ewsv
 
 
