@@ -630,10 +630,12 @@ def main():
             "fp": wk == "c3",
             "comtot": ("table (cubic in ln E, 2048 pts per cell, f64)" if mode == abi.COMTOT_TABLE
                        else "exact 199-term sum"),
-            "arithmetic": ("f64 (positions, weights, tallies, comtot table stored in f64); the fast build "
-                           "samples the probes' absorption points, which weight only prdep, and draws the "
-                           "probe bundle's optical depth to its next collision, -log(u)/n, in f32 "
-                           "(transport.hip C2D_PT_F32, C2D_TAU_F32)" if mode == abi.COMTOT_TABLE
+            "arithmetic": ("f64 (geometry, positions, weights, tallies, the comtot table and its cubic "
+                           "interpolation); three statistics-only quantities of the fast build in f32, each to "
+                           "~1e-7 relative, inside the stated tolerance (tallies 1e-3, spectra <= 1 % L2 per "
+                           "north_star): the probes' absorption points, which weight only prdep "
+                           "(C2D_PT_F32), the bundle's optical depth -log(u)/n (C2D_TAU_F32) and the comtot "
+                           "table coordinate ln xnu (C2D_LNX_F32); DESIGN.md section 2" if mode == abi.COMTOT_TABLE
                            else "f64 throughout (exact build, bit for bit with the oracle)"),
             "tables": ("device-resident (C2D_DEV_EMISSION | C2D_DEV_ELECTRONS)"
                        if wk == "c3" and not args.host_tables else "host arrays"),
