@@ -498,6 +498,12 @@ __device__ __forceinline__ double rcp_nr(double x) {
   q = __builtin_fma(__builtin_fma(-x, q, 1.0), q, q);
   return __builtin_fma(__builtin_fma(-x, q, 1.0), q, q);
 }
+/* ... with 1/0 = inf as IEEE division has it (the Newton steps turn the
+ * estimate's inf into NaN) */
+__device__ __forceinline__ double rcp_nr_safe(double x) {
+  const double q = rcp_nr(x);
+  return x == 0.0 ? __builtin_amdgcn_rcp(x) : q;
+}
 
 /* McDonald moment table (C2D_FPF_MTAB).  Both series are sums over one fixed
  * abscissa lattice, S(z) = sum_{n <= f(z)} w_n exp(-z ts_n), so around a grid
@@ -938,6 +944,7 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
   const double Th_p = Tp_flare / 9.382e5;
   double Th_e = tea / 5.11e2;
   const double f_th = 1.5 * volume * n_lept;
+  const double r_fth = rcp_nr_safe(f_th), r_dt = rcp_nr_safe(P.dt), r_tesc = rcp_nr_safe(t_esc);
   /* dg_ic(i) = -sum_ph n_field(ph) F_IC(i,ph) / volume (:568-574) */
   if (i <= NT - 1) {
     double s = 0.0;
@@ -1049,6 +1056,7 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
   if (i <= NT - 1) f_bigC[i] = bigC_i;
   if (i >= 2 && i <= NT - 1) Delta_g_i = __builtin_sqrt(f_gnt[i] / f_gnt[i - 1]) * dgm;
   const double inj_sum0 = B.sum(inj_prof * dgp);     /* also publishes bigC */
+  const double r_inj0 = rcp_nr(inj_sum0);
   /* Chang-Cooper and tridiagonal factors: smw = bigB kS; with kP = 1/(Delta_g
    * D_gplus), kM = 1/(Delta_g D_gminus): tc = -d_t em_i kP, ta = -d_t bigW_{i-1}
    * bigC_{i-1} kM, tb = 1 + d_t (bigW_i bigC_i kP + em_{i-1} kM) + d_t/t_esc */
@@ -1077,24 +1085,27 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
       if (tid == 0) atomicOr(P.err, FPERR_STEPS);
       return;
     }
-    const double gamma_R = 2.1e-3 * __builtin_sqrt(n_lept) / (Bf * __builtin_sqrt(g_av));
+    /* this chain runs once per sub-step on every thread, ahead of everything
+     * else: its quotients through rcp_nr and exp(-y) through exp_nonpos
+     * (fast mode: a few ulp from the reference's IEEE operations) */
+    const double gamma_R = 2.1e-3 * __builtin_sqrt(n_lept) * rcp_nr_safe(Bf * __builtin_sqrt(g_av));
     const double sT = Th_e + Th_p;
-    const double h_T = F32(.79788) * (2. * (sT * sT) + 2.0 * sT + 1.0) /
-                       (sT * __builtin_sqrt(sT) * (1.0 + 1.875 * Th_e + .8203 * (Th_e * Th_e)));
+    const double h_T = F32(.79788) * (2. * (sT * sT) + 2.0 * sT + 1.0) *
+                       rcp_nr(sT * __builtin_sqrt(sT) * (1.0 + 1.875 * Th_e + .8203 * (Th_e * Th_e)));
     const double hr_th_Coul = f_th * 1.7386e-26 * n_p * LNL * h_T * (Tp_flare - Te_new);
-    const double yR = gamma_R / g_av;
-    const double hr_th_sy = (yR < 100.0) ? -Eloss_sy / (P.dt * c2d_exp_bf(yR)) : 0.0;
+    const double yR = gamma_R * rcp_nr(g_av);
+    const double hr_th_sy = (yR < 100.0) ? -Eloss_sy * exp_nonpos(-yR) * r_dt : 0.0;
     double hr_th_A = tlev * hr_th_Coul;
     if (hr_th_A < 1.0e-20) hr_th_A = 1.0e-20;
     const double hr_th_total = hr_th_sy + hr_th_c + hr_th_A;
-    const double dT_total = 6.25e8 * P.dt * hr_th_total / f_th;
-    double f_t_implicit = P.df_implicit * Te_new / fabs(dT_total);
+    const double dT_total = 6.25e8 * P.dt * hr_th_total * r_fth;
+    double f_t_implicit = P.df_implicit * Te_new * rcp_nr_safe(fabs(dT_total));
     if (f_t_implicit > P.df_T) f_t_implicit = P.df_T;
     const double g_thr = 1.0 + 4.0 * Th_e;
     /* dgdt, disp (:880-889, :1035-1049) */
     if (own) {
       const double y = gamma_R * rg_i;
-      const double dg_sy = (y < 100.0) ? -(sy_i * c2d_exp_bf(-y)) : -1.0e-50;
+      const double dg_sy = (y < 100.0) ? -(sy_i * exp_nonpos(-y)) : -1.0e-50;
       f_dgdt[i] = dg_sy + base_i;
     }
     /* loop 350 sums */
@@ -1130,7 +1141,7 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
       /* sum_i (inj_rho prof_i / inj_sum) dg_i is inj_rho to rounding: the
        * fast mode takes it so, without the second block sum */
       const double inj_rho = P.pick_rate * d_t;
-      if (i <= NT - 1) f_fold[i] = f_fold[i] + inj_rho * inj_prof / inj_sum0 / ne;
+      if (i <= NT - 1) f_fold[i] = f_fold[i] + inj_rho * inj_prof * (r_inj0 * rcp_nr(ne));
       n_inject = n_inject + inj_rho;
     }
     if (P.inj_switch != 0) {
@@ -1167,14 +1178,17 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
     ne = ne + n_inject;
     n_p = n_p + n_inject;
     n_lept = n_lept + n_inject;
-    ne = ne * t_esc / (t_esc + d_t);                  /* escape (:1309-1313) */
-    n_p = n_p * t_esc / (t_esc + d_t);
-    n_lept = n_lept * t_esc / (t_esc + d_t);
-    const double dte = d_t / t_esc;
+    const double f_esc = t_esc * rcp_nr(t_esc + d_t);  /* escape (:1309-1313) */
+    ne = ne * f_esc;
+    n_p = n_p * f_esc;
+    n_lept = n_lept * f_esc;
+    const double dte = d_t * r_tesc;
     /* Chang-Cooper coefficients (:1363-1390) */
     if (i <= NT - 1) {
       const double bigB = (i == 1) ? -(f_dgdt[1] + f_dgdt[2]) : -(f_dgdt[i] + f_dgdt[i + 1]) * 0.5;
       const double smw = bigB * kS;
+      /* IEEE divisions kept: exp(smw) - 1 rounds to 0 for |smw| below an ulp, where
+       * x / 0 = inf as in the reference but rcp_nr(0) is NaN */
       f_bigW[i] = smw / (c2d_exp_bf(smw) - 1.0);
       f_em[i] = bigC_i * smw / (1.0 - c2d_exp_bf(-smw));
     }
@@ -1207,10 +1221,11 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
     const double pref = B.scan_sum(pv, tot, sE);      /* one barrier for both */
     sum_p = tot;
     if (i <= NT - 1) f_Pnt[i] = pref;
-    sum_E = sE / sum_p;
+    const double r_sum = rcp_nr(sum_p);
+    sum_E = sE * r_sum;
     t_fp = t_fp + d_t;
     fp_steps = fp_steps + 1;
-    const double fn = own ? u / sum_p : 0.0;
+    const double fn = own ? u * r_sum : 0.0;
     if (own) {
       f_fnew[i] = fn;
       f_fold[i] = fn;
