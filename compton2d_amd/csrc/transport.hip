@@ -1336,8 +1336,22 @@ __device__ __forceinline__ int flight(const KParams& P, const Tal& T, Pkt& p, Co
 /* ------------------------------------------------------------------ */
 /* sources                                                             */
 /* ------------------------------------------------------------------ */
+/* A source being sampled: sub-stream 0 from counter 0, so draw n is output n
+ * of the SplitMix64 sequence seeded with the key (c2d_stream64); `zs` carries
+ * that sequence's state, key + (n + 1)*gamma, and a draw adds gamma instead
+ * of multiplying it by the counter (the same outputs as U(Pkt&)). */
+struct SrcPkt : Pkt {
+  uint64_t zs;
+};
+__device__ __forceinline__ void src_seed(SrcPkt& p) { p.zs = p.key + 0x9E3779B97F4A7C15ull; }
+__device__ __forceinline__ double U(SrcPkt& p) {
+  const uint64_t x = c2d_mix64(p.zs);
+  p.zs += 0x9E3779B97F4A7C15ull;
+  return c2d_u01_bits((uint32_t)(x >> 32), (uint32_t)x);
+}
+
 /* planck (src/planck2d.f:1-141) */
-__device__ __forceinline__ void planck(const KParams& P, const Geo* G, Pkt& p, double tpl) {
+__device__ __forceinline__ void planck(const KParams& P, const Geo* G, SrcPkt& p, double tpl) {
   double u4, ap0, ap1 = 1.0, ap2 = 1.0, ap3 = 1.0, rn1;
   do {
     u4 = U(p);
@@ -1358,7 +1372,7 @@ __device__ __forceinline__ void planck(const KParams& P, const Geo* G, Pkt& p, d
 }
 
 /* file_sample (src/imcsurf2d_para.f:694-788) */
-__device__ __forceinline__ void file_sample(const KParams& P, const Geo* G, Pkt& p, int spec) {
+__device__ __forceinline__ void file_sample(const KParams& P, const Geo* G, SrcPkt& p, int spec) {
   if (spec < 0 || spec >= P.n_spectra) {
     gor(P.err, ERR_SPEC);
     p.xnu = 1.0;
@@ -1379,7 +1393,7 @@ __device__ __forceinline__ void file_sample(const KParams& P, const Geo* G, Pkt&
 }
 
 /* one volume packet of vol_calc (src/imcvol2d_para.f:157-392) */
-__device__ __forceinline__ void vol_source(const KParams& P, const Geo* g, Pkt& p, int jv, int kv) {
+__device__ __forceinline__ void vol_source(const KParams& P, const Geo* g, SrcPkt& p, int jv, int kv) {
   const int cell = (jv - 1) * P.nr + (kv - 1);
   const double* vf = P.vfrac + 4 * cell;
   const double f_thermal = vf[0], f_inn = vf[1], f_outer = vf[2], f_upper = vf[3];
@@ -1460,7 +1474,7 @@ __device__ __forceinline__ void vol_source(const KParams& P, const Geo* g, Pkt& 
 
 /* surface packets: z_surf_calc / r_surf_calc (src/imcsurf2d_para.f:254-528).
  * side 0 inner z-surface js, 1 outer js, 2 upper r-surface ks, 3 lower ks. */
-__device__ __forceinline__ void surf_source(const KParams& P, const Geo* g, Pkt& p, int side, int s1, int slot) {
+__device__ __forceinline__ void surf_source(const KParams& P, const Geo* g, SrcPkt& p, int side, int s1, int slot) {
   const double lim10 = 0.9999999999;
   const double ew = P.surf_ew[slot], tbb = P.surf_tbb[slot];
   const int spec = P.surf_spec[slot];
@@ -1610,26 +1624,43 @@ __global__ void __launch_bounds__(SRCBLOCK) C2D_SFX(c2d_source_kernel)(const KPa
   const int64_t n = P.n_vol_items + P.n_surf_items;
   const int64_t stride = (int64_t)gridDim.x * SRCBLOCK;
   for (int64_t it = (int64_t)blockIdx.x * SRCBLOCK + threadIdx.x; it < n; it += stride) {
-    Pkt p;
+    SrcPkt p;
     p.ctr = 0;
     p.sub = 0;
     if (it < P.n_vol_items) {
       const int64_t gidx = it * P.world + P.rank;
       int cell;
+      int64_t nn;
       if (pref_in_lds) {
-        int lo = 0, hi = P.ncell - 1;       /* upper_index on the LDS copy */
+        /* upper_index on the LDS copy, once per wave for its first active
+         * lane (the smallest gidx: gidx rises with the lane): the other lanes
+         * share that cell unless the wave straddles a cell boundary (a cell
+         * holds ~1e5 or more sources), and then search for themselves */
+        const int64_t gf = (int64_t)rfl64((uint64_t)gidx);
+        int lo = 0, hi = P.ncell - 1;
         while (lo < hi) {
           const int mid = (lo + hi + 1) >> 1;
-          if (pref_lds[mid] <= gidx) lo = mid;
+          if ((int64_t)rfl64((uint64_t)pref_lds[mid]) <= gf) lo = mid;
           else hi = mid - 1;
         }
         cell = lo;
+        if (!(gidx < pref_lds[lo + 1])) {
+          lo = 0; hi = P.ncell - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pref_lds[mid] <= gidx) lo = mid;
+            else hi = mid - 1;
+          }
+          cell = lo;
+        }
+        nn = gidx - pref_lds[cell];
       } else {
         cell = upper_index(P.vol_prefix, P.ncell, gidx);
+        nn = gidx - P.vol_prefix[cell];
       }
-      const int64_t nn = gidx - P.vol_prefix[cell];
       p.key = c2d_derive(P.step_key, C2D_TAG_VOL, (uint32_t)nn, (uint32_t)cell);
       p.bins = 0u;                       /* kap 0: census/volume phase */
+      src_seed(p);
       vol_source(P, g, p, cell / P.nr + 1, cell % P.nr + 1);
     } else {
       const int64_t gidx = (it - P.n_vol_items) * P.world + P.rank;
@@ -1641,6 +1672,7 @@ __global__ void __launch_bounds__(SRCBLOCK) C2D_SFX(c2d_source_kernel)(const KPa
       p.key = c2d_derive(P.step_key, C2D_TAG_SURF + (uint32_t)side, (uint32_t)nn,
                          (uint32_t)(s1 - 1));
       p.bins = 1u << 24;                 /* kap 1: surface phase */
+      src_seed(p);
       surf_source(P, g, p, side, s1, slot);
     }
     p.ctr = 0;   /* a source's own draws are done: its copies use sub-streams */
