@@ -12,7 +12,9 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 B="$ROOT/bench.py --no-cpu-baseline --no-fp-offclamp $*"
-timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum \
+# PMC="..." overrides the counter set (at most 4 TCC_ and 4 TCP_ counters per pass)
+PMC=${PMC:-TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum}
+timeout -k 10 300 rocprofv3 --pmc $PMC \
     --kernel-trace -d "$OUT/cache" -o run --output-format csv -- \
     python3 $B --steps ${STEPS:-3} --warmup ${WARMUP:-1} > "$OUT/bench_cache.json" 2> "$OUT/cache.err"
 python3 - "$OUT/cache" <<'PY'
