@@ -131,6 +131,29 @@ def test_gpu_fp_fast_within_tolerance(name, capsys):
     eng.close()
 
 
+def test_gpu_fp_fast_zero_field_zone(capsys):
+    """A zone with B = 0: the fast kernel's scalar chain multiplies by hoisted
+    reciprocals (fp_fast.hip rcp_nr_safe), whose 1/0 must be inf as the
+    oracle's division has it (the Newton steps alone give NaN), so the zone's
+    synchrotron terms vanish the same way.  Same tolerance as above."""
+    case = FpGoldenCase("fp_pick")
+    n = case.steps[0]
+    fi = dict(case.fp_in(n))
+    fi["B_field"] = fi["B_field"].copy()
+    fi["B_field"][0, 1] = 0.0
+    eng = Engine(case.grid(device=0))
+    eng.fp_set_config(case.constants())
+    eng.fp_set_mode(abi.FP_FAST)
+    g = eng.fp_step(fi["ncycle"], fi["time"], fi["dt"], fi, fi)
+    o = OL.fp_step(case.grid(), case.constants(), fi["ncycle"], fi["time"], fi["dt"], fi, fi,
+                   flavor="det")
+    assert np.all(np.isfinite(o["f_nt"]))
+    dev = fast_vs_oracle(g, o, "fp_pick B=0 zone")
+    with capsys.disabled():
+        print("\nC2D_FP_FAST fp_pick, zone (0,1) at B = 0: %s" % {k: "%.1e" % v for k, v in dev.items()})
+    eng.close()
+
+
 def test_gpu_fp_fast_mcdonald_moment_table(capsys):
     """The fast kernel's McDonald pair from its moment table (fp_fast.hip
     mcd_mtab: 7 moments per series at 1024 grid points per octave of z, the
