@@ -343,6 +343,9 @@ def build_c3(args, rank, world, local, dev, sources, ccap, ecap, mode):
     eng.use_tally_tensor(T)
     ex, ex_desc = tally_exchange(eng, T, rank, world, dev)
     run = CoupledRun(eng, wl, device_resident=not args.host_tables, allreduce=ex)
+    if args.fp_mode == "fast":           # the coupled step's FP update in C2D_FP_FAST
+        from compton2d_amd import abi
+        eng.fp_set_mode(abi.FP_FAST)
     # C3's named output: the step's escapes binned into the observer-frame SED
     # of postprocessing/mrk421_sed.input (pspt.c:245-294) on the device, from
     # the event buffer the transport just wrote (no event text, no download)
@@ -476,6 +479,8 @@ def main():
     ap.add_argument("--grid", type=int, default=32, help="c2/c4 grid (NxN)")
     ap.add_argument("--grid-c5", type=int, default=16, help="c5 grid (NxN)")
     ap.add_argument("--mode", choices=("fast", "exact"), default="fast")
+    ap.add_argument("--fp-mode", choices=("exact", "fast"), default="exact",
+                    help="C3: the coupled step's FP update (exact: bit-identical to the oracle)")
     ap.add_argument("--host-tables", action="store_true",
                     help="c3: move tables/electrons through host arrays every step")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -1355,8 +1355,13 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
 }
 
 __shared__ int f_zone;
+/* workgroups per CU the register budget is sized for (C2D_FPF_MINB 2: <= 256
+ * VGPRs, so two zones share a CU) */
+#ifndef C2D_FPF_MINB
+#define C2D_FPF_MINB 1
+#endif
 template <int BS>
-__global__ void __launch_bounds__(BS) c2d_fp_fast_kernel(const FpParams* __restrict__ Pp) {
+__global__ void __launch_bounds__(BS, C2D_FPF_MINB) c2d_fp_fast_kernel(const FpParams* __restrict__ Pp) {
   const FpParams& P = *Pp;
   Blk<BS> B;
   B.tid = threadIdx.x;
