@@ -1644,6 +1644,17 @@ __global__ void __launch_bounds__(SRCBLOCK) C2D_SFX(c2d_source_kernel)(const KPa
           else hi = mid - 1;
         }
         cell = lo;
+        if (__ballot(!(gidx < pref_lds[lo + 1])) == 0ull) {
+          /* the whole wave in the cell: a wave-uniform cell, so its
+           * constants (volume fractions, weight, bounds, CDF rows) are
+           * scalar loads */
+          const int cu = lo;
+          p.key = c2d_derive(P.step_key, C2D_TAG_VOL, (uint32_t)(gidx - pref_lds[cu]), (uint32_t)cu);
+          p.bins = 0u;                   /* kap 0: census/volume phase */
+          src_seed(p);
+          vol_source(P, g, p, cu / P.nr + 1, cu % P.nr + 1);
+          goto vol_done;
+        }
         if (!(gidx < pref_lds[lo + 1])) {
           lo = 0; hi = P.ncell - 1;
           while (lo < hi) {
@@ -1662,6 +1673,7 @@ __global__ void __launch_bounds__(SRCBLOCK) C2D_SFX(c2d_source_kernel)(const KPa
       p.bins = 0u;                       /* kap 0: census/volume phase */
       src_seed(p);
       vol_source(P, g, p, cell / P.nr + 1, cell % P.nr + 1);
+    vol_done:;
     } else {
       const int64_t gidx = (it - P.n_vol_items) * P.world + P.rank;
       const int slot = upper_index(P.surf_prefix, P.nslot, gidx);
