@@ -216,9 +216,10 @@ def fp_offclamp(device: int, cpu: bool) -> dict:
     reference's fp_pick FP inputs tiled over 30x9 with n_e and tea varied per
     zone, so no two zones share a temperature-search chain (2 391 implicit
     sub-steps per zone).  On fresh contexts, i.e. with an empty gamma_bar
-    memo: the fast mode's first update (zones in index order), a second with
-    the memo emptied again (zones in the measured, costliest-first order) and
-    a third with the memo warm; the exact mode's first update.  The fast mode
+    memo: the fast mode's first update (zones costliest first by the cost
+    probe; the same update in index order without it on a second context), a
+    second with the memo emptied again (zones in the measured, costliest-first
+    order) and a third with the memo warm; the exact mode's first update.  The fast mode
     takes McDonald pairs from its moment table (fp_fast.hip mcd_mtab, built in
     c2d_fp_set_config: config_wall_ms), so a cold memo costs it little.  cpu: the C
     oracle's FP_calc on 8 zones of the same tile, one process each (the
@@ -241,11 +242,24 @@ def fp_offclamp(device: int, cpu: bool) -> dict:
             setup_ms = 1e3 * (time.perf_counter() - t0)
             eng.fp_set_mode(abi.FP_FAST if mode == "fast" else abi.FP_EXACT)
             r = eng.fp_step(*call)
-            leg = {"ms_cold_index_order": eng.last_fp_ms(),
+            leg = {"ms_first_update": eng.last_fp_ms(),
                    "config_wall_ms": setup_ms,
                    "implicit_substeps": float(np.sum(r["zone_diag"][..., 5])),
                    "Te_new_range": [float(r["Te_new"].min()), float(r["Te_new"].max())]}
             if mode == "fast":
+                leg["first_update_order"] = ("costliest first by the cost probe (every zone's first "
+                                             "implicit sub-step, 1/f_t_implicit)")
+                # the same first update without the probe: one workgroup per zone in index order
+                e2 = Engine(g)
+                try:
+                    os.environ["C2D_FPF_PROBE"] = "0"
+                    e2.fp_set_config(c.constants())
+                    e2.fp_set_mode(abi.FP_FAST)
+                    e2.fp_step(*call)
+                    leg["ms_first_update_index_order"] = e2.last_fp_ms()
+                finally:
+                    del os.environ["C2D_FPF_PROBE"]
+                    e2.close()
                 os.environ["C2D_FPF_MEMO_RESET"] = "1"
                 try:
                     eng.fp_step(*call)
@@ -342,10 +356,9 @@ def build_c3(args, rank, world, local, dev, sources, ccap, ecap, mode):
     T = torch.zeros(eng.layout.total, dtype=torch.float64, device=dev)
     eng.use_tally_tensor(T)
     ex, ex_desc = tally_exchange(eng, T, rank, world, dev)
-    run = CoupledRun(eng, wl, device_resident=not args.host_tables, allreduce=ex)
-    if args.fp_mode == "fast":           # the coupled step's FP update in C2D_FP_FAST
-        from compton2d_amd import abi
-        eng.fp_set_mode(abi.FP_FAST)
+    from compton2d_amd import abi
+    fpm = {"auto": abi.FP_AUTO, "exact": abi.FP_EXACT, "fast": abi.FP_FAST}[args.fp_mode]
+    run = CoupledRun(eng, wl, device_resident=not args.host_tables, allreduce=ex, fp_mode=fpm)
     # C3's named output: the step's escapes binned into the observer-frame SED
     # of postprocessing/mrk421_sed.input (pspt.c:245-294) on the device, from
     # the event buffer the transport just wrote (no event text, no download)
@@ -479,8 +492,10 @@ def main():
     ap.add_argument("--grid", type=int, default=32, help="c2/c4 grid (NxN)")
     ap.add_argument("--grid-c5", type=int, default=16, help="c5 grid (NxN)")
     ap.add_argument("--mode", choices=("fast", "exact"), default="fast")
-    ap.add_argument("--fp-mode", choices=("exact", "fast"), default="exact",
-                    help="C3: the coupled step's FP update (exact: bit-identical to the oracle)")
+    ap.add_argument("--fp-mode", choices=("auto", "exact", "fast"), default="auto",
+                    help="C3: the coupled step's FP update (auto: C2D_FP_AUTO, exact while every "
+                         "zone sits on the tea clamp -- C3's steady state -- fast off it; exact: "
+                         "bit-identical to the oracle)")
     ap.add_argument("--host-tables", action="store_true",
                     help="c3: move tables/electrons through host arrays every step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -541,6 +556,13 @@ def main():
     steps_global = sum(r["packet_steps"] for r in rows)
     census_timed_start = rows[0]["census_records"] if rows else census_start
     all_paths = distributed.allreduce_sum(float(sum(r["all_paths"] for r in rows)), dev)
+    # fail loudly: a run that tracked nothing, or whose last step left NaN/Inf
+    # in a tally, is no measurement (the library already refuses non-finite
+    # tables and tallies with C2D_E_NONFINITE; this guards the line itself)
+    last_tallies = eng.tallies_raw()
+    if not (steps_global > 0 and elapsed > 0 and np.isfinite(last_tallies).all()):
+        raise SystemExit("bench: invalid run on rank %d: %g packet-steps in %g s, %d non-finite tallies"
+                         % (rank, steps_global, elapsed, int((~np.isfinite(last_tallies)).sum())))
     if rank != 0:
         eng.close()
         return
@@ -588,7 +610,10 @@ def main():
     if wk == "c3":
         fp_ms = per_step.get("fp_kernel_ms", 0.0)
         ncell = wl.grid.nz * wl.grid.nr
+        modes = [r.get("fp_mode") for r in rows if r.get("fp_mode")]
         kernels["fp"] = {"ms_avg": fp_ms, "zones": ncell,
+                         "mode": args.fp_mode,
+                         "modes_run": {m: modes.count(m) for m in sorted(set(modes))},
                          "bound": "latency: in-order recurrences per zone (SURVEY a15)",
                          "simd_occupancy": pmc.get("fp_simd_occupancy"),
                          "valu_issue_frac": pmc.get("fp_valu_issue_frac"),

@@ -34,12 +34,14 @@ CNT_STEPS, CNT_ESCAPES, CNT_CENSUS, CNT_COLLIDE, CNT_KILLED, CNT_SOURCES, \
     CNT_COMPB, CNT_EVENTS, CNT_GENS, CNT_ABORTED = range(10)
 CNT_ESC_SCAT = 11          # escapes of Compton-scattered packets (imctrk2d(1) copies)
 
-FP_EXACT, FP_FAST = 0, 1   # c2d_fp_set_mode
+FP_EXACT, FP_FAST, FP_AUTO = 0, 1, 2   # c2d_fp_set_mode
+FP_MODE_NAMES = {FP_EXACT: "exact", FP_FAST: "fast", FP_AUTO: "auto"}
 
 ERRORS = {
     0: "C2D_OK", -1: "C2D_E_ARG", -2: "C2D_E_HIP", -3: "C2D_E_CENSUS_OVERFLOW",
     -4: "C2D_E_EVENT_OVERFLOW", -5: "C2D_E_QUEUE_OVERFLOW", -6: "C2D_E_NOMEM",
     -7: "C2D_E_STATE", -8: "C2D_E_FP", -9: "C2D_E_RCCL", -10: "C2D_E_IO",
+    -11: "C2D_E_NONFINITE",
 }
 
 PD = C.POINTER(C.c_double)
@@ -337,6 +339,7 @@ class StepInputs:
 # Fokker-Planck electron update (c2d_fp_config / c2d_fp_step_in / _out)
 # ---------------------------------------------------------------------------
 C2D_E_FP = -8
+C2D_E_NONFINITE = -11
 ERRORS[C2D_E_FP] = "C2D_E_FP"
 FP_E_OLD, FP_E_NEW, FP_HR, FP_HR_ST, FP_DELTA_T, FP_STEPS, FP_SKIPPED = range(7)
 FP_NDIAG = 8

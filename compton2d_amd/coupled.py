@@ -32,7 +32,10 @@ class CoupledRun:
     """Advance a CoupledWorkload one MC step at a time on `eng`."""
 
     def __init__(self, eng: Engine, wl: CoupledWorkload, device_resident: bool = True,
-                 allreduce: Optional[Callable[[], None]] = None):
+                 allreduce: Optional[Callable[[], None]] = None, fp_mode: int = abi.FP_AUTO):
+        """fp_mode: the FP update's arithmetic (Engine.fp_set_mode); the
+        default abi.FP_AUTO picks exact or fast per update, and each step's
+        row logs what ran (`fp_mode`)."""
         self.eng, self.wl = eng, wl
         self.device_resident = device_resident
         self.allreduce = allreduce
@@ -43,6 +46,8 @@ class CoupledRun:
         self.last = {}
         self.fp_on = int(wl.deck.get("T_const", 0)) == 0
         eng.fp_set_config(wl.fp_const)
+        eng.fp_set_mode(fp_mode)
+        self.fp_mode = fp_mode
         L = abi.tally_layout(nz, nr, int(np.asarray(wl.grid.mu).size))
         self._ecens = L["ecens"]
         self._cnt = L["counters"][0]
@@ -83,6 +88,7 @@ class CoupledRun:
         t3 = _time.perf_counter()
         tal = eng.tallies_raw()
         fp_ms = 0.0
+        fp_mode = None
         if self.fp_on and ncycle > 0:
             inputs = dict(wl.fixed, tea=st["tea"], n_e=st["n_e"], B_field=vem["B_field"],
                           Eloss_sy=vem["Eloss_sy"], ec_old=ec_old, ecens=None, n_field=None)
@@ -97,6 +103,7 @@ class CoupledRun:
                 st["f_nt"], st["Pnt"] = new["f_nt"], new["Pnt"]
             self.last_fp = new
             fp_ms = eng.last_fp_ms()
+            fp_mode = abi.FP_MODE_NAMES.get(eng.last_fp_mode())
         t4 = _time.perf_counter()
         o = self._ecens
         self.ecens_prev = tal[o[0]:o[0] + o[1]].reshape(nz, nr).copy()
@@ -106,7 +113,8 @@ class CoupledRun:
         self.last = dict(
             ncycle=ncycle, tables_s=t1 - t0, transport_s=t2 - t1, allreduce_s=t3 - t2, fp_s=t4 - t3,
             step_s=t4 - t0, vem_kernel_ms=eng.last_vem_ms(), transport_gen0_ms=g0_ms,
-            transport_all_ms=all_ms, fp_kernel_ms=fp_ms, packet_steps=float(c[abi.CNT_STEPS]),
+            transport_all_ms=all_ms, fp_kernel_ms=fp_ms, fp_mode=fp_mode,
+            packet_steps=float(c[abi.CNT_STEPS]),
             gen0_steps=float(eng.last_gen0_steps()), gen0_paths=float(g0_paths),
             all_paths=float(all_paths), sources=float(c[abi.CNT_SOURCES]),
             census=float(c[abi.CNT_CENSUS]), escapes=float(c[abi.CNT_ESCAPES]),

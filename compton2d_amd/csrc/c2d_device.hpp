@@ -156,8 +156,22 @@ struct TallyOff {
 #define C2D_COMTAB_U0 (-27.631021115928547)   /* ln(1e-12) */
 #define C2D_COMTAB_U1 (29.933606208922594)    /* ln(1e13)  */
 
+/* fast build (transport.hip TAU_LOG): log(u), u in (0, 1).  Below 1/2:
+ * v_log_f32 of (float)u (|log u| > 0.69, so its absolute error is small
+ * against it); above: log1p(-v) of the
+ * complement v = 1 - u by Kahan's form log(w) * v / (1 - w), w = 1 - v in
+ * f32 (a few f32 ulp however small v is) */
+__device__ __forceinline__ double c2d_tau_log_f32(double u) {
+  const float v = (float)(1.0 - u);
+  const float w = 1.0f - v;
+  const bool lo = u < 0.5;
+  const float lg = 0.69314718f * __builtin_amdgcn_logf(lo ? (float)u : w);
+  const float r = (w == 1.0f) ? -v : lg * (v * __builtin_amdgcn_rcpf(1.0f - w));
+  return (double)(lo ? lg : r);
+}
+
 enum : int32_t {
-  ERR_CENSUS = 1, ERR_EVENT = 2, ERR_QUEUE = 4, ERR_SPEC = 8
+  ERR_CENSUS = 1, ERR_EVENT = 2, ERR_QUEUE = 4, ERR_SPEC = 8, ERR_NONFINITE = 16
 };
 
 /* Explicit global-address-space access for pointers that arrive through
@@ -345,7 +359,7 @@ enum : int32_t {
 };
 /* per-zone output record [ncell][FO_N]: state, then C2D_FP_NDIAG diagnostics */
 enum : int32_t { FO_TE = 0, FO_NE, FO_GMIN, FO_GMAX, FO_AMXWL, FO_PNTH, FO_DIAG = 8, FO_N = 16 };
-enum : int32_t { FPERR_STEPS = 1, FPERR_GUARD = 2 };
+enum : int32_t { FPERR_STEPS = 1, FPERR_GUARD = 2, FPERR_NF_IN = 4, FPERR_NF_OUT = 8 };
 
 /* McDonald abscissa table: n < C2D_FP_MCD_N -> {t_n, ts_n, (ts_n^2-1)^1.5, (ts_n^2-1)^2.5} */
 #define C2D_FP_MCD_N 16384
@@ -393,6 +407,9 @@ struct FpParams {
    * and whether the shared gamma_bar memo is still consulted beside it */
   const double* mom;       /* [C2D_FPF_MT_N][C2D_FPF_MT_W]                    */
   int32_t mt_glob;
+  /* fast kernel: 1 = cost probe, every zone stops after its first implicit
+   * sub-step's f_t_implicit and writes 1/f_t_implicit to its sub-step count */
+  int32_t probe;
 };
 
 /* ---- observer-frame binning (observe.hip) ---- */

@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -223,6 +224,9 @@ struct c2d_ctx {
   double* fpf_mom = nullptr;                 /* fast kernel: McDonald moment table              */
   std::vector<int32_t> fpf_order;            /* zones by the last update's sub-steps, costliest first */
   bool fpf_ordered = false;                  /* fpf_order holds a measured order */
+  /* C2D_FP_AUTO: the next update's choice, from the last update */
+  bool fp_auto_known = false, fp_auto_exact = false;
+  int32_t last_fp_mode = -1;
   float last_fp_ms = 0.f;
   int last_fp_waves = 0;
   /* emission / absorption tables (c2d_volume_em) */
@@ -569,6 +573,29 @@ __global__ void __launch_bounds__(256) c2d_check_monotone(const double* __restri
   }
 }
 
+/* flag |= bit if some a[i], i < n, is NaN or +-Inf.  The fail-loud guard on
+ * tables, tallies and the electron state: the reference carries a NaN on
+ * (NaN counts cast to int, a run that tracks nothing), the library stops. */
+__global__ void __launch_bounds__(256) c2d_check_finite(const double* __restrict__ a, int64_t n, int32_t bit,
+                                                        int32_t* __restrict__ flag) {
+  bool bad = false;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
+    bad |= !(fabs(a[t]) <= DBL_MAX);
+  if (bad) atomicOr(flag, bit);
+}
+
+static void check_finite(c2d_ctx* c, const double* a, int64_t n, int32_t bit, int32_t* flag, hipStream_t st) {
+  if (n <= 0) return;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 4));
+  hipLaunchKernelGGL(c2d_check_finite, dim3(grid), dim3(256), 0, st, a, n, bit, flag);
+}
+
+static bool all_finite(const double* a, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (!std::isfinite(a[i])) return false;
+  return true;
+}
+
 /* guide rows of the emission CDFs (KParams.cdf_guide): row (t, cell), entry q
  * = the smallest i in [1, n] with cdf(i) >= q / C2D_CDF_GUIDE, n if none --
  * cdf_index's own predicate, so its search restricted to [guide[q],
@@ -596,6 +623,8 @@ __global__ void __launch_bounds__(256) c2d_cdf_guide(const double* __restrict__ 
 extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
   if (!c || !in) return C2D_E_ARG;
   HIPCHK(c, hipSetDevice(c->cfg.device));
+  /* a failed c2d_set_step leaves no step to run (tables may be half replaced) */
+  c->have_step = false;
   const int nz = c->nz, nr = c->nr, nc = c->ncell;
   const size_t nvol = (size_t)nc * C2D_N_VOL, nnt = (size_t)nc * C2D_NUM_NT;
   const int dev = in->device_tables;
@@ -617,23 +646,32 @@ extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
                        c->mono_flag);
     hipLaunchKernelGGL(c2d_check_monotone, dim3(grid), dim3(256), 0, st, c->eps_th, nc, C2D_N_VOL,
                        c->mono_flag);
+    check_finite(c, c->kappa_cur, (int64_t)nvol, 2, c->mono_flag, st);
+    check_finite(c, c->eps_tot, (int64_t)nvol, 2, c->mono_flag, st);
+    check_finite(c, c->eps_th, (int64_t)nvol, 2, c->mono_flag, st);
     HIPCHK(c, hipGetLastError());
     int32_t nonmono = 0;
     HIPCHK(c, hipMemcpyAsync(&nonmono, c->mono_flag, sizeof nonmono, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
-    c->eps_linear = nonmono;
+    if (nonmono & 2)
+      return fail(c, C2D_E_NONFINITE, "c2d_set_step: NaN/Inf in the device emission/absorption tables "
+                  "(kappa_tot, eps_tot or eps_th of the last c2d_volume_em)");
+    c->eps_linear = nonmono & 1;
   } else {
     std::vector<double>& h = c->h_stage;
     h.resize(nvol);
     gather3(c, in->kappa_tot, C2D_N_VOL, h.data());
+    if (!all_finite(h.data(), nvol)) return fail(c, C2D_E_NONFINITE, "c2d_set_step: NaN/Inf in kappa_tot");
     HIPCHK(c, hipMemcpy(c->kappa_cur, h.data(), nvol * sizeof(double), hipMemcpyHostToDevice));
     gather3(c, in->eps_tot, C2D_N_VOL, h.data());
+    if (!all_finite(h.data(), nvol)) return fail(c, C2D_E_NONFINITE, "c2d_set_step: NaN/Inf in eps_tot");
     int nonmono = 0;
     for (int cc = 0; cc < nc && !nonmono; cc++)
       for (int i = 1; i < C2D_N_VOL; i++)
         if (!(h[(size_t)cc * C2D_N_VOL + i] >= h[(size_t)cc * C2D_N_VOL + i - 1])) { nonmono = 1; break; }
     HIPCHK(c, hipMemcpy(c->eps_tot, h.data(), nvol * sizeof(double), hipMemcpyHostToDevice));
     gather3(c, in->eps_th, C2D_N_VOL, h.data());
+    if (!all_finite(h.data(), nvol)) return fail(c, C2D_E_NONFINITE, "c2d_set_step: NaN/Inf in eps_th");
     for (int cc = 0; cc < nc && !nonmono; cc++)
       for (int i = 1; i < C2D_N_VOL; i++)
         if (!(h[(size_t)cc * C2D_N_VOL + i] >= h[(size_t)cc * C2D_N_VOL + i - 1])) { nonmono = 1; break; }
@@ -643,8 +681,10 @@ extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
   if (!(dev & C2D_DEV_ELECTRONS)) {
     std::vector<double> hn(nnt);
     gather3(c, in->f_nt, C2D_NUM_NT, hn.data());
+    if (!all_finite(hn.data(), nnt)) return fail(c, C2D_E_NONFINITE, "c2d_set_step: NaN/Inf in f_nt");
     HIPCHK(c, hipMemcpy(c->f_nt, hn.data(), nnt * sizeof(double), hipMemcpyHostToDevice));
     gather3(c, in->Pnt, C2D_NUM_NT, hn.data());
+    if (!all_finite(hn.data(), nnt)) return fail(c, C2D_E_NONFINITE, "c2d_set_step: NaN/Inf in Pnt");
     HIPCHK(c, hipMemcpy(c->Pnt, hn.data(), nnt * sizeof(double), hipMemcpyHostToDevice));
     c->have_electrons = true;
   }
@@ -672,7 +712,18 @@ extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
       vf[4 * cell + 2] = fi + fo;
       vf[4 * cell + 3] = (fi + fo) + fu;
       const int32_t nsv = in->nsv.data ? in->nsv.data[j * in->nsv.s_j + k * in->nsv.s_k] : 0;
-      vp[cell + 1] = vp[cell] + (nsv > 0 ? nsv : 0);
+      /* a negative count is a NaN budget cast to an integer (imcgen2d.f:448-517
+       * on a non-finite Eloss_tot): the reference's `do i=1,nsv` would skip the
+       * zone silently and the run would track nothing */
+      if (nsv < 0)
+        return fail(c, C2D_E_ARG, "c2d_set_step: nsv(%d,%d) = %d < 0 (a non-finite volume budget?)",
+                    j + 1, k + 1, (int)nsv);
+      if (!std::isfinite(ne[cell]))
+        return fail(c, C2D_E_NONFINITE, "c2d_set_step: n_e(%d,%d) is not finite", j + 1, k + 1);
+      if (nsv > 0 && !(std::isfinite(ew[cell]) && std::isfinite(vf[4 * cell]) && std::isfinite(vf[4 * cell + 3])))
+        return fail(c, C2D_E_NONFINITE, "c2d_set_step: zone (%d,%d) emits %d packets with a non-finite "
+                    "weight ewsv or Eloss_th/Eloss_tot", j + 1, k + 1, (int)nsv);
+      vp[cell + 1] = vp[cell] + nsv;
     }
   c->n_vol_global = vp[nc];
   HIPCHK(c, hipMemcpy(c->n_e, ne.data(), nc * sizeof(double), hipMemcpyHostToDevice));
@@ -712,7 +763,11 @@ extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
     }
     if (cnt > 0 && !(tb > 0.0) && (spec < 0 || spec >= in->n_spectra))
       return fail(c, C2D_E_ARG, "surface slot %d emits %d packets but has no spectrum", s, cnt);
-    sp[s + 1] = sp[s] + (cnt > 0 ? cnt : 0);
+    if (cnt < 0) return fail(c, C2D_E_ARG, "surface slot %d: packet count %d < 0", s, (int)cnt);
+    if (cnt > 0 && !(std::isfinite(w) && std::isfinite(tb)))
+      return fail(c, C2D_E_NONFINITE, "surface slot %d emits %d packets with a non-finite weight or "
+                  "temperature", s, (int)cnt);
+    sp[s + 1] = sp[s] + cnt;
     sew[s] = w;
     stb[s] = tb;
     ssp[s] = spec;
@@ -740,6 +795,9 @@ extern "C" int c2d_set_step(c2d_ctx* c, const c2d_step_in* in) {
       const double* src[5] = {s.E_file, s.a1, s.I_file, s.F_file, s.P_file};
       const int len[5] = {s.nfile, s.nfile - 1, s.nfile - 1, s.nfile, s.nfile - 1};
       double* dst[5];
+      for (int f = 0; f < 5; f++)   /* hazard H9: disk/blackbody.in's NaN column */
+        if (!src[f] || !all_finite(src[f], (size_t)len[f]))
+          return fail(c, C2D_E_NONFINITE, "spectrum %d: missing or NaN/Inf table column %d (hazard H9)", m, f);
       for (int f = 0; f < 5; f++) {
         HIPCHK(c, dalloc(&dst[f], (size_t)len[f]));
         HIPCHK(c, hipMemcpy(dst[f], src[f], len[f] * sizeof(double), hipMemcpyHostToDevice));
@@ -1435,8 +1493,12 @@ static int run_step_body(c2d_ctx* c) {
     qin = 1 - qin;              /* this generation's input = last generation's output */
     HIPCHK(c, hipMemsetAsync(c->ctl + CTL_N2, 0, 2 * sizeof(unsigned long long), c->stream));
     const int64_t total = n2 * cfg.split2 + n3 * cfg.split3;
-    for (int64_t b = 0; b < total; b += c->pk.cap) {
-      const int64_t e = std::min<int64_t>(total, b + c->pk.cap);
+    /* secondaries per launch pair: the packet store.  Test knob
+     * C2D_PK_CHUNK: fewer, so a small case runs the chunked loop */
+    int64_t pk_chunk = c->pk.cap;
+    if (const char* e = getenv("C2D_PK_CHUNK")) pk_chunk = std::max<int64_t>(1, std::min<int64_t>(pk_chunk, atoll(e)));
+    for (int64_t b = 0; b < total; b += pk_chunk) {
+      const int64_t e = std::min<int64_t>(total, b + pk_chunk);
       HIPCHK(c, hipMemsetAsync(c->ctl + CTL_NPK, 0, sizeof(unsigned long long), c->stream));
       HIPCHK(c, hipMemsetAsync(c->ctl + CTL_WORK, 0, sizeof(unsigned long long), c->stream));
       GenArgs A = {};
@@ -1517,6 +1579,9 @@ static int run_step_body(c2d_ctx* c) {
     launches++;
   }
   HIPCHK(c, hipEventRecord(c->ev_end, c->stream));
+  /* fail loudly on a NaN/Inf tally (a non-finite table or weight upstream) */
+  check_finite(c, c->T, c->L.total, ERR_NONFINITE, c->derr, c->stream);
+  HIPCHK(c, hipGetLastError());
   unsigned long long ctl[CTL_WORDS];
   int32_t herr = 0;
   HIPCHK(c, hipMemcpyAsync(ctl, c->ctl, sizeof ctl, hipMemcpyDeviceToHost, c->stream));
@@ -1571,6 +1636,8 @@ static int run_step_body(c2d_ctx* c) {
   }
   if (herr & ERR_QUEUE) return fail(c, C2D_E_QUEUE_OVERFLOW, "scatter queue overflow");
   if (herr & ERR_SPEC) return fail(c, C2D_E_ARG, "surface packet without a seed spectrum");
+  if (herr & ERR_NONFINITE)
+    return fail(c, C2D_E_NONFINITE, "NaN/Inf in the step's tallies (edep, n_field, ecens, ...)");
   return C2D_OK;
 }
 
@@ -1923,6 +1990,21 @@ extern "C" int c2d_last_kernel_ms(c2d_ctx* c, double* gen0_ms, double* all_ms, i
 /* the fast kernel's table: every zone off the clamp inserts its own chain
  * values, so it is sized so that probes stay short (16 MB) */
 #define C2D_FPF_MEMO_SLOTS (1u << 20)
+/* *dst = a zeroed device buffer of n T's, published only once zeroed */
+template <typename T>
+static int alloc_zeroed(c2d_ctx* c, T** dst, size_t n) {
+  if (*dst) return C2D_OK;
+  T* p = nullptr;
+  HIPCHK(c, dalloc(&p, n));
+  const hipError_t e = hipMemset(p, 0, sizeof(T) * n);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    HIPCHK(c, e);
+  }
+  *dst = p;
+  return C2D_OK;
+}
+
 static int ensure_mcd(c2d_ctx* c) {
   /* every buffer has its own guard, so a failed allocation is retried by the
    * next call instead of being reported as done with null pointers */
@@ -1951,22 +2033,12 @@ static int ensure_mcd(c2d_ctx* c) {
    * function of Theta); C2D_FP_MEMO=0 disables it (A/B) */
   const char* e = getenv("C2D_FP_MEMO");
   if (!(e && e[0] == '0')) {
-    if (!c->fp_gb_key) {
-      HIPCHK(c, dalloc(&c->fp_gb_key, C2D_FP_MEMO_SLOTS));
-      HIPCHK(c, hipMemset(c->fp_gb_key, 0, sizeof(unsigned long long) * C2D_FP_MEMO_SLOTS));
-    }
-    if (!c->fp_gb_val) {
-      HIPCHK(c, dalloc(&c->fp_gb_val, C2D_FP_MEMO_SLOTS));
-      HIPCHK(c, hipMemset(c->fp_gb_val, 0, sizeof(double) * C2D_FP_MEMO_SLOTS));
-    }
-    if (!c->fpf_gb_key) {
-      HIPCHK(c, dalloc(&c->fpf_gb_key, C2D_FPF_MEMO_SLOTS));
-      HIPCHK(c, hipMemset(c->fpf_gb_key, 0, sizeof(unsigned long long) * C2D_FPF_MEMO_SLOTS));
-    }
-    if (!c->fpf_gb_val) {
-      HIPCHK(c, dalloc(&c->fpf_gb_val, C2D_FPF_MEMO_SLOTS));
-      HIPCHK(c, hipMemset(c->fpf_gb_val, 0, sizeof(double) * C2D_FPF_MEMO_SLOTS));
-    }
+    /* zeroed before they are published: a buffer whose memset failed is
+     * freed, so the next call retries it instead of reading garbage keys */
+    if (int rc = alloc_zeroed(c, &c->fp_gb_key, C2D_FP_MEMO_SLOTS)) return rc;
+    if (int rc = alloc_zeroed(c, &c->fp_gb_val, C2D_FP_MEMO_SLOTS)) return rc;
+    if (int rc = alloc_zeroed(c, &c->fpf_gb_key, C2D_FPF_MEMO_SLOTS)) return rc;
+    if (int rc = alloc_zeroed(c, &c->fpf_gb_val, C2D_FPF_MEMO_SLOTS)) return rc;
   }
   if (!c->fp_dP) HIPCHK(c, dalloc(&c->fp_dP, 1));
   if (!c->fpf_zq) HIPCHK(c, dalloc(&c->fpf_zq, (size_t)c->ncell + 1));
@@ -2025,11 +2097,20 @@ extern "C" int c2d_fp_set_config(c2d_ctx* c, const c2d_fp_config* fc) {
 
 extern "C" int c2d_fp_set_mode(c2d_ctx* c, int32_t mode) {
   if (!c) return C2D_E_ARG;
-  if (mode != C2D_FP_EXACT && mode != C2D_FP_FAST)
-    return fail(c, C2D_E_ARG, "c2d_fp_set_mode: mode %d is neither C2D_FP_EXACT nor C2D_FP_FAST", mode);
+  if (mode != C2D_FP_EXACT && mode != C2D_FP_FAST && mode != C2D_FP_AUTO)
+    return fail(c, C2D_E_ARG, "c2d_fp_set_mode: mode %d is not C2D_FP_EXACT, C2D_FP_FAST or C2D_FP_AUTO", mode);
   c->fp_mode = mode;
   return C2D_OK;
 }
+
+extern "C" int c2d_last_fp_mode(c2d_ctx* c, int32_t* mode) {
+  if (!c || !mode) return C2D_E_ARG;
+  *mode = c->last_fp_mode;
+  return C2D_OK;
+}
+
+/* the reference's tea clamp (src/update2d.f:266-276): temp_min, temp_max */
+static bool on_tea_clamp(double te) { return te >= 1.0e3 || te <= 5.0; }
 
 extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out* out) {
   if (!c || !in || !out) return C2D_E_ARG;
@@ -2082,6 +2163,25 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
           nf[(size_t)cell * C2D_NPHFIELD + ph] =
               in->n_field.data[ph * in->n_field.s_i + j * in->n_field.s_j + k * in->n_field.s_k];
     }
+  /* C2D_FP_AUTO: exact while the last update left every zone on the tea
+   * clamp within a few sub-steps, fast otherwise (include/compton2d.h) */
+  int32_t fm = c->fp_mode;
+  if (fm == C2D_FP_AUTO) {
+    /* the zones' tea as this update starts (the last update's Te_new,
+     * clamped) and the last update's slowest zone */
+    bool exact = !c->fp_auto_known || c->fp_auto_exact;
+    for (int cell = 0; cell < nc; cell++) {
+      const double* z = &zin[(size_t)cell * FZ_N];
+      if (z[FZ_NE] * (1.0 + z[FZ_FPAIR]) < 1.0e-11) continue;   /* skipped (update2d.f:478) */
+      exact = exact && on_tea_clamp(z[FZ_TEA]);
+    }
+    fm = exact ? C2D_FP_EXACT : C2D_FP_FAST;
+  }
+  /* NaN/Inf in what FP_calc reads is C2D_E_FP (the reference would carry it
+   * into f_nt, tea and the next step's tables) */
+  if (!all_finite(zin.data(), zin.size()) || !all_finite(fin.data(), fin.size()) ||
+      !all_finite(pin.data(), pin.size()) || !all_finite(nf.data(), nf.size()))
+    return fail(c, C2D_E_FP, "c2d_fp_step: NaN/Inf in the zone inputs, f_nt/Pnt or n_field");
   const hipStream_t st = c->stream;
   HIPCHK(c, hipMemcpyAsync(c->fp_zin, zin.data(), zin.size() * sizeof(double), hipMemcpyHostToDevice, st));
   if (!el_dev) {
@@ -2120,7 +2220,7 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   P.P_out = c->fp_Pout;
   P.zout = c->fp_zout; P.err = c->fp_err;
   P.gb_key = c->fp_gb_key; P.gb_val = c->fp_gb_val; P.gb_mask = C2D_FP_MEMO_SLOTS - 1u;
-  if (c->fp_mode == C2D_FP_FAST) {
+  if (fm == C2D_FP_FAST) {
     if (!c->fp_dP || !c->fpf_zq || !c->fp_mcd)
       return fail(c, C2D_E_STATE, "c2d_fp_step: the fast kernel's buffers are not allocated");
     P.gb_key = c->fpf_gb_key; P.gb_val = c->fpf_gb_val; P.gb_mask = C2D_FPF_MEMO_SLOTS - 1u;
@@ -2146,22 +2246,65 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
     }
     HIPCHK(c, hipMemcpyAsync(c->fp_dP, &P, sizeof P, hipMemcpyHostToDevice, st));
   }
+  /* the device-resident inputs: this step's n_field/ecens tallies, f_nt/Pnt */
+  if (nf_dev) check_finite(c, P.nf, (int64_t)nc * C2D_NPHFIELD, FPERR_NF_IN, c->fp_err, st);
+  if (ecens_dev) check_finite(c, P.ecens, nc, FPERR_NF_IN, c->fp_err, st);
+  if (el_dev) {
+    check_finite(c, c->f_nt, (int64_t)nc * C2D_NUM_NT, FPERR_NF_IN, c->fp_err, st);
+    check_finite(c, c->Pnt, (int64_t)nc * C2D_NUM_NT, FPERR_NF_IN, c->fp_err, st);
+  }
+  HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev_g0a, st));
   int rc;
-  if (c->fp_mode == C2D_FP_FAST) {
+  if (fm == C2D_FP_FAST) {
     const int bs = c2d_fp_fast_block(nc, 4 * c->n_cu);
     /* before any order is known: every zone at once (one workgroup each) */
     const char* ge = getenv("C2D_FPF_GRID");
     int grid = ge ? atoi(ge) : (c->fpf_ordered ? c->n_cu : 0);
     if (grid <= 0) grid = (int)nc;
     c->last_fp_waves = bs / 64;
-    rc = c2d_launch_fp_fast(c->fp_dP, nc, bs, grid, st);
+    /* no measured zone order yet: a cost probe first (every zone's first
+     * implicit sub-step, one workgroup each), then the queue costliest first
+     * by the 1/f_t_implicit it implies (C2D_FPF_PROBE=0: index order) */
+    const char* pe = getenv("C2D_FPF_PROBE");
+    rc = 0;
+    if (!c->fpf_ordered && !ge && !(pe && pe[0] == '0')) {
+      FpParams Pp = P;
+      Pp.probe = 1;
+      Pp.zorder = nullptr;
+      HIPCHK(c, hipMemcpyAsync(c->fp_dP, &Pp, sizeof Pp, hipMemcpyHostToDevice, st));
+      HIPCHK(c, hipMemsetAsync(c->fpf_zq, 0, sizeof(int32_t), st));
+      rc = c2d_launch_fp_fast(c->fp_dP, nc, bs, nc, st);
+      if (!rc) {
+        std::vector<double> est((size_t)nc * FO_N);
+        HIPCHK(c, hipMemcpyAsync(est.data(), c->fp_zout, est.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        std::vector<int32_t>& o = c->fpf_order;
+        for (int q = 0; q < nc; q++) o[q] = q;
+        auto cost = [&](int32_t z) {
+          const double v = est[(size_t)z * FO_N + FO_DIAG + C2D_FP_STEPS];
+          return (v == v) ? v : 0.0;
+        };
+        std::stable_sort(o.begin(), o.end(), [&](int32_t a, int32_t b) { return cost(a) > cost(b); });
+        HIPCHK(c, hipMemcpyAsync(c->fpf_zq + 1, o.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        HIPCHK(c, hipMemsetAsync(c->fpf_zq, 0, sizeof(int32_t), st));
+        HIPCHK(c, hipMemcpyAsync(c->fp_dP, &P, sizeof P, hipMemcpyHostToDevice, st));
+        HIPCHK(c, hipStreamSynchronize(st));    /* the host vectors above go out of scope */
+        grid = c->n_cu;
+      }
+    }
+    if (!rc) rc = c2d_launch_fp_fast(c->fp_dP, nc, bs, grid, st);
   } else {
     c->last_fp_waves = c2d_fp_waves(nc, 4 * c->n_cu);
     rc = c2d_launch_fp(&P, nc, c->last_fp_waves, st);
   }
   if (rc) return fail(c, C2D_E_HIP, "fp launch: %s", hipGetErrorString((hipError_t)rc));
   HIPCHK(c, hipEventRecord(c->ev_g0b, st));
+  if (el_dev) {   /* staging rows (seeded with the state: skipped zones too) */
+    check_finite(c, c->fp_fout, (int64_t)nc * C2D_NUM_NT, FPERR_NF_OUT, c->fp_err, st);
+    check_finite(c, c->fp_Pout, (int64_t)nc * C2D_NUM_NT, FPERR_NF_OUT, c->fp_err, st);
+    HIPCHK(c, hipGetLastError());
+  }
   std::vector<double> zout((size_t)nc * FO_N), fout(nnt), pout(nnt);
   std::vector<double> ecd(ecens_dev ? nc : 0);
   int32_t herr = 0;
@@ -2176,12 +2319,36 @@ extern "C" int c2d_fp_step(c2d_ctx* c, const c2d_fp_step_in* in, c2d_fp_step_out
   if (herr & FPERR_STEPS)
     return fail(c, C2D_E_FP, "FP sub-step limit exceeded (reference stops, update2d.f:585-599)");
   if (herr & FPERR_GUARD) return fail(c, C2D_E_FP, "FP temperature/McDonald iteration guard tripped");
-  if (c->fp_mode == C2D_FP_FAST) {      /* next update's queue order: most sub-steps first */
+  if (herr & FPERR_NF_IN)
+    return fail(c, C2D_E_FP, "c2d_fp_step: NaN/Inf in the device n_field/ecens tallies or electron state");
+  if (herr & FPERR_NF_OUT) return fail(c, C2D_E_FP, "c2d_fp_step: the update produced NaN/Inf in f_nt/Pnt");
+  for (int cell = 0; cell < nc; cell++) {   /* skipped zones write Te only */
+    const double* zo = &zout[(size_t)cell * FO_N];
+    bool ok = std::isfinite(zo[FO_TE]);
+    if (zo[FO_DIAG + C2D_FP_SKIPPED] == 0.0) {
+      ok = ok && all_finite(zo, FO_PNTH + 1) && all_finite(zo + FO_DIAG, C2D_FP_NDIAG);
+      if (!el_dev)
+        ok = ok && all_finite(&fout[(size_t)cell * C2D_NUM_NT], C2D_NUM_NT) &&
+             all_finite(&pout[(size_t)cell * C2D_NUM_NT], C2D_NUM_NT);
+    }
+    if (!ok) return fail(c, C2D_E_FP, "c2d_fp_step: the update of zone %d produced NaN/Inf", cell);
+  }
+  {   /* next fast update's queue order: most sub-steps first (either kernel counts them) */
     std::vector<int32_t>& o = c->fpf_order;
     std::stable_sort(o.begin(), o.end(), [&](int32_t a, int32_t b) {
       return zout[(size_t)a * FO_N + FO_DIAG + C2D_FP_STEPS] > zout[(size_t)b * FO_N + FO_DIAG + C2D_FP_STEPS];
     });
     c->fpf_ordered = true;
+  }
+  {   /* C2D_FP_AUTO: the slowest zone's sub-steps, for the next choice */
+    double max_steps = 0.0;
+    for (int cell = 0; cell < nc; cell++) {
+      const double* zo = &zout[(size_t)cell * FO_N];
+      if (zo[FO_DIAG + C2D_FP_SKIPPED] == 0.0) max_steps = std::max(max_steps, zo[FO_DIAG + C2D_FP_STEPS]);
+    }
+    c->fp_auto_known = true;
+    c->fp_auto_exact = max_steps <= (double)C2D_FP_AUTO_STEPS;
+    c->last_fp_mode = fm;
   }
   if (el_dev) {
     HIPCHK(c, hipMemcpyAsync(c->f_nt, c->fp_fout, nt_bytes, hipMemcpyDeviceToDevice, st));
@@ -2315,6 +2482,9 @@ extern "C" int c2d_volume_em(c2d_ctx* c, const c2d_vem_in* in, c2d_vem_out* out)
       for (int i = 0; i < C2D_NUM_NT && !el_dev; i++)
         fnt[cell * C2D_NUM_NT + i] = in->f_nt.data[i * in->f_nt.s_i + j * in->f_nt.s_j + k * in->f_nt.s_k];
     }
+  if (!all_finite(zin.data(), zin.size()) || !all_finite(fnt.data(), el_dev ? 0 : fnt.size()))
+    return fail(c, C2D_E_NONFINITE, "c2d_volume_em: NaN/Inf in the zone inputs or f_nt");
+  c->have_vem = false;
   const hipStream_t st = c->stream;
   HIPCHK(c, hipMemcpyAsync(c->vem_zin, zin.data(), zin.size() * sizeof(double), hipMemcpyHostToDevice, st));
   if (!el_dev)
@@ -2328,6 +2498,16 @@ extern "C" int c2d_volume_em(c2d_ctx* c, const c2d_vem_in* in, c2d_vem_out* out)
   int rc = c2d_launch_vem(&P, (int)nc, st);
   if (rc) return fail(c, C2D_E_HIP, "vem launch: %s", hipGetErrorString((hipError_t)rc));
   HIPCHK(c, hipEventRecord(c->ev_g0b, st));
+  /* NaN/Inf in the device electron state read, or in the tables written */
+  if (!c->mono_flag) HIPCHK(c, dalloc(&c->mono_flag, 1));
+  HIPCHK(c, hipMemsetAsync(c->mono_flag, 0, sizeof(int32_t), st));
+  if (el_dev) check_finite(c, c->f_nt, (int64_t)nc * C2D_NUM_NT, 1, c->mono_flag, st);
+  check_finite(c, c->vem_kap, (int64_t)nc * C2D_N_VOL, 2, c->mono_flag, st);
+  check_finite(c, c->vem_et, (int64_t)nc * C2D_N_VOL, 2, c->mono_flag, st);
+  check_finite(c, c->vem_eh, (int64_t)nc * C2D_N_VOL, 2, c->mono_flag, st);
+  HIPCHK(c, hipGetLastError());
+  int32_t vflag = 0;
+  HIPCHK(c, hipMemcpyAsync(&vflag, c->mono_flag, sizeof vflag, hipMemcpyDeviceToHost, st));
   /* tables cross to the host only for the output views that are present */
   std::vector<double> kap(out->kappa_tot.data ? nc * C2D_N_VOL : 0),
       et(out->eps_tot.data ? nc * C2D_N_VOL : 0), eh(out->eps_th.data ? nc * C2D_N_VOL : 0), zo(nc * VO_N);
@@ -2340,6 +2520,12 @@ extern "C" int c2d_volume_em(c2d_ctx* c, const c2d_vem_in* in, c2d_vem_out* out)
   HIPCHK(c, hipMemcpyAsync(zo.data(), c->vem_zout, zo.size() * sizeof(double), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   (void)hipEventElapsedTime(&c->last_vem_ms, c->ev_g0a, c->ev_g0b);
+  if (vflag & 1) return fail(c, C2D_E_NONFINITE, "c2d_volume_em: NaN/Inf in the device f_nt");
+  bool zo_ok = true;
+  for (size_t cell = 0; cell < nc; cell++) zo_ok = zo_ok && all_finite(&zo[cell * VO_N], VO_ETOT + 1);
+  if ((vflag & 2) || !zo_ok)
+    return fail(c, C2D_E_NONFINITE, "c2d_volume_em: NaN/Inf in the emission/absorption tables or "
+                "Eloss outputs (volume2d.f:343-390)");
   c->have_vem = true;
   if (out->E_ph) std::copy(eph.begin(), eph.end(), out->E_ph);
   auto put3 = [&](c2d_marray3& m, const std::vector<double>& v, size_t cell, int j, int k) {

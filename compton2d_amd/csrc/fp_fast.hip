@@ -1101,6 +1101,13 @@ __device__ __forceinline__ void fp_zone_fast(const FpParams& P, Blk<BS>& B, cons
     const double dT_total = 6.25e8 * P.dt * hr_th_total * r_fth;
     double f_t_implicit = P.df_implicit * Te_new * rcp_nr_safe(fabs(dT_total));
     if (f_t_implicit > P.df_T) f_t_implicit = P.df_T;
+    if (P.probe) {   /* cost probe: the sub-steps this first one implies (:1142, :1473) */
+      if (tid == 0) {
+        zo[FO_DIAG + C2D_FP_STEPS] = 1.0 / f_t_implicit;
+        zo[FO_DIAG + C2D_FP_SKIPPED] = 0.0;
+      }
+      return;
+    }
     const double g_thr = 1.0 + 4.0 * Th_e;
     /* dgdt, disp (:880-889, :1035-1049) */
     if (own) {

@@ -8,6 +8,7 @@
 
 #include <vector>
 
+#include "c2d_device.hpp"
 #include "c2d_math.h"
 #include "c2d_rng.h"
 #include "c2d_wave.hpp"
@@ -42,6 +43,8 @@ __global__ void c2d_selftest_math_kernel(int fn, const double* x, double* y, int
       r = q * __builtin_fma(-0.5 * v, q * q, 1.5);
       break;
     }
+    /* the fast build's optical depth log (transport.hip TAU_LOG) */
+    case 14: r = c2d_tau_log_f32(v); break;
     default: r = c2d_draw((uint64_t)(int64_t)v, (uint32_t)i); break;
   }
   y[i] = r;

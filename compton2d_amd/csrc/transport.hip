@@ -130,9 +130,13 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 #define C2D_PT_F32 1
 #endif
 /* fast build: the probe bundle's optical depth to its next collision,
- * tau = -log(u)/n, with v_log_f32 (C2D_TAU_F32=1; 0: the f64 log).  tau only
- * decides where the exponential collision process puts the next collision,
- * so a ~1e-7 relative error leaves the process's statistics unchanged */
+ * tau = -log(u)/n, in f32 (C2D_TAU_F32=1; 0: the f64 log) to ~2e-7 relative
+ * for every u (tau_log_f32).  tau only decides where the exponential
+ * collision process puts the next collision, so that error leaves the
+ * process's statistics unchanged.  In an optically thin medium a collision
+ * needs u within ~1e-5 of 1: there (float)u would keep only 1-u to 6e-8
+ * absolute (1e-3 relative in tau, and tau = 0 for u > 1 - 2^-25), so the
+ * tail is taken from the complement 1 - u, exact in f64 */
 #ifndef C2D_TAU_F32
 #define C2D_TAU_F32 1
 #endif
@@ -144,7 +148,7 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 #define C2D_LNX_F32 1
 #endif
 #if C2D_TABLE_COMTOT && C2D_TAU_F32
-#define TAU_LOG(u) ((double)(0.69314718f * __builtin_amdgcn_logf((float)(u))))
+#define TAU_LOG(u) c2d_tau_log_f32(u)
 #else
 #define TAU_LOG(u) FLOG(u)
 #endif

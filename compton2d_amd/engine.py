@@ -118,6 +118,8 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_fp_step.argtypes = [vp, C.POINTER(abi.FpStepIn), C.POINTER(abi.FpStepOut)]
     lib.c2d_fp_set_mode.restype = C.c_int
     lib.c2d_fp_set_mode.argtypes = [vp, C.c_int32]
+    lib.c2d_last_fp_mode.restype = C.c_int
+    lib.c2d_last_fp_mode.argtypes = [vp, C.POINTER(C.c_int32)]
     lib.c2d_last_fp_ms.restype = C.c_int
     lib.c2d_last_fp_ms.argtypes = [vp, C.POINTER(C.c_double)]
     lib.c2d_volume_em.restype = C.c_int
@@ -355,10 +357,18 @@ class Engine:
         self._check(self.lib.c2d_fp_set_config(self.ctx, C.byref(self._fpc)))
 
     def fp_set_mode(self, mode: int) -> None:
-        """abi.FP_EXACT (bit for bit the reference order, default) or
+        """abi.FP_EXACT (bit for bit the reference order, default),
         abi.FP_FAST (block-parallel sums, PCR tridag, tree-summed McDonald
-        series: equal within rounding; include/compton2d.h c2d_fp_set_mode)."""
+        series: equal within rounding) or abi.FP_AUTO (per update: exact while
+        every zone sits on the tea clamp within a few sub-steps, fast
+        otherwise); include/compton2d.h c2d_fp_set_mode."""
         self._check(self.lib.c2d_fp_set_mode(self.ctx, int(mode)))
+
+    def last_fp_mode(self) -> int:
+        """abi.FP_EXACT or abi.FP_FAST: what the last fp_step ran (-1: none yet)."""
+        m = C.c_int32()
+        self._check(self.lib.c2d_last_fp_mode(self.ctx, C.byref(m)))
+        return m.value
 
     def fp_step(self, ncycle: int, time: float, dt: float, inputs: dict, state: dict) -> dict:
         """One `update` (src/update2d.f:7-327) on the GPU; returns the new state.

@@ -196,6 +196,15 @@ def volume_budget(nst: int, fas: np.ndarray):
     fas = np.ascontiguousarray(fas, np.float64)
     nz, nr = fas.shape
     emiss_tot = float(np.cumsum(fas.ravel())[-1]) if fas.size else 0.0
+    # the reference casts a NaN budget to an integer (a negative count: the
+    # zone's `do i=1,nsv` loop is skipped and the run tracks nothing)
+    if not (np.isfinite(fas).all() and np.isfinite(emiss_tot)):
+        bad = np.argwhere(~np.isfinite(fas))
+        raise FloatingPointError("volume_budget: non-finite emission (Eloss_tot) in %d zone(s), first "
+                                 "(j, k) = %s; Emiss_tot = %r" % (len(bad), tuple(int(x) + 1 for x in bad[0])
+                                                                  if len(bad) else None, emiss_tot))
+    if (fas < 0).any():
+        raise ValueError("volume_budget: negative emission in %d zone(s)" % int((fas < 0).sum()))
     if emiss_tot == 0.0:
         return np.zeros((nz, nr), np.int32), np.zeros((nz, nr))
     half = 0.5 * float(nst)

@@ -47,7 +47,8 @@ c     C2D_SHIM_SED=0 (no on-device SED),
 c     C2D_SHIM_EVENTS=1 (also write the event file),
 c     C2D_SHIM_CENSUS_MIRROR=1|0 (dbufout mirror every step | never;
 c     default: only near write_record's elapsed-time mark),
-c     C2D_SHIM_FP_FAST=1 (the fast FP mode, c2d_fp_set_mode),
+c     C2D_SHIM_FP_MODE=0|1|2 (exact | fast | auto FP, default auto,
+c     c2d_fp_set_mode), C2D_SHIM_FP_FAST=1 (= C2D_SHIM_FP_MODE=1),
 c     C2D_SHIM_ALLREDUCE=0 (N workers: no all-reduce inside the C-ABI;
 c     every worker deposits its own tallies into COMMON instead).
 c     Errors print the library's message and MPI_ABORT (the reference
@@ -730,6 +731,7 @@ c     around it (cens_add_up, E_add_up, FP_end_bcast) are kept
       type(c2d_fp_step_in) :: fpi
       type(c2d_fp_step_out) :: fpo
       integer(c_int) rc
+      integer(c_int32_t) fpmode
       integer(c_int64_t) s1, sj, sk
       integer*8 c2d_shim_env
 
@@ -780,13 +782,17 @@ c     edep, ecens, n_field of all workers -> master (update2d.f:1929)
             rc = c2d_fp_set_config(fctx, fcfg)
             if (rc .ne. C2D_OK) call c2d_shim_fail(fctx,
      1           'c2d_fp_set_config', rc)
-c           C2D_SHIM_FP_FAST=1: the block-parallel FP (within its stated
-c           tolerance of the reference order, include/compton2d.h)
-            if (c2d_shim_env('C2D_SHIM_FP_FAST', 0_8) .eq. 1) then
-               rc = c2d_fp_set_mode(fctx, C2D_FP_FAST)
-               if (rc .ne. C2D_OK) call c2d_shim_fail(fctx,
-     1              'c2d_fp_set_mode', rc)
-            endif
+c           FP arithmetic: C2D_FP_AUTO by default (exact while every
+c           zone sits on the tea clamp, the block-parallel fast mode off
+c           it, include/compton2d.h); C2D_SHIM_FP_MODE=0|1|2 picks exact,
+c           fast or auto; C2D_SHIM_FP_FAST=1 is fast
+            fpmode = int(c2d_shim_env('C2D_SHIM_FP_MODE',
+     1           int(C2D_FP_AUTO, 8)), c_int32_t)
+            if (c2d_shim_env('C2D_SHIM_FP_FAST', 0_8) .eq. 1)
+     1           fpmode = C2D_FP_FAST
+            rc = c2d_fp_set_mode(fctx, fpmode)
+            if (rc .ne. C2D_OK) call c2d_shim_fail(fctx,
+     1           'c2d_fp_set_mode', rc)
             fready = .true.
          endif
 c        zone arrays in place: (j, k) of (jmax, kmax); the electron

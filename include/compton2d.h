@@ -61,9 +61,14 @@ extern "C" {
 #define C2D_E_NOMEM            -6
 #define C2D_E_STATE            -7   /* call order violated                        */
 #define C2D_E_FP               -8   /* FP sub-step limit (reference `stop`,
-                                       src/update2d.f:585-599) or a solver guard  */
+                                       src/update2d.f:585-599), a solver guard,
+                                       or NaN/Inf in n_field, ecens or the
+                                       updated electron state                     */
 #define C2D_E_RCCL             -9   /* RCCL (communicator / all-reduce) error     */
 #define C2D_E_IO              -10   /* a file could not be written                */
+#define C2D_E_NONFINITE       -11   /* NaN/Inf in a table, a tally or an emission
+                                       output (the reference would carry it on:
+                                       NaN counts, a collapsed run)               */
 
 /* comtot (src/comtot2d.f:1-334, icoms=6) evaluation mode. */
 #define C2D_COMTOT_EXACT  0   /* 199-term electron-spectrum sum per call (reference)   */
@@ -432,10 +437,28 @@ int  c2d_fp_step(c2d_ctx* ctx, const c2d_fp_step_in* in, c2d_fp_step_out* out);
  *     reductions/scans, tridag by parallel cyclic reduction, McDonald's terms
  *     summed as a tree (the same terms: the reference's stopping index) --
  *     equal to the exact mode within rounding (DESIGN.md §4b states the
- *     tolerance: f_nt 1e-10 relative, Te_new on the same 1.005 lattice). */
+ *     tolerance: f_nt 1e-10 relative, Te_new on the same 1.005 lattice);
+ *   C2D_FP_AUTO: per update, C2D_FP_EXACT when every zone's tea sits on the
+ *     reference's clamp (tea <= temp_min = 5 or >= temp_max = 1000 keV, the
+ *     last update's Te_new clamped, src/update2d.f:266-276; skipped zones
+ *     aside) and the last update's slowest zone took <= C2D_FP_AUTO_STEPS
+ *     implicit sub-steps (src/update2d.f:1473; no last update: not asked):
+ *     the exact kernel's in-order chain is then short (C3: 5 sub-steps,
+ *     1.1 ms against the fast kernel's 3.4 ms); C2D_FP_FAST otherwise (off
+ *     the clamp: ~29 ms against ~380 ms).  c2d_last_fp_mode reports it.
+ * A fast update with no measured zone order yet (the context's first update;
+ * either kernel's sub-step counts order the next) takes the zones costliest
+ * first by an a-priori estimate: a probe launch evaluates every zone's first
+ * implicit sub-step and orders the zones by 1/f_t_implicit (the sub-steps it
+ * implies, src/update2d.f:662-665). */
 #define C2D_FP_EXACT 0
 #define C2D_FP_FAST  1
+#define C2D_FP_AUTO  2
+#define C2D_FP_AUTO_STEPS 64
 int  c2d_fp_set_mode(c2d_ctx* ctx, int32_t mode);
+/* The arithmetic the last c2d_fp_step used (C2D_FP_EXACT or C2D_FP_FAST:
+ * C2D_FP_AUTO's choice); -1 before the first update. */
+int  c2d_last_fp_mode(c2d_ctx* ctx, int32_t* mode);
 
 /* Device timing of the last step's dominant kernel (transport generation 0):
  * milliseconds and launches, measured with HIP events on the library's

@@ -12,10 +12,11 @@ module compton2d
 
   integer(c_int), parameter :: C2D_OK = 0, C2D_E_ARG = -1, C2D_E_HIP = -2, &
        C2D_E_CENSUS_OVERFLOW = -3, C2D_E_EVENT_OVERFLOW = -4, C2D_E_QUEUE_OVERFLOW = -5, &
-       C2D_E_NOMEM = -6, C2D_E_STATE = -7, C2D_E_FP = -8, C2D_E_RCCL = -9, C2D_E_IO = -10
+       C2D_E_NOMEM = -6, C2D_E_STATE = -7, C2D_E_FP = -8, C2D_E_RCCL = -9, C2D_E_IO = -10, &
+       C2D_E_NONFINITE = -11
   ! c2d_step_in%device_tables flags; RCCL unique-id size (c2d_comm_unique_id)
   integer(c_int32_t), parameter :: C2D_DEV_EMISSION = 1, C2D_DEV_ELECTRONS = 2
-  integer(c_int32_t), parameter :: C2D_FP_EXACT = 0, C2D_FP_FAST = 1
+  integer(c_int32_t), parameter :: C2D_FP_EXACT = 0, C2D_FP_FAST = 1, C2D_FP_AUTO = 2
   integer, parameter :: C2D_COMM_ID_BYTES = 128
   integer(c_int32_t), parameter :: C2D_COMTOT_EXACT = 0, C2D_COMTOT_TABLE = 1
   integer(c_int32_t), parameter :: C2D_TRK_SRC = 0, C2D_TRK_2012_11 = 1
@@ -252,11 +253,18 @@ module compton2d
      end function c2d_fp_set_config
 
      ! C2D_FP_EXACT (default, bit for bit the reference order) | C2D_FP_FAST
+     ! | C2D_FP_AUTO (per update: exact on the tea clamp, fast off it)
      integer(c_int) function c2d_fp_set_mode(ctx, mode) bind(C, name='c2d_fp_set_mode')
        import :: c_int, c_ptr, c_int32_t
        type(c_ptr), value :: ctx
        integer(c_int32_t), value :: mode
      end function c2d_fp_set_mode
+
+     integer(c_int) function c2d_last_fp_mode(ctx, mode) bind(C, name='c2d_last_fp_mode')
+       import :: c_int, c_ptr, c_int32_t
+       type(c_ptr), value :: ctx
+       integer(c_int32_t), intent(out) :: mode
+     end function c2d_last_fp_mode
 
      integer(c_int) function c2d_fp_step(ctx, fin, fout) bind(C, name='c2d_fp_step')
        import :: c_int, c_ptr, c2d_fp_step_in, c2d_fp_step_out

@@ -211,7 +211,14 @@ int c2d_fp_set_config(c2d_ctx* c, const c2d_fp_config* fc) {
 
 /* the oracle has one FP arithmetic (the reference's order): either mode maps to it */
 int c2d_fp_set_mode(c2d_ctx* c, int32_t mode) {
-  if (!c || (mode != C2D_FP_EXACT && mode != C2D_FP_FAST)) return C2D_E_ARG;
+  if (!c || (mode != C2D_FP_EXACT && mode != C2D_FP_FAST && mode != C2D_FP_AUTO)) return C2D_E_ARG;
+  return C2D_OK;
+}
+
+/* the stand-in always runs the oracle's FP_calc (the exact arithmetic) */
+int c2d_last_fp_mode(c2d_ctx* c, int32_t* mode) {
+  if (!c || !mode) return C2D_E_ARG;
+  *mode = C2D_FP_EXACT;
   return C2D_OK;
 }
 

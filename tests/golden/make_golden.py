@@ -33,6 +33,21 @@ sys.path.insert(0, str(ROOT / "tests"))
 
 import refcase  # noqa: E402
 
+# src_20121026/input.dat:113-116
+PROD_SPLITS = dict(split1=1000, split2=1000, split3=300, spl3_trg=10)
+
+
+def _c3_transport(nst: int) -> dict:
+    """The C3 deck (compton2d_amd/synth.py C3_DECK) with T_const = 1: the
+    transport inputs and tallies only (no FP_calc between steps)."""
+    from compton2d_amd import synth
+    d = synth.c3_refcase(nst=nst)
+    d["T_const"] = 1
+    for k in PROD_SPLITS:
+        d.pop(k)
+    return d
+
+
 CASES = {
     # optically thicker SSC blob: collisions, split2/split3, census, escapes
     "ssc_tau": dict(case=dict(nz=2, nr=2, n_e=4.0e6, nst=2000), nsteps=3),
@@ -65,6 +80,17 @@ CASES = {
     # (collisions, split3, census) and grid3x4's (12 cells, 2 angular bins)
     "ssc_tau_2012": dict(case=dict(nz=2, nr=2, n_e=4.0e6, nst=2000), nsteps=3, trk_variant=1),
     "grid3x4_2012": dict(case=dict(nz=3, nr=4, n_e=1.0e6, nst=1500, nmu=2), nsteps=2, trk_variant=1),
+    # the production splits of the C3 deck (src_20121026/input.dat:113-116:
+    # split1/2/3 = 1000/1000/300, spl3_trg = 10; SURVEY.md §8(d) "parity run").
+    # C3's 30x9 grid and inputm.dat medium, FP off: the optically thin case,
+    # where every source is 1000 probes (src/imctrk2d.f:105-138) -- on the GPU
+    # 32 bundle restarts of up to 32 probes each (transport.hip bundle_begin)
+    "prod_c3": dict(case=dict(PROD_SPLITS, **_c3_transport(nst=6000)), nsteps=2),
+    # the same splits in a medium where split1 probes collide: n_e = 1e5
+    # (tau_T ~ 5e-4, so 1000 probes see ~0.5 collisions per source and every
+    # collision fans out to 1000 secondaries, src/imctrk2d.f:584-704; split3
+    # fires on the gmax = 1e5 tail's >1e7 gains)
+    "prod_dense": dict(case=dict(PROD_SPLITS, nz=2, nr=2, n_e=1.0e5, nst=60), nsteps=2),
 }
 
 # C3: the Mrk 421 SSC deck src_20121026/input.dat:1-130 +

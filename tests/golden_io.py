@@ -11,7 +11,7 @@ from compton2d_amd import abi
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
 CASES = ("ssc_tau", "ec_lower", "grid3x4", "ec_upper", "bb_upper", "c3_mrk421", "c1_ec1x1",
-         "c2_32x32", "ssc_tau_2012", "grid3x4_2012")
+         "c2_32x32", "ssc_tau_2012", "grid3x4_2012", "prod_c3", "prod_dense")
 IN_KEYS = ("kappa_tot", "eps_tot", "eps_th", "f_nt", "Pnt", "n_e", "Eloss_th", "Eloss_tot",
            "zsurf", "ewsv", "nsv", "nsurfi", "nsurfo", "ewsurfi", "ewsurfo", "nsurfu", "nsurfl",
            "ewsurfu", "ewsurfl", "tbbi", "tbbo", "tbbu", "tbbl")

@@ -183,3 +183,71 @@ def test_gpu_c3_fp_fast_within_tolerance():
             assert d <= 1e-10, (n, k, d)
         np.testing.assert_array_equal(g["Te_new"], gc.fp_out(n)["Te_new"])
     eng.close()
+
+
+def _expected_auto(tea_in, last_max_steps):
+    """C2D_FP_AUTO's rule (include/compton2d.h): exact iff every zone's tea sits
+    on the clamp (<= 5 or >= 1000 keV) and the last update's slowest zone took
+    <= C2D_FP_AUTO_STEPS (64) sub-steps."""
+    on = np.all((tea_in <= 5.0) | (tea_in >= 1000.0))
+    return abi.FP_EXACT if on and (last_max_steps is None or last_max_steps <= 64) else abi.FP_FAST
+
+
+def test_gpu_c3_fp_auto_mode_switches_and_stays_in_tolerance(capsys):
+    """C2D_FP_AUTO on the C3 deck's FP inputs, then on the same grid with the
+    zones taken off the clamp (tea varied per zone, the fp_bench --vary
+    recipe): the mode follows the rule, each result equals the det oracle
+    bit for bit (exact) or within tests/test_gpu_fp.py's tolerance (fast)."""
+    from test_gpu_fp import fast_vs_oracle
+    gc = case()
+    eng = Engine(gc.grid(device=0))
+    eng.fp_set_config(gc.constants())
+    eng.fp_set_mode(abi.FP_AUTO)
+    assert eng.last_fp_mode() == -1
+    js, ks = np.divmod(np.array(SAMPLE), gc.nr)
+    cell = np.arange(gc.nz * gc.nr, dtype=np.float64).reshape(gc.nz, gc.nr)
+    off = dict(gc.fp_in(2), tea=300.0 * (1.0 + 0.007 * (cell % 41)))   # every zone off the clamp
+    calls = [("step1", gc.fp_in(1)), ("step2", gc.fp_in(2)), ("step2 again", gc.fp_in(2)),
+             ("off clamp", off), ("step2 back", gc.fp_in(2)), ("step2 settled", gc.fp_in(2))]
+    last_steps, log = None, []
+    for label, fi in calls:
+        want = _expected_auto(np.asarray(fi["tea"]), last_steps)
+        g = eng.fp_step(fi["ncycle"], fi["time"], fi["dt"], fi, fi)
+        got = eng.last_fp_mode()
+        log.append((label, abi.FP_MODE_NAMES[got], float(np.max(g["zone_diag"][..., 5])), eng.last_fp_ms()))
+        assert got == want, (label, got, want)
+        o = OL.fp_step(gc.grid(), gc.constants(), fi["ncycle"], fi["time"], fi["dt"], fi, fi,
+                       flavor="det", cells=SAMPLE)
+        gs = {k: (np.asarray(v)[js, ks] if np.ndim(v) >= 2 else v) for k, v in g.items()}
+        os_ = {k: (np.asarray(v)[js, ks] if np.ndim(v) >= 2 else v) for k, v in o.items()}
+        for k in ("E_tot_old", "E_tot_new", "hr_total"):
+            gs.pop(k), os_.pop(k)
+        if got == abi.FP_EXACT:
+            for k in ZONE_KEYS:
+                np.testing.assert_array_equal(gs[k], os_[k], err_msg="%s %s" % (label, k))
+        else:
+            for k in ("Te_new", "tea", "gmin", "gmax", "p_nth"):
+                np.testing.assert_array_equal(gs[k], os_[k], err_msg="%s %s" % (label, k))
+            for k in ("f_nt", "Pnt"):
+                assert np.max(np.abs(gs[k] - os_[k])) <= 1e-10 * np.max(np.abs(os_[k])), (label, k)
+        last_steps = float(np.max(g["zone_diag"][..., 5]))
+    with capsys.disabled():
+        print("\nC2D_FP_AUTO on C3: " + "; ".join("%s: %s (max %d sub-steps, %.2f ms)" % x for x in log))
+    modes = [m for _, m, _, _ in log]
+    assert "exact" in modes and "fast" in modes
+    assert modes[3] == "fast" and modes[-1] == "exact"
+    eng.close()
+
+
+def test_gpu_coupled_run_logs_fp_mode():
+    """CoupledRun's default C2D_FP_AUTO on the C3 workload: every step with an
+    FP update logs the mode it ran; the coupled run reaches the clamp and then
+    runs the exact kernel (C3's steady state, the bench's timed steps)."""
+    wl = synth.c3_workload(sources=100_000, comtot_mode=abi.COMTOT_TABLE)
+    eng = Engine(wl.grid)
+    run = CoupledRun(eng, wl)
+    rows = [run.step() for _ in range(5)]
+    assert rows[0]["fp_mode"] is None                        # ncycle = 0: no update
+    assert all(r["fp_mode"] in ("exact", "fast") for r in rows[1:])
+    assert rows[-1]["fp_mode"] == "exact" and rows[-1]["mean_Te"] > 1.0e3
+    eng.close()

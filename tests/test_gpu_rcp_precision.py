@@ -26,3 +26,21 @@ def test_rcp_rsq_one_newton_step(capsys):
     # measured on the box (r05k): estimates 4.6e-8 / 5.2e-8, one step 2.2e-15 / 4.1e-15
     assert out["rcp"] > 1e-9 and out["rsq"] > 1e-9
     assert out["rcp+1N"] < 1e-14 and out["rsq+1N"] < 1e-14
+
+
+def test_tau_log_f32_relative_precision_in_the_tail(capsys):
+    """The fast build's optical-depth log (c2d_device.hpp c2d_tau_log_f32,
+    transport.hip TAU_LOG) over uniforms spread from 1e-16 to within 1e-16 of
+    1: relative error ~1e-7 everywhere.  A collision in the optically thin C3
+    medium needs u within ~1e-5 of 1, where v_log_f32 of (float)u kept only
+    1 - u to 6e-8 absolute (1e-3 relative; 0 for u > 1 - 2^-25)."""
+    rng = np.random.default_rng(12)
+    tail = 1.0 - 10.0 ** rng.uniform(-16, -0.31, 1 << 19)
+    u = np.concatenate([rng.random(1 << 19), tail, 10.0 ** rng.uniform(-16, -0.31, 1 << 16)])
+    u = u[(u > 0) & (u < 1)]
+    y = selftest_math(14, u)
+    rel = np.abs(y - np.log(u)) / np.abs(np.log(u))
+    with capsys.disabled():
+        print("\ntau log f32: max relative error %.2e (tail u > 0.99999: %.2e)"
+              % (rel.max(), rel[u > 0.99999].max()))
+    assert rel.max() < 1e-6

@@ -148,3 +148,18 @@ def test_volume_budget_matches_reference(name):
         nsv, ewsv = S.volume_budget(nst, si.Eloss_tot)
         np.testing.assert_array_equal(nsv, si.nsv)
         np.testing.assert_array_equal(ewsv, si.ewsv)
+
+
+@pytest.mark.parametrize("bad", [np.nan, np.inf, -np.inf])
+def test_volume_budget_raises_on_non_finite_emission(bad):
+    """A NaN emissivity (r08b: NaN tables after an n_field overflow) raises
+    instead of casting NaN to a negative packet count, which the reference's
+    `do i=1,nsv` would skip silently (src/imcgen2d.f:446-456)."""
+    si = GoldenCase("c3_mrk421").step_inputs(1)
+    fas = np.array(si.Eloss_tot, float)
+    fas[3, 2] = bad
+    with pytest.raises(FloatingPointError, match="non-finite"):
+        S.volume_budget(20000, fas)
+    fas[3, 2] = -1.0
+    with pytest.raises(ValueError, match="negative"):
+        S.volume_budget(20000, fas)
