@@ -502,6 +502,10 @@ def main():
     ap.add_argument("--no-fp-offclamp", action="store_true",
                     help="c3: skip the untimed off-clamp FP update (kernels.fp_offclamp)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--dump", default=None,
+                    help="directory: each rank writes rank<r>.npz with the last timed step's tally "
+                         "buffer, and for c3 the timed steps' SED sums and the electron state "
+                         "(the N-rank rehearsal compares them, tests/test_gpu_bench_ranks.py)")
     args = ap.parse_args()
 
     import torch
@@ -563,6 +567,16 @@ def main():
     if not (steps_global > 0 and elapsed > 0 and np.isfinite(last_tallies).all()):
         raise SystemExit("bench: invalid run on rank %d: %g packet-steps in %g s, %d non-finite tallies"
                          % (rank, steps_global, elapsed, int((~np.isfinite(last_tallies)).sum())))
+    if args.dump:
+        d = Path(args.dump)
+        d.mkdir(parents=True, exist_ok=True)
+        blob = {"tallies": last_tallies}
+        if wk == "c3":
+            F, F2, cnt, _ = eng.obs_result()
+            f_nt, Pnt = run.electrons()
+            blob.update(sed_F=F, sed_F2=F2, sed_count=cnt, f_nt=f_nt, Pnt=Pnt,
+                        tea=np.asarray(run.state["tea"]), Te_new=np.asarray(run.state["Te_new"]))
+        np.savez(d / ("rank%d.npz" % rank), **blob)
     if rank != 0:
         eng.close()
         return

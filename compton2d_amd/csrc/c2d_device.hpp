@@ -82,7 +82,10 @@ struct SpecDev {             /* file_sp table (imcsurf2d_para.f:544-685) */
  * xnu (the kappa_tot column, imctrk2d.f:382-384) and efl its E_field bin (the
  * n_field row, imctrk2d.f:547-549): xnu does not change between a census
  * write and the next step's read, so a census packet looks neither up
- * again.  ie, efl = 0: not known (the reader looks them up). */
+ * again.  Every writer stores both (the kernels, c2d_census_import by the
+ * same bisection; c2d_census_append rejects a record with ie = 0): ie is
+ * 1..400, efl 1..400 or 0 for xnu at or below the field grid's lower edge
+ * (no n_field row, imctrk2d.f:544-549). */
 __host__ __device__ __forceinline__ uint32_t c2d_cens_jk(int jph, int kph, int ie, int efl) {
   return (uint32_t)kph | ((uint32_t)ie << 7) | ((uint32_t)jph << 16) | ((uint32_t)efl << 23);
 }
@@ -194,6 +197,22 @@ __device__ __forceinline__ void cst4(c2d_u4* p, uint32_t jk, uint32_t bins, uint
 }
 __device__ __forceinline__ c2d_u4 cld4(const c2d_u4* p) { return *(const C2D_GLOBAL c2d_u4*)p; }
 __device__ __forceinline__ uint64_t c2d_tg_key(c2d_u4 t) { return ((uint64_t)t.w << 32) | (uint64_t)t.z; }
+/* the same accesses marked non-temporal (read or written once per step:
+ * the census stream through the transport kernels, C2D_CENS_NT) */
+__device__ __forceinline__ void cst2_nt(c2d_d2* p, double a, double b) {
+  const c2d_d2 v = {a, b};
+  __builtin_nontemporal_store(v, (C2D_GLOBAL c2d_d2*)p);
+}
+__device__ __forceinline__ c2d_d2 cld2_nt(const c2d_d2* p) {
+  return __builtin_nontemporal_load((const C2D_GLOBAL c2d_d2*)p);
+}
+__device__ __forceinline__ void cst4_nt(c2d_u4* p, uint32_t jk, uint32_t bins, uint64_t key) {
+  const c2d_u4 v = {jk, bins, (uint32_t)key, (uint32_t)(key >> 32)};
+  __builtin_nontemporal_store(v, (C2D_GLOBAL c2d_u4*)p);
+}
+__device__ __forceinline__ c2d_u4 cld4_nt(const c2d_u4* p) {
+  return __builtin_nontemporal_load((const C2D_GLOBAL c2d_u4*)p);
+}
 /* a record's bins word alone (compaction scans, dead marks) */
 __device__ __forceinline__ uint32_t cens_bins(const c2d_u4* tg, int64_t s) {
   return gld(reinterpret_cast<const uint32_t*>(tg + s) + 1);

@@ -32,16 +32,16 @@ extern "C" int c2d_launch_source_exact(const KParams* P, int grid, hipStream_t s
 extern "C" int c2d_launch_source_fast(const KParams* P, int grid, hipStream_t s);
 extern "C" int c2d_launch_scatter_exact(const KParams* P, const GenArgs* A, int grid, hipStream_t s);
 extern "C" int c2d_launch_scatter_fast(const KParams* P, const GenArgs* A, int grid, hipStream_t s);
-extern "C" int c2d_transport_occupancy_exact(int* blocks_per_cu, size_t lds);
-extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds);
+extern "C" int c2d_transport_occupancy_exact(int* blocks_per_cu, size_t lds, int trk);
+extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds, int trk);
 extern "C" int c2d_aux_occupancy_exact(int which, int* blocks_per_cu);
 extern "C" int c2d_aux_occupancy_fast(int which, int* blocks_per_cu);
 extern "C" int c2d_launch_bundle_exact(const KParams* P, const GenArgs* A, int grid, size_t lds,
                                        int trk, hipStream_t s);
 extern "C" int c2d_launch_bundle_fast(const KParams* P, const GenArgs* A, int grid, size_t lds,
                                       int trk, hipStream_t s);
-extern "C" int c2d_bundle_occupancy_exact(int* blocks_per_cu, size_t lds);
-extern "C" int c2d_bundle_occupancy_fast(int* blocks_per_cu, size_t lds);
+extern "C" int c2d_bundle_occupancy_exact(int* blocks_per_cu, size_t lds, int trk);
+extern "C" int c2d_bundle_occupancy_fast(int* blocks_per_cu, size_t lds, int trk);
 extern "C" int c2d_launch_comtab_sigma(const double* gnt, double* S, hipStream_t s);
 extern "C" int c2d_launch_comtab_gemm(const double* f_nt, const double* gnt, const double* S,
                                       double* tab, int ncell, hipStream_t s);
@@ -411,15 +411,15 @@ extern "C" int c2d_init(const c2d_config* cfg, c2d_ctx** out) {
    * from the runtime's occupancy calculator for this kernel and LDS size) */
   int blocks_per_cu = 0;
   int orc = cfg->comtot_mode == C2D_COMTOT_TABLE
-                ? c2d_transport_occupancy_fast(&blocks_per_cu, c->lds_bytes)
-                : c2d_transport_occupancy_exact(&blocks_per_cu, c->lds_bytes);
+                ? c2d_transport_occupancy_fast(&blocks_per_cu, c->lds_bytes, cfg->trk_variant)
+                : c2d_transport_occupancy_exact(&blocks_per_cu, c->lds_bytes, cfg->trk_variant);
   if (orc) return fail(c, C2D_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)orc));
   c->max_grid = c->n_cu * std::max(1, blocks_per_cu);
   {
     auto occ = cfg->comtot_mode == C2D_COMTOT_TABLE ? c2d_bundle_occupancy_fast
                                                     : c2d_bundle_occupancy_exact;
     int b0 = 0;
-    orc = occ(&b0, c->lds_bytes);
+    orc = occ(&b0, c->lds_bytes, cfg->trk_variant);
     if (orc) return fail(c, C2D_E_HIP, "occupancy query: %s", hipGetErrorString((hipError_t)orc));
     c->bundle_lds = c->lds_bytes;
     c->bundle_grid = c->n_cu * std::max(1, b0);
@@ -1726,6 +1726,18 @@ __global__ void __launch_bounds__(256) c2d_census_unpack_kernel(CensusSoA cs, co
     rec_unpack(cs, cens_slot(clist, first + i), rec + i * C2D_CENSUS_REC_WORDS);
 }
 
+/* flag = 1 if a packed record's jk word lacks its E_ph bin (ie = 0) or its
+ * cell lies off the grid: the kernels read kappa at ie - 1 without a lookup */
+__global__ void __launch_bounds__(256) c2d_census_check_kernel(const uint64_t* __restrict__ rec, int64_t n,
+                                                               int nz, int nr, int32_t* __restrict__ flag) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t jk = (uint32_t)(rec[i * C2D_CENSUS_REC_WORDS + 6] & 0xffffffffull);
+    const int ie = c2d_cens_ie(jk), j = c2d_cens_j(jk), k = c2d_cens_k(jk);
+    if (ie < 1 || ie > C2D_N_VOL || j < 1 || j > nz || k < 1 || k > nr) atomicOr(flag, 1);
+  }
+}
+
 static const int32_t* cens_list(const c2d_ctx* c) { return c->chunked ? c->clist[c->ccur] : nullptr; }
 
 /* m census records first, first + stride, ... to the host, as the
@@ -1877,6 +1889,18 @@ extern "C" int c2d_census_append(c2d_ctx* c, const uint64_t* d_rec, int64_t n) {
                 (long long)c->n_census, (long long)n, (long long)c->cfg.census_capacity);
   if (n == 0) return C2D_OK;
   HIPCHK(c, hipSetDevice(c->cfg.device));
+  {   /* every record carries its cell and E_ph bin (c2d_cens_jk) */
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 8);
+    int32_t bad = 0;
+    HIPCHK(c, hipMemsetAsync(c->derr, 0, sizeof(int32_t), c->stream));
+    hipLaunchKernelGGL(c2d_census_check_kernel, dim3(grid), dim3(256), 0, c->stream, d_rec, n, c->nz, c->nr,
+                       c->derr);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(&bad, c->derr, sizeof bad, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (bad) return fail(c, C2D_E_ARG, "c2d_census_append: a record without its cell or E_ph bin (c2d_census_pack "
+                         "format, include/compton2d.h)");
+  }
   if (c->chunked) {
     /* the list's last chunk fills up first, then free chunks join the list */
     const int64_t k = (c->n_census + n + C2D_CCHUNK - 1) / C2D_CCHUNK - c->n_clist;

@@ -140,6 +140,31 @@ constexpr long long CHUNK = C2D_WORK_CHUNK;
 #ifndef C2D_TAU_F32
 #define C2D_TAU_F32 1
 #endif
+/* the census stream (records read once at a source's start, written once at
+ * its census; the source kernel's volume records likewise) as non-temporal
+ * accesses (C2D_CENS_NT=1, default): they need not stay in the XCD's 4 MB L2
+ * beside the cell tables (comtot 4.4 MB + kappa 0.9 MB on C3), which every
+ * flight step gathers.  C3 generation 0: 112.4 -> 106.7 ms (profiles/r09d,
+ * r09e: two A/B pairs each, same histories) */
+#ifndef C2D_CENS_NT
+#define C2D_CENS_NT 1
+#endif
+/* the escape-event records likewise (C2D_EV_NT=1; measured neutral, r09e) */
+#ifndef C2D_EV_NT
+#define C2D_EV_NT 0
+#endif
+#define EV_ST(p, v) __builtin_nontemporal_store((double)(v), (C2D_GLOBAL double*)(p))
+#if C2D_CENS_NT
+#define CENS_ST2 cst2_nt
+#define CENS_ST4 cst4_nt
+#define CENS_LD2 cld2_nt
+#define CENS_LD4 cld4_nt
+#else
+#define CENS_ST2 cst2
+#define CENS_ST4 cst4
+#define CENS_LD2 cld2
+#define CENS_LD4 cld4
+#endif
 /* fast build: the comtot table coordinate ln(xnu) of a source with
  * v_log_f32 (C2D_LNX_F32=1).  An absolute error of ~1e-7 in ln(xnu) moves
  * the cubic interpolation point by 4e-6 of a table step (ln 1e25 / 2047),
@@ -736,8 +761,13 @@ __device__ __forceinline__ void push_event(const KParams& P0, double tb, const P
   const unsigned long long slot = wave_reserve(P.n_ev_sh + sh * C2D_EV_SHARD_STRIDE);
   if (slot < (unsigned long long)P.cap_ev_sh) {
     double* e = P.ev + ((int64_t)sh * P.cap_ev_sh + (int64_t)slot) * C2D_EVENT_WORDS;
+#if C2D_EV_NT
+    EV_ST(e, tb); EV_ST(e + 1, p.xnu); EV_ST(e + 2, p.ew); EV_ST(e + 3, p.rpre); EV_ST(e + 4, p.zpre);
+    EV_ST(e + 5, p.wmu); EV_ST(e + 6, p.phi);
+#else
     gst(e, tb); gst(e + 1, p.xnu); gst(e + 2, p.ew); gst(e + 3, p.rpre); gst(e + 4, p.zpre);
     gst(e + 5, p.wmu); gst(e + 6, p.phi);
+#endif
   } else {
     gor(P.err, ERR_EVENT);
   }
@@ -989,14 +1019,14 @@ C2D_COLD_FN void census_write(const KParams& P0, const Tal& T, const Pkt& p, Lan
   }
   const unsigned long long slot = census_slot_chunk(P);
   if (slot < (unsigned long long)P.cap_cout) {
-    cst2(P.cout.rz + slot, p.rpre, p.zpre);
+    CENS_ST2(P.cout.rz + slot, p.rpre, p.zpre);
 #if C2D_TABLE_COMTOT
-    cst2(P.cout.wp + slot, p.wmu, p.eta);            /* encoded azimuth (CensusSoA) */
+    CENS_ST2(P.cout.wp + slot, p.wmu, p.eta);        /* encoded azimuth (CensusSoA) */
 #else
-    cst2(P.cout.wp + slot, p.wmu, p.phi);
+    CENS_ST2(P.cout.wp + slot, p.wmu, p.phi);
 #endif
-    cst2(P.cout.ex + slot, p.ew, p.xnu);
-    cst4(P.cout.tg + slot, c2d_cens_jk(p.jph, p.kph, p.ie & 0xffff, efl),
+    CENS_ST2(P.cout.ex + slot, p.ew, p.xnu);
+    CENS_ST4(P.cout.tg + slot, c2d_cens_jk(p.jph, p.kph, p.ie & 0xffff, efl),
          (p.bins & 0x00ffffffu)
 #if C2D_TABLE_COMTOT
              | (p.esw == -1 ? C2D_CENS_ESW : 0u)
@@ -1696,20 +1726,20 @@ __global__ void __launch_bounds__(SRCBLOCK) C2D_SFX(c2d_source_kernel)(const KPa
       if (it < P.n_vol_items) {
         /* census format (pf_apply reads it back; C2D_CENS_VOL: dcen from the key) */
         const int64_t s = P.vol_cens_base + it;
-        cst2(P.cin.rz + s, p.rpre, p.zpre);
+        CENS_ST2(P.cin.rz + s, p.rpre, p.zpre);
 #if C2D_TABLE_COMTOT
         const double eta = c2d_cos(p.phi);           /* set_phi's encoding (CensusSoA) */
         const bool esw_neg = !(p.phi <= PI_REF && p.phi >= 1.0e-10);
-        cst2(P.cin.wp + s, p.wmu, eta);
+        CENS_ST2(P.cin.wp + s, p.wmu, eta);
 #else
         const bool esw_neg = false;
-        cst2(P.cin.wp + s, p.wmu, p.phi);
+        CENS_ST2(P.cin.wp + s, p.wmu, p.phi);
 #endif
-        cst2(P.cin.ex + s, p.ew, p.xnu);
+        CENS_ST2(P.cin.ex + s, p.ew, p.xnu);
         const int ie = grid_lookup(g->E_ph, C2D_N_VOL, g->eph_start, g->eph_k0, p.xnu);
         const int efl = p.xnu > P.egg_min ? grid_lookup(g->E_field, C2D_NPHFIELD, g->efl_start, g->efl_k0, p.xnu) : 0;
-        cst4(P.cin.tg + s, c2d_cens_jk(p.jph, p.kph, ie, efl),
-             (p.bins & 0x00ffffffu) | C2D_CENS_VOL | (esw_neg ? C2D_CENS_ESW : 0u), p.key);
+        CENS_ST4(P.cin.tg + s, c2d_cens_jk(p.jph, p.kph, ie, efl),
+                 (p.bins & 0x00ffffffu) | C2D_CENS_VOL | (esw_neg ? C2D_CENS_ESW : 0u), p.key);
       } else {
         store_pk(P.pk, it - P.n_vol_items, p);
       }
@@ -1813,8 +1843,8 @@ struct CensRec {
 
 __device__ __forceinline__ void pf_issue(const KParams& P0, CensRec& r, long long i) {
   const KParams& P = cold(P0);
-  const c2d_d2 rz = cld2(P.cin.rz + i), wp = cld2(P.cin.wp + i), ex = cld2(P.cin.ex + i);
-  const c2d_u4 tg = cld4(P.cin.tg + i);
+  const c2d_d2 rz = CENS_LD2(P.cin.rz + i), wp = CENS_LD2(P.cin.wp + i), ex = CENS_LD2(P.cin.ex + i);
+  const c2d_u4 tg = CENS_LD4(P.cin.tg + i);
   r.rpre = rz.x; r.zpre = rz.y;
   r.wmu = wp.x; r.cphi = wp.y;
   r.ew = ex.x; r.xnu = ex.y;
@@ -2438,11 +2468,15 @@ __device__ __forceinline__ void bundle_step(const KParams& P1, const Tal& T, con
        * no cancellation near the axis in f32.  u: the top 24 bits of each
        * 32-bit half of the point stream's output, (u + 1/2) 2^-24 in (0,1)
        * exactly in f32; -log(1-x) by its series below 1e-2 (truncation
-       * < x^4/5), else by v_log_f32 */
+       * < x^4/5), else by v_log_f32.  Lengths in units of rs = max(rpre,
+       * 1/sigabs) (wmustar is a ratio of lengths): s/rs, rpre/rs <= O(10),
+       * so nothing overflows f32 however large rpre (1.8e19 cm unscaled) */
       {
-        const float isig = (float)FDIV_POS(1.0, sigabs);
-        const float Aw = (float)(wmu * rpre);
-        const float Cw = (float)(rpre * rpre * (1.0 - wmu * wmu));
+        const double sr = sigabs * rpre;            /* rpre in absorption lengths */
+        const double a = sr < 1.0 ? sr : 1.0;       /* rpre / rs */
+        const float isig = (float)(sr > 1.0 ? FDIV_POS(1.0, sr) : 1.0);   /* 1 / (sigabs rs) */
+        const float Aw = (float)(wmu * a);
+        const float Cw = (float)(a * a * (1.0 - wmu * wmu));
         const float qf = (float)qabs;
         float wsum = 0.0f;
         /* c2d_abspt(key, sub, n) = mix64(key + gamma ((sub << 32 | n) + 1)):
@@ -2825,10 +2859,14 @@ extern "C" int C2D_SFX(c2d_launch_bundle)(const c2d::KParams* P_dev, const c2d::
   return (int)hipGetLastError();
 }
 
-extern "C" int C2D_SFX(c2d_bundle_occupancy)(int* blocks_per_cu, size_t lds_bytes) {
+/* trk: the tracker instance the context launches (c2d_config.trk_variant):
+ * its own VGPR count sets the resident blocks */
+extern "C" int C2D_SFX(c2d_bundle_occupancy)(int* blocks_per_cu, size_t lds_bytes, int trk) {
   if (C2D_SFX(bundle_lds_attr)(lds_bytes) != 0) { *blocks_per_cu = 0; return 0; }
-  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      blocks_per_cu, C2D_SFX(c2d::c2d_bundle_kernel)<0>, c2d::BLOCK, lds_bytes);
+  return (int)(trk ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                         blocks_per_cu, C2D_SFX(c2d::c2d_bundle_kernel)<1>, c2d::BLOCK, lds_bytes)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                         blocks_per_cu, C2D_SFX(c2d::c2d_bundle_kernel)<0>, c2d::BLOCK, lds_bytes));
 }
 
 extern "C" int C2D_SFX(c2d_launch_source)(const c2d::KParams* P_dev, int grid, hipStream_t stream) {
@@ -2853,9 +2891,11 @@ extern "C" int C2D_SFX(c2d_aux_occupancy)(int which, int* blocks_per_cu) {
   return (int)e;
 }
 
-extern "C" int C2D_SFX(c2d_transport_occupancy)(int* blocks_per_cu, size_t lds_bytes) {
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      blocks_per_cu, C2D_SFX(c2d::c2d_transport_kernel)<0>, c2d::BLOCK, lds_bytes);
+extern "C" int C2D_SFX(c2d_transport_occupancy)(int* blocks_per_cu, size_t lds_bytes, int trk) {
+  hipError_t e = trk ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                           blocks_per_cu, C2D_SFX(c2d::c2d_transport_kernel)<1>, c2d::BLOCK, lds_bytes)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                           blocks_per_cu, C2D_SFX(c2d::c2d_transport_kernel)<0>, c2d::BLOCK, lds_bytes);
   return (int)e;
 }
 

@@ -128,4 +128,7 @@ def compare_runs(FA, EA, FB, EB):
             "max_abs_z": float(np.abs(z).max()), "chi2": chi2,
             "p_value": float(stats.chi2.sf(chi2, len(live))),
             "bins_over_4sigma": [int(b) for b in live[np.abs(z) > 4.0]],
-            "band_z": [float(x) for x in zb], "rel_l2": rel, "rel_l2_expected": rel_exp}
+            "band_z": [float(x) for x in zb],
+            "band_rel_dev": [float((a - b) / b) if b > 0 else 0.0 for a, b in zip(eA, eB)],
+            "band_rel_sigma": [float(x / b) if b > 0 else 0.0 for x, b in zip(se, eB)],
+            "rel_l2": rel, "rel_l2_expected": rel_exp}

@@ -71,9 +71,11 @@ def test_fast_kernel_spectrum_vs_reference_stream_fixture():
     lagged-Fibonacci streams (tests/golden/spectrum_fib.npz: 3 seeds x 1.9e6
     escapes, C oracle bit-exact to the Fortran, regenerated and checked in
     tests/test_spectrum_rng.py): F(E) relative L2 <= 1 %; each light-curve
-    band to 1 % or, where rare Compton events reach it, to 4 sigma of the
-    combined statistical error (reference seed scatter and the lineage run's
-    shard scatter, both in the fixture); the first synchrotron band to 1 %."""
+    band the fixture resolves to 4 sigma <= 1 % of the combined statistical
+    error (reference seed scatter and the lineage run's shard scatter) to 1 %:
+    the synchrotron band 0.  The Compton bands, which 3 reference seeds of this
+    thin medium leave at 0.6-96 % sigma, are pinned to <= 5 % bounds by
+    tests/test_gpu_compton.py on the Compton workload."""
     from pathlib import Path
     import spectrum_case as S
     fx = np.load(Path(__file__).resolve().parent / "golden" / "spectrum_fib.npz", allow_pickle=False)
@@ -92,7 +94,7 @@ def test_fast_kernel_spectrum_vs_reference_stream_fixture():
     E = np.asarray(t["edout"]).ravel()
     E_ref = fx["edout"].mean(axis=0)
     sig = S.band_errors(fx["edout"], fx["lineage_edout_shards"])
-    bands = [i for i in range(E_ref.size) if fx["edout"][:, i].min() > 0]
+    bands = [i for i in range(E_ref.size) if fx["edout"][:, i].min() > 0 and 4.0 * sig[i] <= 1e-2]
+    assert bands and bands[0] == 0
     for i in bands:
-        assert abs(E[i] - E_ref[i]) <= max(1e-2, 4.0 * sig[i]) * E_ref[i], (i, E[i], E_ref[i], sig[i])
-    assert sig[bands[0]] < 2e-3 and abs(E[bands[0]] - E_ref[bands[0]]) <= 1e-2 * E_ref[bands[0]]
+        assert abs(E[i] - E_ref[i]) <= 1e-2 * E_ref[i], (i, E[i], E_ref[i], sig[i])

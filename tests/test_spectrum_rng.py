@@ -52,14 +52,14 @@ def test_lineage_rng_spectrum_within_1pct_of_reference_streams(capsys):
     # light curves per band (lcb_01.dat columns).  Each band's statistical
     # error is estimated from both sides: the reference's seed-to-seed
     # scatter (3 runs) and the lineage run's shard-to-shard scatter (8 shards
-    # of 1.25e6 sources).  The synchrotron bands are carried by the
-    # unscattered copies (errors < 0.2 %) and hold the 1 % bound; a band that
-    # rare Compton events reach (~3 collisions per 1e6 packets in this thin
-    # medium, each handing split2 x split3 secondaries a large gain) has a
-    # heavy tail that 3 reference seeds under-sample, so it must agree within
-    # 4 sigma of the combined error.  (At n_e x 5e4 the two generators'
-    # collision counts agree to their Poisson noise: 14325 vs 14370 per 1e5
-    # packets, 4 seeds each.)
+    # of 1.25e6 sources).  A band this sample resolves to the north-star
+    # bound (4 sigma <= 1 %: the synchrotron band 0, carried by the
+    # unscattered copies) must agree to 1 %.  The bands that rare Compton
+    # events reach (~3 collisions per 1e6 packets in this thin medium, each
+    # handing split2 x split3 secondaries a large gain; sigma 0.6-96 %) are
+    # not asserted here: tests/test_gpu_compton.py pins every Compton band on
+    # the Compton workload (n_e x 5e4, thousands of reference-stream runs)
+    # to an explicit bound of at most 5 %.
     E_all = np.array([r[1] for r in fib])
     sig_b = S.band_errors(E_all, [r[1] for r in lin])
     bands = [i for i in range(E_all.shape[1]) if E_all[:, i].min() > 0]
@@ -74,9 +74,10 @@ def test_lineage_rng_spectrum_within_1pct_of_reference_streams(capsys):
         print("light curves per band (band, |dev|, combined 1-sigma error): %s" %
               ["(%d, %.4f, %.4f)" % x for x in lc])
     assert cross <= 1.0e-2, cross
-    for i, dev, sig in lc:
-        assert dev <= max(1.0e-2, 4.0 * sig), (i, dev, sig)
-    assert lc[0][2] < 2.0e-3 and lc[0][1] <= 1.0e-2     # the first synchrotron band: 1 %
+    resolved = [(i, dev, sig) for i, dev, sig in lc if 4.0 * sig <= 1.0e-2]
+    assert resolved and resolved[0][0] == 0              # the first synchrotron band
+    for i, dev, sig in resolved:
+        assert dev <= 1.0e-2, (i, dev, sig)
     # no bias beyond the noise: the larger-sample comparison is no further
     # apart than two reference runs of 2e6 packets are from each other
     assert cross <= max(floor), (cross, floor)
