@@ -127,6 +127,7 @@ struct PktSoA {
   uint32_t* jk;      /* jph << 16 | kph                                         */
   uint32_t* bins;    /* jgpsp | jgplc << 8 | jgpmu << 16 | kap << 24            */
   uint32_t* ctr;     /* RNG counter position of `key`                           */
+  uint32_t* sub;     /* its sub-stream (a split3 copy's successful resample)    */
   uint64_t* key;
 };
 
@@ -344,6 +345,8 @@ struct GenArgs {
   unsigned long long* n_pk;        /* scatter: secondaries written; transport: item count */
   unsigned long long* work_counter;
   unsigned long long* work_sh;     /* bundle kernel: C2D_WORK_SHARDS counters, stride 16 */
+  unsigned long long* n_hard;      /* scatter: split3 copies left for the hard kernel */
+  int64_t* hard;                   /* their item indices (capacity KParams.cap_pk)  */
   int64_t item_begin, item_end;    /* scatter kernel item range                   */
   int64_t n_items;                 /* transport, generation 0: census + sources    */
   int64_t n2_in, n3_in;

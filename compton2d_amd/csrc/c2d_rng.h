@@ -33,6 +33,8 @@
  *   recombined       = (K_src, sub C2D_SUB_RECOMB)            (imctrk2d.f:690-704)
  *   scatter copy ii  = derive(K_par, TAG_SCAT2, ii, ctr_par; sub_par)  (imctrk2d.f:611)
  *   split3 copy ii2  = derive(K_chd, TAG_SCAT3, ii2, ctr_chd)          (imctrk2d.f:633)
+ *   its resample k   = (K_split3, sub k), counter 0 at each attempt    (imctrk2d.f:634-648,
+ *                      `goto 215`); the copy flies on from its first success's stream
  *   census key       = census_key(K_pkt, ctr_pkt, sub_pkt)             (imctrk2d.f:571)
  * Draw n of (key, sub) = u53(mix64(key + gamma * ((sub << 32 | n) + 1)));
  * derive(key, tag, a, b; sub) = Philox_key({a, b, tag | sub << 8, C_DERIVE}).

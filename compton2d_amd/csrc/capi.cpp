@@ -30,8 +30,8 @@ extern "C" int c2d_launch_transport_fast(const KParams* P, const GenArgs* A, int
                                          int trk, hipStream_t s);
 extern "C" int c2d_launch_source_exact(const KParams* P, int grid, hipStream_t s);
 extern "C" int c2d_launch_source_fast(const KParams* P, int grid, hipStream_t s);
-extern "C" int c2d_launch_scatter_exact(const KParams* P, const GenArgs* A, int grid, hipStream_t s);
-extern "C" int c2d_launch_scatter_fast(const KParams* P, const GenArgs* A, int grid, hipStream_t s);
+extern "C" int c2d_launch_scatter_exact(const KParams* P, const GenArgs* A, int grid, int hard_grid, hipStream_t s);
+extern "C" int c2d_launch_scatter_fast(const KParams* P, const GenArgs* A, int grid, int hard_grid, hipStream_t s);
 extern "C" int c2d_transport_occupancy_exact(int* blocks_per_cu, size_t lds, int trk);
 extern "C" int c2d_transport_occupancy_fast(int* blocks_per_cu, size_t lds, int trk);
 extern "C" int c2d_aux_occupancy_exact(int which, int* blocks_per_cu);
@@ -62,10 +62,12 @@ namespace {
 
 /* CTL_EVSH: the C2D_EV_SHARDS event counters, one per 128-B line */
 enum { CTL_WORK = 0, CTL_NCOUT = 1, CTL_POOLH = 2, CTL_N2 = 3, CTL_N3 = 4, CTL_NPK = 5,
-       CTL_NOUT = 6, CTL_POOLN = 7, CTL_CNT = 8, CTL_RELN = CTL_CNT + C2D_NCOUNTERS, CTL_RELH,
+       CTL_NOUT = 6, CTL_POOLN = 7, CTL_CNT = 8, CTL_RELN = CTL_CNT + C2D_NCOUNTERS, CTL_RELH, CTL_NHARD,
        CTL_EVSH = 32, CTL_PROF = CTL_EVSH + C2D_EV_SHARDS * C2D_EV_SHARD_STRIDE,
        CTL_WSH = CTL_PROF + C2D_TR_PROF_WORDS,
        CTL_WORDS = CTL_WSH + C2D_WORK_SHARDS * C2D_EV_SHARD_STRIDE };
+
+static_assert(CTL_NHARD < CTL_EVSH, "control words overlap the event counters");
 
 /* the packet store (c2d_device.hpp PktSoA) */
 struct DevPk {
@@ -73,12 +75,14 @@ struct DevPk {
   uint32_t* jk = nullptr;
   uint32_t* bins = nullptr;
   uint32_t* ctr = nullptr;
+  uint32_t* sub = nullptr;
   uint64_t* key = nullptr;
+  int64_t* hard = nullptr;    /* the scatter kernel's hard list (GenArgs.hard) */
   int64_t cap = 0;
   PktSoA soa() const {
     PktSoA s;
     s.rpre = d[0]; s.zpre = d[1]; s.wmu = d[2]; s.phi = d[3]; s.ew = d[4]; s.xnu = d[5];
-    s.dcen = d[6]; s.jk = jk; s.bins = bins; s.ctr = ctr; s.key = key;
+    s.dcen = d[6]; s.jk = jk; s.bins = bins; s.ctr = ctr; s.sub = sub; s.key = key;
     return s;
   }
   void release() {
@@ -86,9 +90,12 @@ struct DevPk {
     if (jk) (void)hipFree(jk);
     if (bins) (void)hipFree(bins);
     if (ctr) (void)hipFree(ctr);
+    if (sub) (void)hipFree(sub);
     if (key) (void)hipFree(key);
-    jk = bins = ctr = nullptr;
+    if (hard) (void)hipFree(hard);
+    jk = bins = ctr = sub = nullptr;
     key = nullptr;
+    hard = nullptr;
     cap = 0;
   }
 };
@@ -1408,7 +1415,9 @@ static int run_step_body(c2d_ctx* c) {
       HIPCHK(c, dalloc(&c->pk.jk, want));
       HIPCHK(c, dalloc(&c->pk.bins, want));
       HIPCHK(c, dalloc(&c->pk.ctr, want));
+      HIPCHK(c, dalloc(&c->pk.sub, want));
       HIPCHK(c, dalloc(&c->pk.key, want));
+      HIPCHK(c, dalloc(&c->pk.hard, want));
       c->pk.cap = want;
     }
   }
@@ -1501,6 +1510,7 @@ static int run_step_body(c2d_ctx* c) {
       const int64_t e = std::min<int64_t>(total, b + pk_chunk);
       HIPCHK(c, hipMemsetAsync(c->ctl + CTL_NPK, 0, sizeof(unsigned long long), c->stream));
       HIPCHK(c, hipMemsetAsync(c->ctl + CTL_WORK, 0, sizeof(unsigned long long), c->stream));
+      HIPCHK(c, hipMemsetAsync(c->ctl + CTL_NHARD, 0, sizeof(unsigned long long), c->stream));
       GenArgs A = {};
       A.gen = gen;
       A.q2_in = c->q2[qin]; A.q3_in = c->q3[qin];
@@ -1508,9 +1518,11 @@ static int run_step_body(c2d_ctx* c) {
       A.n2_out = c->ctl + CTL_N2; A.n3_out = c->ctl + CTL_N3;
       A.n_pk = c->ctl + CTL_NPK;
       A.work_counter = c->ctl + CTL_WORK;
+      A.n_hard = c->ctl + CTL_NHARD;
+      A.hard = c->pk.hard;
       A.item_begin = b; A.item_end = e;
       A.n2_in = n2; A.n3_in = n3;
-      int rc = launch_sc(c->dP, &A, aux_grid(e - b, c->sc_grid), c->stream);
+      int rc = launch_sc(c->dP, &A, aux_grid(e - b, c->sc_grid), 2 * c->n_cu, c->stream);
       if (rc) return fail(c, C2D_E_HIP, "scatter launch (gen %d): %s", gen, hipGetErrorString((hipError_t)rc));
       rc = launch_tr(c->dP, &A, tr_grid(e - b), c->lds_bytes, cfg.trk_variant, c->stream);
       if (rc) return fail(c, C2D_E_HIP, "transport launch (gen %d): %s", gen, hipGetErrorString((hipError_t)rc));

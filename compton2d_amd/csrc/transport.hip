@@ -649,6 +649,11 @@ __device__ __forceinline__ int cdf_index(const double* cdf /*0-based*/, int n, d
 /* ------------------------------------------------------------------ */
 /* nth2d (src/nontherm2d.f:159-183) + compb2d (src/compb_2d.f:1-318)    */
 /* ------------------------------------------------------------------ */
+/* TALLY = +1: the call's nelectron samples and counters are added; -1: the
+ * same call subtracts them again (a speculative split3 attempt beyond the
+ * first success, c2d_scatter_hard_kernel) */
+#define CB_CNT(w) do { if (TALLY > 0) atomicAdd(&c2d_cnt_lds[w], 1u); else atomicSub(&c2d_cnt_lds[w], 1u); } while (0)
+template <int TALLY = 1>
 __device__ __forceinline__ int compb2d(const KParams& P, const Geo* g, double* nel, Pkt& p, LaneCnt& lc) {
   const double fuzz = 1.0e-10, lim = 9.9999999e-1;
   const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
@@ -658,9 +663,10 @@ __device__ __forceinline__ int compb2d(const KParams& P, const Geo* g, double* n
   double sz, games, phat, znues, wa, wb, swa;
   int i_gam;
   int guard = 0;
-  LC_ADD(lc, C2D_CNT_COMPB);
+  (void)lc;
+  CB_CNT(C2D_CNT_COMPB);
   for (;;) {
-    if (++guard > MAX_REJECT) { LC_ADD(lc, C2D_CNT_ABORTED); break; }
+    if (++guard > MAX_REJECT) { CB_CNT(C2D_CNT_ABORTED); break; }
     /* nth2d */
     double rnum = U(p);
     rnum = (double)(int32_t)(rnum * 1.0e6) / 1.0e6 + 1.0e-6 * U(p);
@@ -676,7 +682,7 @@ __device__ __forceinline__ int compb2d(const KParams& P, const Geo* g, double* n
     }
     gamm = __builtin_sqrt(P.gnt[i - 1] * P.gnt[i - 2]) + 1.0;
     betb = __builtin_sqrt(1.0 - 1.0 / (gamm * gamm));
-    atomicAdd(&nel[i], 1.0);
+    atomicAdd(&nel[i], (double)TALLY);
     i_gam = i;
     omeg = 2.0 * U(p) - 1.0;
     omeg = clampd(omeg, lim);
@@ -700,7 +706,7 @@ __device__ __forceinline__ int compb2d(const KParams& P, const Geo* g, double* n
   }
   betz = 1.0 + 2.0 * znue;
   for (;;) {
-    if (++guard > 2 * MAX_REJECT) { LC_ADD(lc, C2D_CNT_ABORTED); break; }
+    if (++guard > 2 * MAX_REJECT) { CB_CNT(C2D_CNT_ABORTED); break; }
     sz = (1.0 + 2.0 * znue * U(p)) / betz;
     games = 1.0 + (1.0 - 1.0 / sz) / znue;
     if ((1.0 - games * games) < 0.0) continue;
@@ -711,7 +717,7 @@ __device__ __forceinline__ int compb2d(const KParams& P, const Geo* g, double* n
   }
   znues = znue * sz;
   for (;;) {
-    if (++guard > 3 * MAX_REJECT) { LC_ADD(lc, C2D_CNT_ABORTED); break; }
+    if (++guard > 3 * MAX_REJECT) { CB_CNT(C2D_CNT_ABORTED); break; }
     wa = U(p);
     wb = 2.0 * U(p) - 1.0;
     swa = wa * wa + wb * wb;
@@ -726,7 +732,7 @@ __device__ __forceinline__ int compb2d(const KParams& P, const Geo* g, double* n
   double znus = (1.0 + betb * omeges) * gamm * znues;
   double gams = clampd(1.0 - (znue - znues) / (znu * znus), lim);
   for (;;) {
-    if (++guard > 4 * MAX_REJECT) { LC_ADD(lc, C2D_CNT_ABORTED); break; }
+    if (++guard > 4 * MAX_REJECT) { CB_CNT(C2D_CNT_ABORTED); break; }
     wa = U(p);
     wb = 2.0 * U(p) - 1.0;
     swa = wa * wa + wb * wb;
@@ -1619,6 +1625,7 @@ __device__ __forceinline__ void store_pk(const PktSoA& s, int64_t i, const Pkt& 
   s.jk[i] = ((uint32_t)p.jph << 16) | (uint32_t)p.kph;
   s.bins[i] = p.bins;
   s.ctr[i] = p.ctr;
+  s.sub[i] = p.sub;
   s.key[i] = p.key;
 }
 
@@ -1630,7 +1637,7 @@ __device__ __forceinline__ void load_pk(Pkt& p, const PktSoA& s, int64_t i) {
   p.bins = bn;
   p.ctr = gld(s.ctr + i);
   p.key = gld(s.key + i);
-  p.sub = 0;
+  p.sub = gld(s.sub + i);
 }
 
 }  // namespace
@@ -1752,6 +1759,66 @@ __global__ void __launch_bounds__(SRCBLOCK) C2D_SFX(c2d_source_kernel)(const KPa
 /* ------------------------------------------------------------------ */
 /* scatter secondaries (imctrk2d.f:580-684): one lane per split copy     */
 /* ------------------------------------------------------------------ */
+/* A split3 copy resamples its scatter until the gain exceeds the trigger
+ * (imctrk2d.f:634-648, `goto 215`): attempt k draws from sub-stream k of the
+ * copy's key (c2d_rng.h), so attempts are independent.  The scatter kernel
+ * runs a copy's first SC_K1 attempts on its own lane; a copy still below the
+ * trigger (a gain the electron tail reaches with probability ~1e-3..1e-6)
+ * goes to the hard list, whose copies c2d_scatter_hard_kernel resamples 64
+ * attempts at a time, one wave per copy: a single long chain no longer holds
+ * a whole launch (Compton workload: 98.9 % of the GPU time was one lane's
+ * chain in the scatter kernel, profiles/r09i). */
+#ifndef C2D_SC_K1
+#define C2D_SC_K1 16
+#endif
+constexpr int SC_K1 = C2D_SC_K1;
+
+struct ScatItem {
+  ScatRec rec;
+  uint32_t ii;
+  bool is2;
+};
+__device__ __forceinline__ ScatItem scat_item(const KParams& P, const GenArgs& A, int64_t item) {
+  const int64_t n2items = A.n2_in * P.split2;
+  ScatItem s;
+  s.is2 = item < n2items;
+  if (s.is2) {
+    s.rec = A.q2_in[item / P.split2];
+    s.ii = (uint32_t)(item % P.split2);
+  } else {
+    const int64_t it3 = item - n2items;
+    s.rec = A.q3_in[it3 / P.split3];
+    s.ii = (uint32_t)(it3 % P.split3);
+  }
+  return s;
+}
+
+/* one attempt: the copy's state at the collision, weight ewold, sub-stream k */
+template <int TALLY = 1>
+__device__ __forceinline__ int scat_attempt(const KParams& P, const Geo* g, double* nel, LaneCnt& lc, Pkt& p,
+                                            const ScatRec& rec, uint64_t key, uint32_t k, double ewold) {
+  p.key = key;
+  p.sub = k;
+  p.ctr = 0;
+  load_rec(p, rec);
+  p.ew = ewold;
+  return compb2d<TALLY>(P, g, nel, p, lc);
+}
+
+/* the scattered copy: edep / E_IC, then into the packet store for this
+ * generation's transport launch (imctrk2d.f:649-660, 664-678) */
+__device__ __forceinline__ void scat_emit(const KParams& P, const GenArgs& A, double* eic, Pkt& p, int i_gam,
+                                          double ewold) {
+  const double twopi = 2.0 * PI_REF;
+  const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
+  atomicAdd(&P.T[P.off.edep + cell], p.ew - ewold);
+  atomicAdd(&eic[i_gam], p.ew - ewold);
+  if (p.phi > twopi) p.phi = p.phi - twopi;
+  const unsigned long long slot = wave_reserve(A.n_pk);
+  if (slot < (unsigned long long)P.cap_pk) store_pk(P.pk, (int64_t)slot, p);
+  else gor(P.err, ERR_QUEUE);
+}
+
 __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KParams* __restrict__ Pg,
                                                                      const GenArgs A) {
   const KParams& P = *Pg;
@@ -1768,57 +1835,107 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
   __syncthreads();
   const Geo* g = reinterpret_cast<const Geo*>(geo_lds);
   LaneCnt lc = {0u};
-  const double twopi = 2.0 * PI_REF;
-  const int64_t n2items = A.n2_in * P.split2;
   const int64_t stride = (int64_t)gridDim.x * SBLOCK;
   for (int64_t item = A.item_begin + (int64_t)blockIdx.x * SBLOCK + threadIdx.x; item < A.item_end;
        item += stride) {
-    const bool is2 = item < n2items;
-    ScatRec rec;
-    uint32_t ii;
-    if (is2) {
-      rec = A.q2_in[item / P.split2];
-      ii = (uint32_t)(item % P.split2);
-    } else {
-      const int64_t it3 = item - n2items;
-      rec = A.q3_in[it3 / P.split3];
-      ii = (uint32_t)(it3 % P.split3);
-    }
+    const ScatItem it = scat_item(P, A, item);
     Pkt p;
-    const double ewcsv = rec.ew / P.split2;
+    const double ewcsv = it.rec.ew / P.split2;
     /* split2 copy: ew = ewcsv; split3 copy: ew = ewcsv / split3 (imctrk2d.f:611,636) */
-    const double ewold = is2 ? ewcsv : ewcsv / P.split3;
+    const double ewold = it.is2 ? ewcsv : ewcsv / P.split3;
     const double thr = ewold * P.split2 * P.split1 * P.spl3_trg;
-    p.key = c2d_derive_s(rec.key, is2 ? C2D_TAG_SCAT2 : C2D_TAG_SCAT3, ii, rec.ctr, rec.sub);
-    p.sub = 0;
-    p.ctr = 0;
-    int i_gam = 0, guard = 0;
-    bool third = false;
-    for (;;) {
-      load_rec(p, rec);
-      p.ew = ewold;
-      i_gam = compb2d(P, g, nel_lds, p, lc);
-      if (is2) {
-        third = p.ew > thr;   /* third split (imctrk2d.f:631-661): resampled next generation */
-        break;
+    const uint64_t key = c2d_derive_s(it.rec.key, it.is2 ? C2D_TAG_SCAT2 : C2D_TAG_SCAT3, it.ii, it.rec.ctr,
+                                      it.rec.sub);
+    int i_gam = 0;
+    bool done = true;
+    if (it.is2) {
+      i_gam = scat_attempt(P, g, nel_lds, lc, p, it.rec, key, 0u, ewold);
+      if (p.ew > thr) {   /* third split (imctrk2d.f:631-661): resampled next generation */
+        ScatRec r3 = it.rec;
+        r3.key = p.key;
+        r3.ctr = p.ctr;
+        r3.sub = 0;
+        push_scat(P, A.q3_out, A.n3_out, r3);
+        continue;
       }
-      if (p.ew > thr) break;   /* split3 copies resample until the gain exceeds the trigger */
-      if (++guard > MAX_REJECT) { LC_ADD(lc, C2D_CNT_ABORTED); break; }
-    }
-    if (third) {
-      ScatRec r3 = rec;
-      r3.key = p.key;
-      r3.ctr = p.ctr;
-      r3.sub = 0;
-      push_scat(P, A.q3_out, A.n3_out, r3);
     } else {
-      const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
-      atomicAdd(&P.T[P.off.edep + cell], p.ew - ewold);
-      atomicAdd(&eic_lds[i_gam], p.ew - ewold);
-      if (p.phi > twopi) p.phi = p.phi - twopi;
-      const unsigned long long slot = wave_reserve(A.n_pk);
-      if (slot < (unsigned long long)P.cap_pk) store_pk(P.pk, (int64_t)slot, p);
+      /* split3 copies resample until the gain exceeds the trigger */
+      done = false;
+      for (uint32_t k = 0; k < (uint32_t)SC_K1; k++) {
+        i_gam = scat_attempt(P, g, nel_lds, lc, p, it.rec, key, k, ewold);
+        if (p.ew > thr) { done = true; break; }
+      }
+    }
+    if (done) {
+      scat_emit(P, A, eic_lds, p, i_gam, ewold);
+    } else {
+      const unsigned long long h = wave_reserve(A.n_hard);
+      if (h < (unsigned long long)P.cap_pk) A.hard[h] = item;
       else gor(P.err, ERR_QUEUE);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C2D_NUM_NT + 2; i += SBLOCK) {
+    if (nel_lds[i] != 0.0) atomicAdd(&P.T[P.off.nelectron + i], nel_lds[i]);
+    if (eic_lds[i] != 0.0) atomicAdd(&P.T[P.off.E_IC + i], eic_lds[i]);
+  }
+  flush_counters(P, lc, lane_id());
+}
+
+/* The hard list: one wave per split3 copy, attempts SC_K1 + 64 r + lane in
+ * round r.  Every lane's attempt is tallied (nelectron, compb2d calls) as
+ * it runs; the first success (lowest lane) is the copy's result, and the
+ * lanes after it in that round subtract their attempt's tallies again, so
+ * the sums are those of the sequential loop.  Attempt MAX_REJECT ends the
+ * copy as the sequential guard does (C2D_CNT_ABORTED). */
+__global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_hard_kernel)(const KParams* __restrict__ Pg,
+                                                                          const GenArgs A) {
+  const KParams& P = *Pg;
+  __shared__ double geo_lds[GEO_DOUBLES];
+  __shared__ double nel_lds[C2D_NUM_NT + 2];
+  __shared__ double eic_lds[C2D_NUM_NT + 2];
+  for (int i = threadIdx.x; i < GEO_DOUBLES; i += SBLOCK)
+    geo_lds[i] = reinterpret_cast<const double*>(P.geo)[i];
+  for (int i = threadIdx.x; i < C2D_NUM_NT + 2; i += SBLOCK) {
+    nel_lds[i] = 0.0;
+    eic_lds[i] = 0.0;
+  }
+  init_counters(c2d_cnt_lds);
+  __syncthreads();
+  const Geo* g = reinterpret_cast<const Geo*>(geo_lds);
+  LaneCnt lc = {0u};
+  const uint32_t lane = lane_id();
+  const int wpb = SBLOCK / 64;
+  const int64_t n_hard = (int64_t)rfl64(*A.n_hard);
+  const int64_t n_take = n_hard < P.cap_pk ? n_hard : P.cap_pk;
+  for (int64_t h = (int64_t)blockIdx.x * wpb + (int64_t)(__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
+       h < n_take; h += (int64_t)gridDim.x * wpb) {
+    const ScatItem it = scat_item(P, A, A.hard[h]);
+    const double ewold = it.rec.ew / P.split2 / P.split3;
+    const double thr = ewold * P.split2 * P.split1 * P.spl3_trg;
+    const uint64_t key = c2d_derive_s(it.rec.key, C2D_TAG_SCAT3, it.ii, it.rec.ctr, it.rec.sub);
+    for (uint32_t k0 = (uint32_t)SC_K1;; k0 += 64u) {
+      const uint32_t k = k0 + lane;
+      const bool live = k <= (uint32_t)MAX_REJECT;
+      Pkt p;
+      int i_gam = 0;
+      bool ok = false;
+      if (live) {
+        i_gam = scat_attempt(P, g, nel_lds, lc, p, it.rec, key, k, ewold);
+        ok = p.ew > thr || k == (uint32_t)MAX_REJECT;
+      }
+      const unsigned long long m = __ballot(ok);
+      if (m == 0ull) continue;
+      const uint32_t kf = (uint32_t)(__ffsll((long long)m) - 1);
+      if (live && lane > kf) {                 /* beyond the first success: not run */
+        Pkt q;
+        (void)scat_attempt<-1>(P, g, nel_lds, lc, q, it.rec, key, k, ewold);
+      }
+      if (lane == kf) {
+        if (!(p.ew > thr)) atomicAdd(&c2d_cnt_lds[C2D_CNT_ABORTED], 1u);
+        scat_emit(P, A, eic_lds, p, i_gam, ewold);
+      }
+      break;
     }
   }
   __syncthreads();
@@ -2874,10 +2991,15 @@ extern "C" int C2D_SFX(c2d_launch_source)(const c2d::KParams* P_dev, int grid, h
   return (int)hipGetLastError();
 }
 
+/* the scatter kernel over items [item_begin, item_end), then the hard list
+ * it leaves (A->n_hard zeroed by the caller); hard_grid blocks of SBLOCK */
 extern "C" int C2D_SFX(c2d_launch_scatter)(const c2d::KParams* P_dev, const c2d::GenArgs* A, int grid,
-                                           hipStream_t stream) {
+                                           int hard_grid, hipStream_t stream) {
   hipLaunchKernelGGL(C2D_SFX(c2d::c2d_scatter_kernel), dim3(grid), dim3(c2d::SBLOCK), 0, stream, P_dev,
                      *A);
+  if (hipError_t e = hipGetLastError()) return (int)e;
+  hipLaunchKernelGGL(C2D_SFX(c2d::c2d_scatter_hard_kernel), dim3(hard_grid), dim3(c2d::SBLOCK), 0, stream,
+                     P_dev, *A);
   return (int)hipGetLastError();
 }
 

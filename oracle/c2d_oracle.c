@@ -728,9 +728,19 @@ static void collision(c2o_ctx* c, pkt_t* p, int scat_flag, rng_t* g) {
       for (int ii2 = 0; ii2 < c->split3; ii2++) {
         rng_t g3 = rng_child(&gc, C2D_TAG_SCAT3, (uint32_t)ii2, ctr_chd);
         rng_t* g3p = (gc.mode == C2O_RNG_LINEAGE) ? &g3 : &gc;
+        /* lineage mode: resample k draws from sub-stream k of the copy's key
+         * (c2d_rng.h), so the attempts are independent of one another and the
+         * GPU evaluates them in parallel (transport.hip scatter kernels);
+         * the packet flies on from the first success's stream */
+        uint32_t attempt = 0;
         do {
           *p = csv;
           p->ew = ewcsv / c->split3;
+          if (gc.mode == C2O_RNG_LINEAGE) {
+            g3.sub = attempt;
+            g3.ctr = 0;
+          }
+          attempt++;
           i_gam = compb2d(c, p, g3p);
         } while (p->ew <= ewold * c->split2 * c->split1 * c->spl3_trg);
         int cell = CELL(c, p->jph, p->kph);
