@@ -358,16 +358,18 @@ def build_c3(args, rank, world, local, dev, sources, ccap, ecap, mode):
     ex, ex_desc = tally_exchange(eng, T, rank, world, dev)
     from compton2d_amd import abi
     fpm = {"auto": abi.FP_AUTO, "exact": abi.FP_EXACT, "fast": abi.FP_FAST}[args.fp_mode]
-    run = CoupledRun(eng, wl, device_resident=not args.host_tables, allreduce=ex, fp_mode=fpm)
     # C3's named output: the step's escapes binned into the observer-frame SED
     # of postprocessing/mrk421_sed.input (pspt.c:245-294) on the device, from
-    # the event buffer the transport just wrote (no event text, no download)
+    # the event buffer the transport just wrote (no event text, no download),
+    # on a second stream beside the census close, the FP update and the next
+    # step's tables
     from compton2d_amd import observer
     eng.obs_begin(observer.mrk421_sed_binning())
+    run = CoupledRun(eng, wl, device_resident=not args.host_tables, allreduce=ex, fp_mode=fpm,
+                     after_transport=lambda: eng.obs_accumulate(None))
 
     def one_step():
         r = dict(run.step())
-        eng.obs_accumulate(None)
         r["census_records"] = float(eng.census_count())
         r["escape_events"] = float(eng.last_event_count())
         return r

@@ -32,11 +32,16 @@ class CoupledRun:
     """Advance a CoupledWorkload one MC step at a time on `eng`."""
 
     def __init__(self, eng: Engine, wl: CoupledWorkload, device_resident: bool = True,
-                 allreduce: Optional[Callable[[], None]] = None, fp_mode: int = abi.FP_AUTO):
+                 allreduce: Optional[Callable[[], None]] = None, fp_mode: int = abi.FP_AUTO,
+                 after_transport: Optional[Callable[[], None]] = None):
         """fp_mode: the FP update's arithmetic (Engine.fp_set_mode); the
         default abi.FP_AUTO picks exact or fast per update, and each step's
-        row logs what ran (`fp_mode`)."""
+        row logs what ran (`fp_mode`).  after_transport: called as soon as a
+        step's transport has returned, before the tally exchange and the FP
+        update (e.g. the on-device SED binning of the step's escapes, which
+        then runs on its own stream beside them)."""
         self.eng, self.wl = eng, wl
+        self.after_transport = after_transport
         self.device_resident = device_resident
         self.allreduce = allreduce
         self.state = {k: np.array(v, copy=True) for k, v in wl.state0.items()}
@@ -82,6 +87,8 @@ class CoupledRun:
             ewsurfo=zz, nsurfu=izr, nsurfl=izr, ewsurfu=zr, ewsurfl=zr, tbbi=zz, tbbo=zz,
             tbbu=zr, tbbl=zr)
         eng.transport_step(si)
+        if self.after_transport is not None:
+            self.after_transport()
         t2 = _time.perf_counter()
         if self.allreduce is not None:
             self.allreduce()
