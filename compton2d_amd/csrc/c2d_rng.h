@@ -36,6 +36,10 @@
  *   its resample k   = (K_split3, sub k), counter 0 at each attempt    (imctrk2d.f:634-648,
  *                      `goto 215`); the copy flies on from its first success's stream
  *   census key       = census_key(K_pkt, ctr_pkt, sub_pkt)             (imctrk2d.f:571)
+ *   compb2d's first rejection loop (compb_2d.f:59-93): iteration j draws
+ *                      counters c0 + 5j .. c0 + 5j + 4 of the packet's stream (c0:
+ *                      the counter at the call), the rest of compb2d follows
+ *                      c0 + 5 (j_accepted + 1)
  * Draw n of (key, sub) = u53(mix64(key + gamma * ((sub << 32 | n) + 1)));
  * derive(key, tag, a, b; sub) = Philox_key({a, b, tag | sub << 8, C_DERIVE}).
  */

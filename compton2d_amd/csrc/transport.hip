@@ -649,62 +649,164 @@ __device__ __forceinline__ int cdf_index(const double* cdf /*0-based*/, int n, d
 /* ------------------------------------------------------------------ */
 /* nth2d (src/nontherm2d.f:159-183) + compb2d (src/compb_2d.f:1-318)    */
 /* ------------------------------------------------------------------ */
-/* TALLY = +1: the call's nelectron samples and counters are added; -1: the
- * same call subtracts them again (a speculative split3 attempt beyond the
- * first success, c2d_scatter_hard_kernel) */
+/* compb2d in three parts, so that its first rejection loop (electron +
+ * Klein-Nishina acceptance, compb_2d.f:59-93) can run wave-parallel when it
+ * is long (acceptance ~1e-5 for photons deep in the KN regime):
+ *   kn_loop   a lane's own iterations, at most `cap` of them;
+ *   kn_coop   wave-uniform: every lane left without an acceptance is resolved
+ *             by the whole wave, 64 iterations per round;
+ *   compb2d_b the rest of the scatter (:98-307).
+ * Iteration j of the first loop draws its five uniforms from positions
+ * ctrA + 5j .. ctrA + 5j + 4 of the packet's stream (ctrA: the counter at
+ * the loop's start; an iteration that skips at znue < 1e-10 leaves its fifth
+ * unused), so iterations are independent; the oracle's lineage mode draws
+ * the same (oracle/c2d_oracle.c compb2d).
+ * TALLY = +1: the nelectron samples and counters are added; -1: subtracted
+ * again (a speculative split3 attempt beyond the first success,
+ * c2d_scatter_hard_kernel). */
 #define CB_CNT(w) do { if (TALLY > 0) atomicAdd(&c2d_cnt_lds[w], 1u); else atomicSub(&c2d_cnt_lds[w], 1u); } while (0)
-template <int TALLY = 1>
-__device__ __forceinline__ int compb2d(const KParams& P, const Geo* g, double* nel, Pkt& p, LaneCnt& lc) {
-  const double fuzz = 1.0e-10, lim = 9.9999999e-1;
+#ifndef C2D_KN_CAP
+#define C2D_KN_CAP 32
+#endif
+struct KnState {
+  double gamm, betb, omeg, znue;
+  int i;            /* electron bin (i_gam) */
+  uint32_t ctrA;    /* the packet's counter at the loop's start */
+  int j;            /* iterations run (the next one to run) */
+};
+
+/* iteration j of the first loop; true if accepted */
+__device__ __forceinline__ bool kn_iter(const KParams& P, Pkt& p, uint32_t ctrA, int j, double znu,
+                                        KnState& st) {
+  const double lim = 9.9999999e-1;
   const int cell = (p.jph - 1) * P.nr + (p.kph - 1);
   const double* Pc = P.Pnt + (int64_t)cell * C2D_NUM_NT;
-  double znu = p.xnu / EMASSKEV;
-  double gamm, betb, omeg, tl, tr, znue, betz, xknot;
-  double sz, games, phat, znues, wa, wb, swa;
-  int i_gam;
-  int guard = 0;
-  (void)lc;
-  CB_CNT(C2D_CNT_COMPB);
-  for (;;) {
-    if (++guard > MAX_REJECT) { CB_CNT(C2D_CNT_ABORTED); break; }
-    /* nth2d */
-    double rnum = U(p);
-    rnum = (double)(int32_t)(rnum * 1.0e6) / 1.0e6 + 1.0e-6 * U(p);
-    int i = 2;
-    {   /* first i in 2..200 with Pnt(i) > rnum, else 201 (bisection on the CDF) */
-      int lo = 2, hi = C2D_NUM_NT + 1;
-      while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (Pc[mid - 1] > rnum) hi = mid;
-        else lo = mid + 1;
-      }
-      i = lo > C2D_NUM_NT ? C2D_NUM_NT : lo;   /* Pnt(200) = 1 > rnum in valid input */
+  p.ctr = ctrA + 5u * (uint32_t)j;
+  /* nth2d (nontherm2d.f:159-183) */
+  double rnum = U(p);
+  rnum = (double)(int32_t)(rnum * 1.0e6) / 1.0e6 + 1.0e-6 * U(p);
+  int i = 2;
+  {   /* first i in 2..200 with Pnt(i) > rnum, else 201 (bisection on the CDF) */
+    int lo = 2, hi = C2D_NUM_NT + 1;
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      if (Pc[mid - 1] > rnum) hi = mid;
+      else lo = mid + 1;
     }
-    gamm = __builtin_sqrt(P.gnt[i - 1] * P.gnt[i - 2]) + 1.0;
-    betb = __builtin_sqrt(1.0 - 1.0 / (gamm * gamm));
-    atomicAdd(&nel[i], (double)TALLY);
-    i_gam = i;
-    omeg = 2.0 * U(p) - 1.0;
-    omeg = clampd(omeg, lim);
-    tl = U(p);
-    tr = 0.5 * (1.0 - betb * omeg);
-    if (tl > tr) omeg = -omeg;
-    omeg = clampd(omeg, lim);
-    znue = (1.0 - betb * omeg) * znu * gamm;
-    if (znue < 1.0e-10) continue;
-    if (znue <= 1.0e-2) {
-      xknot = 1.0 - znue * (2.0 - znue * (5.2 - znue * (13.3 - 1.144e3 * znue / 3.5e1)));
-    } else {
-      double znue3 = znue * znue * znue;
-      betz = 1.0 + 2.0 * znue;
-      double gamz = znue * (znue - 2.0) - 2.0;
-      double xxx = 4.0 * znue + 2.0 * znue3 * (1.0 + znue) / (betz * betz) + gamz * c2d_log(betz);
-      xknot = 3.75e-1 * xxx / znue3;
-    }
-    if (U(p) > xknot) continue;
-    break;
+    i = lo > C2D_NUM_NT ? C2D_NUM_NT : lo;   /* Pnt(200) = 1 > rnum in valid input */
   }
-  betz = 1.0 + 2.0 * znue;
+  const double gamm = __builtin_sqrt(P.gnt[i - 1] * P.gnt[i - 2]) + 1.0;
+  const double betb = __builtin_sqrt(1.0 - 1.0 / (gamm * gamm));
+  double omeg = 2.0 * U(p) - 1.0;
+  omeg = clampd(omeg, lim);
+  const double tl = U(p);
+  const double tr = 0.5 * (1.0 - betb * omeg);
+  if (tl > tr) omeg = -omeg;
+  omeg = clampd(omeg, lim);
+  const double znue = (1.0 - betb * omeg) * znu * gamm;
+  st.i = i; st.gamm = gamm; st.betb = betb; st.omeg = omeg; st.znue = znue;
+  if (znue < 1.0e-10) return false;
+  double xknot;
+  if (znue <= 1.0e-2) {
+    xknot = 1.0 - znue * (2.0 - znue * (5.2 - znue * (13.3 - 1.144e3 * znue / 3.5e1)));
+  } else {
+    double znue3 = znue * znue * znue;
+    double betz = 1.0 + 2.0 * znue;
+    double gamz = znue * (znue - 2.0) - 2.0;
+    double xxx = 4.0 * znue + 2.0 * znue3 * (1.0 + znue) / (betz * betz) + gamz * c2d_log(betz);
+    xknot = 3.75e-1 * xxx / znue3;
+  }
+  p.ctr = ctrA + 5u * (uint32_t)j + 4u;
+  return !(U(p) > xknot);
+}
+
+/* a lane's own iterations of the first loop, at most cap; true when one was
+ * accepted (p.ctr then follows it) */
+template <int TALLY = 1>
+__device__ __forceinline__ bool kn_loop(const KParams& P, double* nel, Pkt& p, KnState& st, int cap) {
+  CB_CNT(C2D_CNT_COMPB);
+  st.ctrA = p.ctr;
+  st.j = 0;
+  const double znu = p.xnu / EMASSKEV;
+  for (; st.j < cap; st.j++) {
+    const bool ok = kn_iter(P, p, st.ctrA, st.j, znu, st);
+    atomicAdd(&nel[st.i], (double)TALLY);
+    if (ok) {
+      st.j++;
+      p.ctr = st.ctrA + 5u * (uint32_t)st.j;
+      return true;
+    }
+  }
+  return false;
+}
+
+__device__ __forceinline__ double rl_d(double v, uint32_t l) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+/* wave-uniform: every lane with `need` (its kn_loop ran out of iterations)
+ * is resolved by the whole wave, lane after lane, 64 iterations per round;
+ * iteration MAX_REJECT - 1 ends a loop the reference would not end
+ * (C2D_CNT_ABORTED, as the sequential guard) */
+template <int TALLY = 1>
+__device__ __forceinline__ void kn_coop(const KParams& P, double* nel, Pkt& p, KnState& st, bool& need) {
+  const uint32_t lane = lane_id();
+  for (;;) {
+    const unsigned long long m = __ballot(need);
+    if (m == 0ull) break;
+    const uint32_t L = (uint32_t)(__ffsll((long long)m) - 1);
+    /* the owner's packet as the iterations read it */
+    Pkt q;
+    /* readlane returns int: through uint32_t, so the low word is not sign-extended */
+    q.key = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)p.key, L) |
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(p.key >> 32), L) << 32);
+    q.sub = __builtin_amdgcn_readlane(p.sub, L);
+    q.jph = __builtin_amdgcn_readlane(p.jph, L);
+    q.kph = __builtin_amdgcn_readlane(p.kph, L);
+    const double znu = rl_d(p.xnu, L) / EMASSKEV;
+    const uint32_t ctrA = __builtin_amdgcn_readlane(st.ctrA, L);
+    int j0 = __builtin_amdgcn_readlane(st.j, L);
+    for (;;) {
+      const int j = j0 + (int)lane;
+      KnState t;
+      t.i = 0; t.gamm = t.betb = t.omeg = t.znue = 0.0;
+      const bool live = j < MAX_REJECT;
+      const bool acc = live && kn_iter(P, q, ctrA, j, znu, t);
+      const bool ok = acc || j == MAX_REJECT - 1;
+      const unsigned long long ma = __ballot(ok);
+      const uint32_t jf = ma ? (uint32_t)(__ffsll((long long)ma) - 1) : 64u;
+      if (live && lane <= jf) atomicAdd(&nel[t.i], (double)TALLY);
+      if (ma) {
+        const bool abort = __builtin_amdgcn_readlane((uint32_t)(!acc), jf) != 0u;
+        const double gamm = rl_d(t.gamm, jf), betb = rl_d(t.betb, jf);
+        const double omeg = rl_d(t.omeg, jf), znue = rl_d(t.znue, jf);
+        const int ii = __builtin_amdgcn_readlane(t.i, jf);
+        if (lane == L) {
+          st.gamm = gamm; st.betb = betb; st.omeg = omeg; st.znue = znue; st.i = ii;
+          st.j = j0 + (int)jf + 1;
+          p.ctr = ctrA + 5u * (uint32_t)st.j;
+          need = false;
+          if (abort) CB_CNT(C2D_CNT_ABORTED);
+        }
+        break;
+      }
+      j0 += 64;
+    }
+  }
+}
+
+/* the rest of compb2d (:98-307) from the accepted electron */
+template <int TALLY = 1>
+__device__ __forceinline__ int compb2d_b(const KParams& P, const Geo* g, Pkt& p, const KnState& st) {
+  const double fuzz = 1.0e-10, lim = 9.9999999e-1;
+  const double znu = p.xnu / EMASSKEV;
+  const double gamm = st.gamm, betb = st.betb, omeg = st.omeg, znue = st.znue;
+  double sz, games, phat, znues, wa, wb, swa, tr;
+  int guard = st.j;
+  const double betz = 1.0 + 2.0 * znue;
   for (;;) {
     if (++guard > 2 * MAX_REJECT) { CB_CNT(C2D_CNT_ABORTED); break; }
     sz = (1.0 + 2.0 * znue * U(p)) / betz;
@@ -755,6 +857,21 @@ __device__ __forceinline__ int compb2d(const KParams& P, const Geo* g, double* n
   p.xnu = xnus;
   p.wmu = wmus;
   p.phi = phis;
+  return st.i;
+}
+
+/* wave-uniform compb2d (imctrk2d.f's `call compb2d`, compb_2d.f:1-318): every
+ * lane calls it; lanes with run = false take no part but the wave's
+ * cooperation.  Returns i_gam for running lanes. */
+template <int TALLY = 1>
+__device__ __forceinline__ int compb2d_w(const KParams& P, const Geo* g, double* nel, Pkt& p, bool run) {
+  KnState st;
+  st.i = 0; st.j = 0; st.ctrA = 0;
+  bool need = false;
+  if (run) need = !kn_loop<TALLY>(P, nel, p, st, C2D_KN_CAP);
+  kn_coop<TALLY>(P, nel, p, st, need);
+  int i_gam = 0;
+  if (run) i_gam = compb2d_b<TALLY>(P, g, p, st);
   return i_gam;
 }
 
@@ -1793,16 +1910,20 @@ __device__ __forceinline__ ScatItem scat_item(const KParams& P, const GenArgs& A
   return s;
 }
 
-/* one attempt: the copy's state at the collision, weight ewold, sub-stream k */
+/* one attempt (wave-uniform call): the copy's state at the collision,
+ * weight ewold, sub-stream k; lanes with run = false only cooperate */
 template <int TALLY = 1>
-__device__ __forceinline__ int scat_attempt(const KParams& P, const Geo* g, double* nel, LaneCnt& lc, Pkt& p,
-                                            const ScatRec& rec, uint64_t key, uint32_t k, double ewold) {
-  p.key = key;
-  p.sub = k;
-  p.ctr = 0;
-  load_rec(p, rec);
-  p.ew = ewold;
-  return compb2d<TALLY>(P, g, nel, p, lc);
+__device__ __forceinline__ int scat_attempt(const KParams& P, const Geo* g, double* nel, Pkt& p,
+                                            const ScatRec& rec, uint64_t key, uint32_t k, double ewold,
+                                            bool run) {
+  if (run) {
+    p.key = key;
+    p.sub = k;
+    p.ctr = 0;
+    load_rec(p, rec);
+    p.ew = ewold;
+  }
+  return compb2d_w<TALLY>(P, g, nel, p, run);
 }
 
 /* the scattered copy: edep / E_IC, then into the packet store for this
@@ -1836,37 +1957,53 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
   const Geo* g = reinterpret_cast<const Geo*>(geo_lds);
   LaneCnt lc = {0u};
   const int64_t stride = (int64_t)gridDim.x * SBLOCK;
-  for (int64_t item = A.item_begin + (int64_t)blockIdx.x * SBLOCK + threadIdx.x; item < A.item_end;
-       item += stride) {
-    const ScatItem it = scat_item(P, A, item);
+  const uint32_t lane = lane_id();
+  /* wave-uniform trip count: compb2d_w cooperates across the wave */
+  for (int64_t base = A.item_begin + (int64_t)blockIdx.x * SBLOCK +
+                      (int64_t)(__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+       base < A.item_end; base += stride) {
+    const int64_t item = base + lane;
+    const bool act = item < A.item_end;
+    ScatItem it;
+    it.is2 = true; it.ii = 0;
+    double ewold = 0.0, thr = 0.0;
+    uint64_t key = 0;
+    if (act) {
+      it = scat_item(P, A, item);
+      const double ewcsv = it.rec.ew / P.split2;
+      /* split2 copy: ew = ewcsv; split3 copy: ew = ewcsv / split3 (imctrk2d.f:611,636) */
+      ewold = it.is2 ? ewcsv : ewcsv / P.split3;
+      thr = ewold * P.split2 * P.split1 * P.spl3_trg;
+      key = c2d_derive_s(it.rec.key, it.is2 ? C2D_TAG_SCAT2 : C2D_TAG_SCAT3, it.ii, it.rec.ctr, it.rec.sub);
+    }
+    /* a split2 copy: one scatter; a split3 copy: resamples until the gain
+     * exceeds the trigger, its first SC_K1 attempts here */
     Pkt p;
-    const double ewcsv = it.rec.ew / P.split2;
-    /* split2 copy: ew = ewcsv; split3 copy: ew = ewcsv / split3 (imctrk2d.f:611,636) */
-    const double ewold = it.is2 ? ewcsv : ewcsv / P.split3;
-    const double thr = ewold * P.split2 * P.split1 * P.spl3_trg;
-    const uint64_t key = c2d_derive_s(it.rec.key, it.is2 ? C2D_TAG_SCAT2 : C2D_TAG_SCAT3, it.ii, it.rec.ctr,
-                                      it.rec.sub);
     int i_gam = 0;
-    bool done = true;
-    if (it.is2) {
-      i_gam = scat_attempt(P, g, nel_lds, lc, p, it.rec, key, 0u, ewold);
-      if (p.ew > thr) {   /* third split (imctrk2d.f:631-661): resampled next generation */
-        ScatRec r3 = it.rec;
-        r3.key = p.key;
-        r3.ctr = p.ctr;
-        r3.sub = 0;
-        push_scat(P, A.q3_out, A.n3_out, r3);
-        continue;
+    bool pending = act, done = false;
+    for (uint32_t k = 0; k < (uint32_t)SC_K1; k++) {
+      if (__ballot(pending) == 0ull) break;
+      if (pending) {
+        p.key = key;
+        p.sub = k;
+        p.ctr = 0;
+        load_rec(p, it.rec);
+        p.ew = ewold;
       }
-    } else {
-      /* split3 copies resample until the gain exceeds the trigger */
-      done = false;
-      for (uint32_t k = 0; k < (uint32_t)SC_K1; k++) {
-        i_gam = scat_attempt(P, g, nel_lds, lc, p, it.rec, key, k, ewold);
-        if (p.ew > thr) { done = true; break; }
+      const int ig = compb2d_w(P, g, nel_lds, p, pending);
+      if (pending) {
+        i_gam = ig;
+        if (it.is2 || p.ew > thr) { done = true; pending = false; }
       }
     }
-    if (done) {
+    if (!act) continue;
+    if (it.is2 && p.ew > thr) {   /* third split (imctrk2d.f:631-661): resampled next generation */
+      ScatRec r3 = it.rec;
+      r3.key = p.key;
+      r3.ctr = p.ctr;
+      r3.sub = 0;
+      push_scat(P, A.q3_out, A.n3_out, r3);
+    } else if (done) {
       scat_emit(P, A, eic_lds, p, i_gam, ewold);
     } else {
       const unsigned long long h = wave_reserve(A.n_hard);
@@ -1918,18 +2055,14 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_hard_kernel)(const
       const uint32_t k = k0 + lane;
       const bool live = k <= (uint32_t)MAX_REJECT;
       Pkt p;
-      int i_gam = 0;
-      bool ok = false;
-      if (live) {
-        i_gam = scat_attempt(P, g, nel_lds, lc, p, it.rec, key, k, ewold);
-        ok = p.ew > thr || k == (uint32_t)MAX_REJECT;
-      }
+      const int i_gam = scat_attempt(P, g, nel_lds, p, it.rec, key, k, ewold, live);
+      const bool ok = live && (p.ew > thr || k == (uint32_t)MAX_REJECT);
       const unsigned long long m = __ballot(ok);
       if (m == 0ull) continue;
       const uint32_t kf = (uint32_t)(__ffsll((long long)m) - 1);
-      if (live && lane > kf) {                 /* beyond the first success: not run */
+      {                                        /* beyond the first success: not run */
         Pkt q;
-        (void)scat_attempt<-1>(P, g, nel_lds, lc, q, it.rec, key, k, ewold);
+        (void)scat_attempt<-1>(P, g, nel_lds, q, it.rec, key, k, ewold, live && lane > kf);
       }
       if (lane == kf) {
         if (!(p.ew > thr)) atomicAdd(&c2d_cnt_lds[C2D_CNT_ABORTED], 1u);

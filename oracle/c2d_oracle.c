@@ -531,7 +531,13 @@ static int compb2d(c2o_ctx* c, pkt_t* p, rng_t* g) {
   double cazs, wmus, xnus, cosdphi, dphi, phis;
   int i_gam;
   TALLY(c, counters + C2D_CNT_COMPB) += 1.0;
-  for (;;) {                                            /* label 100 */
+  /* lineage mode: iteration j of label 100 draws from counters ctr0 + 5j ..
+   * ctr0 + 5j + 4 (a znue < 1e-10 skip leaves the fifth unused), so that the
+   * GPU can run iterations of one packet wave-parallel (transport.hip kn_iter) */
+  const uint32_t ctr0 = g->ctr;
+  uint32_t jit = 0;
+  for (;; jit++) {                                      /* label 100 */
+    if (g->mode == C2O_RNG_LINEAGE) g->ctr = ctr0 + 5u * jit;
     i_gam = nth2d(c, cell, g, &gamm, &betb);
     omeg = 2.0 * U(g) - 1.0;
     omeg = clampd(omeg, lim);
@@ -553,6 +559,7 @@ static int compb2d(c2o_ctx* c, pkt_t* p, rng_t* g) {
     if (U(g) > xknot) continue;
     break;
   }
+  if (g->mode == C2O_RNG_LINEAGE) g->ctr = ctr0 + 5u * (jit + 1u);
   betz = 1.0 + 2.0 * znue;
   for (;;) {                                            /* labels 200/202 */
     sz = (1.0 + 2.0 * znue * U(g)) / betz;
