@@ -335,6 +335,9 @@ struct KParams {
 #define C2D_CDF_GUIDE 256
 
 /* Per-launch arguments (passed by value; KParams stays constant over a step). */
+/* scatter kernels' defaults (GenArgs.kn_cap, GenArgs.sc_k1; transport.hip) */
+#define C2D_KN_CAP_DEFAULT 32
+#define C2D_SC_K1_DEFAULT 16
 struct GenArgs {
   const ScatRec* q2_in;            /* scatter kernel: this generation's records   */
   const ScatRec* q3_in;
@@ -351,6 +354,10 @@ struct GenArgs {
   int64_t n_items;                 /* transport, generation 0: census + sources    */
   int64_t n2_in, n3_in;
   int32_t gen;
+  int32_t kn_cap;                  /* scatter: compb2d first-loop iterations a lane runs alone
+                                      before the wave resolves it (C2D_KN_CAP_ITERS test knob) */
+  int32_t sc_k1;                   /* scatter: split3 attempts per lane before the hard list
+                                      (C2D_SC_K1_ATTEMPTS test knob) */
 };
 
 /* ---- emission / absorption tables (vem.hip) ---- */

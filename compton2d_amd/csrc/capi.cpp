@@ -1506,6 +1506,11 @@ static int run_step_body(c2d_ctx* c) {
      * C2D_PK_CHUNK: fewer, so a small case runs the chunked loop */
     int64_t pk_chunk = c->pk.cap;
     if (const char* e = getenv("C2D_PK_CHUNK")) pk_chunk = std::max<int64_t>(1, std::min<int64_t>(pk_chunk, atoll(e)));
+    /* test knobs: 0 sends every compb2d first loop to the wave's cooperative
+     * resolution, and every split3 copy to the hard kernel */
+    int32_t kn_cap = C2D_KN_CAP_DEFAULT, sc_k1 = C2D_SC_K1_DEFAULT;
+    if (const char* e = getenv("C2D_KN_CAP_ITERS")) kn_cap = (int32_t)std::max(0, std::min(1 << 20, atoi(e)));
+    if (const char* e = getenv("C2D_SC_K1_ATTEMPTS")) sc_k1 = (int32_t)std::max(0, std::min(1 << 20, atoi(e)));
     for (int64_t b = 0; b < total; b += pk_chunk) {
       const int64_t e = std::min<int64_t>(total, b + pk_chunk);
       HIPCHK(c, hipMemsetAsync(c->ctl + CTL_NPK, 0, sizeof(unsigned long long), c->stream));
@@ -1522,6 +1527,7 @@ static int run_step_body(c2d_ctx* c) {
       A.hard = c->pk.hard;
       A.item_begin = b; A.item_end = e;
       A.n2_in = n2; A.n3_in = n3;
+      A.kn_cap = kn_cap; A.sc_k1 = sc_k1;
       int rc = launch_sc(c->dP, &A, aux_grid(e - b, c->sc_grid), 2 * c->n_cu, c->stream);
       if (rc) return fail(c, C2D_E_HIP, "scatter launch (gen %d): %s", gen, hipGetErrorString((hipError_t)rc));
       rc = launch_tr(c->dP, &A, tr_grid(e - b), c->lds_bytes, cfg.trk_variant, c->stream);

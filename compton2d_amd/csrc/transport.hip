@@ -665,9 +665,7 @@ __device__ __forceinline__ int cdf_index(const double* cdf /*0-based*/, int n, d
  * again (a speculative split3 attempt beyond the first success,
  * c2d_scatter_hard_kernel). */
 #define CB_CNT(w) do { if (TALLY > 0) atomicAdd(&c2d_cnt_lds[w], 1u); else atomicSub(&c2d_cnt_lds[w], 1u); } while (0)
-#ifndef C2D_KN_CAP
-#define C2D_KN_CAP 32
-#endif
+
 struct KnState {
   double gamm, betb, omeg, znue;
   int i;            /* electron bin (i_gam) */
@@ -864,11 +862,12 @@ __device__ __forceinline__ int compb2d_b(const KParams& P, const Geo* g, Pkt& p,
  * lane calls it; lanes with run = false take no part but the wave's
  * cooperation.  Returns i_gam for running lanes. */
 template <int TALLY = 1>
-__device__ __forceinline__ int compb2d_w(const KParams& P, const Geo* g, double* nel, Pkt& p, bool run) {
+__device__ __forceinline__ int compb2d_w(const KParams& P, const Geo* g, double* nel, Pkt& p, bool run,
+                                          int kn_cap) {
   KnState st;
   st.i = 0; st.j = 0; st.ctrA = 0;
   bool need = false;
-  if (run) need = !kn_loop<TALLY>(P, nel, p, st, C2D_KN_CAP);
+  if (run) need = !kn_loop<TALLY>(P, nel, p, st, kn_cap);
   kn_coop<TALLY>(P, nel, p, st, need);
   int i_gam = 0;
   if (run) i_gam = compb2d_b<TALLY>(P, g, p, st);
@@ -1879,16 +1878,12 @@ __global__ void __launch_bounds__(SRCBLOCK) C2D_SFX(c2d_source_kernel)(const KPa
 /* A split3 copy resamples its scatter until the gain exceeds the trigger
  * (imctrk2d.f:634-648, `goto 215`): attempt k draws from sub-stream k of the
  * copy's key (c2d_rng.h), so attempts are independent.  The scatter kernel
- * runs a copy's first SC_K1 attempts on its own lane; a copy still below the
+ * runs a copy's first GenArgs.sc_k1 (16) attempts on its own lane; a copy still below the
  * trigger (a gain the electron tail reaches with probability ~1e-3..1e-6)
  * goes to the hard list, whose copies c2d_scatter_hard_kernel resamples 64
  * attempts at a time, one wave per copy: a single long chain no longer holds
  * a whole launch (Compton workload: 98.9 % of the GPU time was one lane's
  * chain in the scatter kernel, profiles/r09i). */
-#ifndef C2D_SC_K1
-#define C2D_SC_K1 16
-#endif
-constexpr int SC_K1 = C2D_SC_K1;
 
 struct ScatItem {
   ScatRec rec;
@@ -1915,7 +1910,7 @@ __device__ __forceinline__ ScatItem scat_item(const KParams& P, const GenArgs& A
 template <int TALLY = 1>
 __device__ __forceinline__ int scat_attempt(const KParams& P, const Geo* g, double* nel, Pkt& p,
                                             const ScatRec& rec, uint64_t key, uint32_t k, double ewold,
-                                            bool run) {
+                                            bool run, int kn_cap) {
   if (run) {
     p.key = key;
     p.sub = k;
@@ -1923,7 +1918,7 @@ __device__ __forceinline__ int scat_attempt(const KParams& P, const Geo* g, doub
     load_rec(p, rec);
     p.ew = ewold;
   }
-  return compb2d_w<TALLY>(P, g, nel, p, run);
+  return compb2d_w<TALLY>(P, g, nel, p, run, kn_cap);
 }
 
 /* the scattered copy: edep / E_IC, then into the packet store for this
@@ -1958,6 +1953,9 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
   LaneCnt lc = {0u};
   const int64_t stride = (int64_t)gridDim.x * SBLOCK;
   const uint32_t lane = lane_id();
+  /* split2 copies: one attempt; split3 copies: A.sc_k1 here (0: all to the hard list) */
+  const uint32_t sc_k1 = (uint32_t)A.sc_k1;
+  const uint32_t k_loop = sc_k1 > 1u ? sc_k1 : 1u;
   /* wave-uniform trip count: compb2d_w cooperates across the wave */
   for (int64_t base = A.item_begin + (int64_t)blockIdx.x * SBLOCK +
                       (int64_t)(__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
@@ -1977,11 +1975,11 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
       key = c2d_derive_s(it.rec.key, it.is2 ? C2D_TAG_SCAT2 : C2D_TAG_SCAT3, it.ii, it.rec.ctr, it.rec.sub);
     }
     /* a split2 copy: one scatter; a split3 copy: resamples until the gain
-     * exceeds the trigger, its first SC_K1 attempts here */
+     * exceeds the trigger, its first sc_k1 attempts here */
     Pkt p;
     int i_gam = 0;
-    bool pending = act, done = false;
-    for (uint32_t k = 0; k < (uint32_t)SC_K1; k++) {
+    bool pending = act && (it.is2 || sc_k1 > 0u), done = false;
+    for (uint32_t k = 0; k < k_loop; k++) {
       if (__ballot(pending) == 0ull) break;
       if (pending) {
         p.key = key;
@@ -1990,10 +1988,11 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
         load_rec(p, it.rec);
         p.ew = ewold;
       }
-      const int ig = compb2d_w(P, g, nel_lds, p, pending);
+      const int ig = compb2d_w(P, g, nel_lds, p, pending, A.kn_cap);
       if (pending) {
         i_gam = ig;
         if (it.is2 || p.ew > thr) { done = true; pending = false; }
+        else if (k + 1u >= sc_k1) pending = false;
       }
     }
     if (!act) continue;
@@ -2019,7 +2018,7 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_kernel)(const KPar
   flush_counters(P, lc, lane_id());
 }
 
-/* The hard list: one wave per split3 copy, attempts SC_K1 + 64 r + lane in
+/* The hard list: one wave per split3 copy, attempts sc_k1 + 64 r + lane in
  * round r.  Every lane's attempt is tallied (nelectron, compb2d calls) as
  * it runs; the first success (lowest lane) is the copy's result, and the
  * lanes after it in that round subtract their attempt's tallies again, so
@@ -2051,18 +2050,18 @@ __global__ void __launch_bounds__(SBLOCK) C2D_SFX(c2d_scatter_hard_kernel)(const
     const double ewold = it.rec.ew / P.split2 / P.split3;
     const double thr = ewold * P.split2 * P.split1 * P.spl3_trg;
     const uint64_t key = c2d_derive_s(it.rec.key, C2D_TAG_SCAT3, it.ii, it.rec.ctr, it.rec.sub);
-    for (uint32_t k0 = (uint32_t)SC_K1;; k0 += 64u) {
+    for (uint32_t k0 = (uint32_t)A.sc_k1;; k0 += 64u) {
       const uint32_t k = k0 + lane;
       const bool live = k <= (uint32_t)MAX_REJECT;
       Pkt p;
-      const int i_gam = scat_attempt(P, g, nel_lds, p, it.rec, key, k, ewold, live);
+      const int i_gam = scat_attempt(P, g, nel_lds, p, it.rec, key, k, ewold, live, A.kn_cap);
       const bool ok = live && (p.ew > thr || k == (uint32_t)MAX_REJECT);
       const unsigned long long m = __ballot(ok);
       if (m == 0ull) continue;
       const uint32_t kf = (uint32_t)(__ffsll((long long)m) - 1);
       {                                        /* beyond the first success: not run */
         Pkt q;
-        (void)scat_attempt<-1>(P, g, nel_lds, q, it.rec, key, k, ewold, live && lane > kf);
+        (void)scat_attempt<-1>(P, g, nel_lds, q, it.rec, key, k, ewold, live && lane > kf, A.kn_cap);
       }
       if (lane == kf) {
         if (!(p.ew > thr)) atomicAdd(&c2d_cnt_lds[C2D_CNT_ABORTED], 1u);

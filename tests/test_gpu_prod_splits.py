@@ -15,6 +15,9 @@ mode is bit-identical to them in tests/test_oracle_golden.py):
   gmax = 1e5 tail and resamples 300 copies (src/imctrk2d.f:584-704); the
   secondaries run as scatter generations.
 
+The scatter kernels' cooperative paths are forced on prod_dense through the
+test knobs C2D_KN_CAP_ITERS and C2D_SC_K1_ATTEMPTS.
+
 Bar (as tests/test_gpu_parity.py): the exact build is bit-identical to the
 oracle's lineage mode (counters, census records by key, escape events) with
 tallies to 1e-11 (f64 atomic order), in both census layouts; the secondary
@@ -137,5 +140,29 @@ def test_exact_kernel_bit_parity_production_splits_few_waves(monkeypatch):
         eng.transport_step(si)
         assert orc.step(si) == 0
         _assert_same_histories(eng, orc, "few waves step %d" % n)
+    eng.close()
+    orc.close()
+
+
+@pytest.mark.parametrize("kn,sc", [("0", "0"), ("1", "1"), ("0", "16"), ("32", "0")])
+def test_exact_kernel_bit_parity_cooperative_scatter(monkeypatch, kn, sc):
+    """The scatter kernels' wave-cooperative paths forced on prod_dense:
+    C2D_KN_CAP_ITERS = 0 resolves every compb2d first loop (compb_2d.f:59-93)
+    64 iterations per round across the wave (transport.hip kn_coop), and
+    C2D_SC_K1_ATTEMPTS = 0 sends every split3 copy to the hard kernel (one
+    wave per copy, 64 resamples per round, the ones past the first success
+    rolled back).  Iteration j of the first loop draws counters c0 + 5j ..
+    c0 + 5j + 4 and resample k sub-stream k in both the kernels and the
+    oracle's lineage mode, so the histories stay the oracle's bit for bit."""
+    monkeypatch.setenv("C2D_KN_CAP_ITERS", kn)
+    monkeypatch.setenv("C2D_SC_K1_ATTEMPTS", sc)
+    gc = GoldenCase("prod_dense")
+    eng = Engine(gc.grid(comtot_mode=abi.COMTOT_EXACT))
+    orc = OL.Oracle(gc.grid(), OL.RNG_LINEAGE, "det")
+    for n in range(gc.nsteps):
+        si = gc.step_inputs(n)
+        eng.transport_step(si)
+        assert orc.step(si) == 0
+        _assert_same_histories(eng, orc, "kn %s sc %s step %d" % (kn, sc, n))
     eng.close()
     orc.close()
