@@ -174,7 +174,7 @@ def _fib_check(seed):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--runs", type=int, default=1200)
+    ap.add_argument("--runs", type=int, default=5000)
     ap.add_argument("--procs", type=int, default=8)
     ap.add_argument("--work", default="/tmp/c2d_compton_fib")
     ap.add_argument("--lin-runs", type=int, default=256)

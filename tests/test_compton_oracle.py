@@ -8,7 +8,7 @@ the Compton component of the RNG swap (tests/compton_case.py).
   recomputed bit for bit.
 * The lineage streams, with probe bundles and with per-copy probes
   (compton_lin: 256 runs each), against the reference streams (compton_fib:
-  1200 runs), all runs of 1e5 sources: a chi^2 over the Compton bins of F(E)
+  5000 runs), all runs of 1e5 sources: a chi^2 over the Compton bins of F(E)
   and a z per Compton light-curve band from run-to-run variances, printed.
 """
 from multiprocessing import get_context
@@ -47,12 +47,13 @@ def test_compton_fixtures_recompute_bitwise():
 def test_lineage_streams_compton_component_vs_reference_streams(capsys):
     """The lineage streams with probe bundles (the GPU's algorithm), and with
     per-copy probes, against the reference's algorithm on its own streams:
-    compton_lin.npz's 256 + 256 lineage runs and compton_fib.npz's 1200
+    compton_lin.npz's 256 + 256 lineage runs and compton_fib.npz's 5000
     lagged-Fibonacci runs, all of FIB_SOURCES sources, every error from
     run-to-run scatter (CC.compare_runs).  Three pairs separate the RNG swap
     (per-copy vs fib) from the superposition (bundles vs per-copy).  Each:
     chi^2 p-value over the Compton bins of F(E) > 1e-3, rms z <= 1.2, no bin
-    beyond 4.5 sigma, every Compton band within 4 sigma, rel L2 of F(E)
+    beyond its permutation null's 99.9 % (CC.perm_max_z: the top tail bins are
+    too skewed for a normal bar at 256 runs), every Compton band within 4 sigma, rel L2 of F(E)
     within the 99.9 % quantile of its sampling distribution; collision rates
     within 4 sigma.  (Round 3 used 8 lineage shards for the lineage sigma:
     rms z 1.42 was that estimator's noise.)"""
@@ -74,7 +75,13 @@ def test_lineage_streams_compton_component_vs_reference_streams(capsys):
     for k, d in res.items():
         assert d["p_value"] > 1e-3, (k, d)
         assert d["rms_z"] <= 1.2, (k, d)
-        assert d["max_abs_z"] <= 4.5, (k, d)
+        # the largest bin |z| against its permutation null (CC.perm_max_z):
+        # runs of one size on both sides, so they are exchangeable
+        a, b = k.split(" vs ")
+        zmax, p_perm, q999 = CC.perm_max_z(sides[a][0], sides[b][0])
+        with capsys.disabled():
+            print("%s: max |z| %.2f, permutation p %.4f (99.9 %% quantile %.2f)" % (k, zmax, p_perm, q999))
+        assert p_perm > 1e-3, (k, zmax, p_perm, q999)
         for i in CC.COMPTON_BANDS:
             assert abs(d["band_z"][i]) <= 4.0, (k, i, d)
         assert d["rel_l2"] <= d["rel_l2_bound_999"], (k, d)

@@ -126,7 +126,7 @@ def test_fast_kernel_compton_vs_reference_streams(capsys):
     lineages, with the census emptied in between; a run's F(E) and bands do
     not depend on its size, only their scatter does), against the
     reference's algorithm on its own lagged-Fibonacci streams
-    (compton_fib.npz, 1200 runs) and against the CPU bundle runs
+    (compton_fib.npz, 5000 runs) and against the CPU bundle runs
     (compton_lin.npz): both sides' errors from their run-to-run scatter
     (CC.compare_runs).  Bounds: chi^2 p-value > 1e-3 over the Compton bins,
     rms z <= 1.2, no bin beyond 4.5 sigma, each Compton band within 4 sigma;
