@@ -1509,8 +1509,8 @@ static int run_step_body(c2d_ctx* c) {
     /* test knobs: 0 sends every compb2d first loop to the wave's cooperative
      * resolution, and every split3 copy to the hard kernel */
     int32_t kn_cap = C2D_KN_CAP_DEFAULT, sc_k1 = C2D_SC_K1_DEFAULT;
-    if (const char* e = getenv("C2D_KN_CAP_ITERS")) kn_cap = (int32_t)std::max(0, std::min(1 << 20, atoi(e)));
-    if (const char* e = getenv("C2D_SC_K1_ATTEMPTS")) sc_k1 = (int32_t)std::max(0, std::min(1 << 20, atoi(e)));
+    if (const char* e = getenv("C2D_KN_CAP_ITERS")) kn_cap = (int32_t)std::max(0, std::min(4096, atoi(e)));
+    if (const char* e = getenv("C2D_SC_K1_ATTEMPTS")) sc_k1 = (int32_t)std::max(0, std::min(4096, atoi(e)));
     for (int64_t b = 0; b < total; b += pk_chunk) {
       const int64_t e = std::min<int64_t>(total, b + pk_chunk);
       HIPCHK(c, hipMemsetAsync(c->ctl + CTL_NPK, 0, sizeof(unsigned long long), c->stream));

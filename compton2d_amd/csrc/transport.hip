@@ -867,7 +867,8 @@ __device__ __forceinline__ int compb2d_w(const KParams& P, const Geo* g, double*
   KnState st;
   st.i = 0; st.j = 0; st.ctrA = 0;
   bool need = false;
-  if (run) need = !kn_loop<TALLY>(P, nel, p, st, kn_cap);
+  /* kn_coop needs a live iteration left (it ends at MAX_REJECT - 1) */
+  if (run) need = !kn_loop<TALLY>(P, nel, p, st, kn_cap < MAX_REJECT - 1 ? kn_cap : MAX_REJECT - 1);
   kn_coop<TALLY>(P, nel, p, st, need);
   int i_gam = 0;
   if (run) i_gam = compb2d_b<TALLY>(P, g, p, st);
