@@ -128,6 +128,19 @@ def test_exact_kernel_bit_parity_few_waves(monkeypatch, name, inplace):
 
 @pytest.mark.parametrize("name", CASES)
 def test_fast_kernel_close_to_oracle(name):
+    _assert_fast_close(name)
+
+
+def test_fast_kernel_close_to_oracle_cooperative_scatter(monkeypatch):
+    """prod_dense's secondaries with every compb2d first loop resolved by the
+    wave and every split3 copy in the hard kernel (test knobs; the exact
+    build's bitwise runs are in test_gpu_prod_splits.py)."""
+    monkeypatch.setenv("C2D_KN_CAP_ITERS", "0")
+    monkeypatch.setenv("C2D_SC_K1_ATTEMPTS", "0")
+    _assert_fast_close("prod_dense")
+
+
+def _assert_fast_close(name):
     for n, eng, orc in _run_pair(name, abi.COMTOT_TABLE):
         tg, to = eng.tallies(), orc.split()
         for c in COUNTERS:
