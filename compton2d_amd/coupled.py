@@ -93,7 +93,11 @@ class CoupledRun:
         if self.allreduce is not None:
             self.allreduce()
         t3 = _time.perf_counter()
-        tal = eng.tallies_raw()
+        # what the step reads back: this step's ecens (the next step's ec_old)
+        # and the counters, not the whole tally buffer
+        o = self._ecens
+        ecens_now = eng.tally_range(o[0], o[1])
+        c = eng.tally_range(self._cnt, abi.NCOUNTERS)
         fp_ms = 0.0
         fp_mode = None
         if self.fp_on and ncycle > 0:
@@ -112,9 +116,7 @@ class CoupledRun:
             fp_ms = eng.last_fp_ms()
             fp_mode = abi.FP_MODE_NAMES.get(eng.last_fp_mode())
         t4 = _time.perf_counter()
-        o = self._ecens
-        self.ecens_prev = tal[o[0]:o[0] + o[1]].reshape(nz, nr).copy()
-        c = tal[self._cnt:self._cnt + abi.NCOUNTERS]
+        self.ecens_prev = ecens_now.reshape(nz, nr)
         g0_ms, all_ms, _ = eng.last_kernel_ms()
         g0_paths, all_paths = eng.last_path_steps()
         self.last = dict(

@@ -51,6 +51,8 @@ extern "C" int c2d_fp_fast_block(int ncell, int n_simd);
 extern "C" int c2d_fp_mom_build(const double* mcd, double* mom, hipStream_t stream);
 extern "C" int c2d_fp_waves(int ncell, int n_simd);
 extern "C" int c2d_launch_vem(const VemParams* P, int ncell, hipStream_t s);
+extern "C" int c2d_launch_obs_segs(const ObsDev* O, const double* const* ev, const int64_t* n, int nseg,
+                                   int grid, hipStream_t stream);
 extern "C" int c2d_launch_obs(const ObsDev* O, const double* ev, int64_t n, int grid,
                               hipStream_t s);
 extern "C" size_t c2d_obs_lds_bytes(int n_t, int n_mu, int n_e, int lds_rows);
@@ -1686,6 +1688,16 @@ extern "C" int c2d_tally_download(c2d_ctx* c, double* host, int64_t n) {
   return C2D_OK;
 }
 
+extern "C" int c2d_tally_download_range(c2d_ctx* c, double* host, int64_t offset, int64_t n) {
+  if (!c || (!host && n > 0) || offset < 0 || n < 0 || offset + n > c->L.total) return C2D_E_ARG;
+  if (n == 0) return C2D_OK;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  /* synchronous like c2d_tally_download: ordered after the library's stream
+   * and a caller's all-reduce on the null stream alike */
+  HIPCHK(c, hipMemcpy(host, c->T + offset, sizeof(double) * n, hipMemcpyDeviceToHost));
+  return C2D_OK;
+}
+
 extern "C" int c2d_events(c2d_ctx* c, double* buf, int64_t cap, int64_t* n) {
   if (!c || !n) return C2D_E_ARG;
   *n = c->n_ev;
@@ -2647,11 +2659,12 @@ extern "C" int c2d_obs_begin(c2d_ctx* c, const c2d_obs_bins* b) {
   {
     const size_t edges = c2d_obs_lds_bytes(b->n_t, b->n_mu, b->n_e, 0);
     const size_t row = c2d_obs_lds_bytes(0, b->n_mu, b->n_e, 1) - c2d_obs_lds_bytes(0, b->n_mu, b->n_e, 0);
-    const size_t avail = c->lds_max > edges ? c->lds_max - edges : 0;
+    /* 1 KiB for the kernel's static segment table (observe.hip ObsSegs) */
+    const size_t avail = c->lds_max > edges + 1024 ? c->lds_max - edges - 1024 : 0;
     O.lds_rows = (int)std::min<size_t>((size_t)b->n_t, avail / row);
     const size_t bytes = c2d_obs_lds_bytes(b->n_t, b->n_mu, b->n_e, O.lds_rows);
     /* workgroups per CU that fit the CU's 160 KiB of LDS, at most 4 */
-    c->obs_wg_per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / std::max<size_t>(bytes, 1)));
+    c->obs_wg_per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / (bytes + 1024)));
   }
   auto sorted = [](const double* lo, const double* hi, int n) {
     for (int i = 1; i < n; i++)
@@ -2687,10 +2700,9 @@ static int obs_launch_segments(c2d_ctx* c, const double* const* ev, const int64_
   /* enough blocks to fill the chip, each privatising its own histogram */
   const int64_t bs = c2d_obs_block();
   HIPCHK(c, hipEventRecord(c->ev_g0a, c->stream));
-  for (int s = 0; s < nseg; s++) {
-    if (m[s] == 0) continue;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * c->obs_wg_per_cu, (m[s] + bs - 1) / bs));
-    int rc = c2d_launch_obs(&c->obs, ev[s], m[s], grid, c->stream);
+  {   /* every segment in one launch */
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * c->obs_wg_per_cu, (tot + bs - 1) / bs));
+    int rc = c2d_launch_obs_segs(&c->obs, ev, m, nseg, grid, c->stream);
     if (rc) return fail(c, C2D_E_HIP, "obs launch: %s", hipGetErrorString((hipError_t)rc));
   }
   HIPCHK(c, hipEventRecord(c->ev_g0b, c->stream));
@@ -2727,6 +2739,10 @@ extern "C" int c2d_obs_accumulate(c2d_ctx* c, const double* events, int64_t n) {
     HIPCHK(c, hipStreamWaitEvent(c->obs_stream, c->ev_obs_src, 0));
     const int64_t bs = c2d_obs_block();
     HIPCHK(c, hipEventRecord(c->ev_obs_a, c->obs_stream));
+    /* one launch per shard: between the short launches the FP update's
+     * workgroups (69 KB of LDS each) find room beside them (binning all
+     * shards in one launch beside the FP slowed it 1.26 -> 2.3-2.8 ms,
+     * at one or two workgroups per CU) */
     for (int s = 0; s < C2D_EV_SHARDS; s++) {
       if (cnt[s] == 0) continue;
       const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)c->n_cu * c->obs_wg_per_cu, (cnt[s] + bs - 1) / bs));

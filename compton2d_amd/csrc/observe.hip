@@ -76,8 +76,20 @@ __device__ inline int first_bin(const double* lo, const double* hi, int n, bool 
   return (a < n && x >= lo[a]) ? a : n;
 }
 
-__global__ void __launch_bounds__(OBS_BLOCK) c2d_obs_kernel(const ObsDev O, const double* __restrict__ ev,
-                                                          int64_t n) {
+/* the event segments of one launch (the transport's event shards, back to
+ * back): event e lies in segment s with pre[s] <= e < pre[s + 1] */
+struct ObsSegs {
+  const double* base[C2D_EV_SHARDS];
+  int64_t pre[C2D_EV_SHARDS + 1];
+  int32_t nseg;
+};
+
+__global__ void __launch_bounds__(OBS_BLOCK) c2d_obs_kernel(const ObsDev O, const ObsSegs S) {
+  __shared__ int64_t seg_pre[C2D_EV_SHARDS + 1];
+  __shared__ const double* seg_base[C2D_EV_SHARDS];
+  if (threadIdx.x <= (unsigned)S.nseg) seg_pre[threadIdx.x] = S.pre[threadIdx.x];
+  if (threadIdx.x < (unsigned)S.nseg) seg_base[threadIdx.x] = S.base[threadIdx.x];
+  const int64_t n = S.pre[S.nseg];
   extern __shared__ double sh[];
   double* t0 = sh;
   double* t1 = t0 + O.n_t;
@@ -111,7 +123,13 @@ __global__ void __launch_bounds__(OBS_BLOCK) c2d_obs_kernel(const ObsDev O, cons
   for (int64_t base = (int64_t)blockIdx.x * OBS_BLOCK; base < n; base += (int64_t)gridDim.x * OBS_BLOCK) {
     const int64_t e = base + threadIdx.x;
     const bool valid = e < n;
-    const double* v = ev + (valid ? e : 0) * C2D_EVENT_WORDS;
+    const int64_t ee = valid ? e : 0;
+    int sg = 0;                            /* last segment with seg_pre[sg] <= ee */
+    for (int hi = S.nseg - 1; sg < hi;) {
+      const int m = (sg + hi + 1) >> 1;
+      if (seg_pre[m] <= ee) sg = m; else hi = m - 1;
+    }
+    const double* v = seg_base[sg] + (ee - seg_pre[sg]) * C2D_EVENT_WORDS;
     double t_bound = v[0], E = v[1], ew = v[2];
     const double r = v[3], z = v[4];
     double mu = v[5];
@@ -165,15 +183,33 @@ extern "C" size_t c2d_obs_lds_bytes(int n_t, int n_mu, int n_e, int lds_rows) {
 
 extern "C" int c2d_obs_block(void) { return c2d::OBS_BLOCK; }
 
-extern "C" int c2d_launch_obs(const c2d::ObsDev* O, const double* ev, int64_t n, int grid,
-                              hipStream_t stream) {
-  if (n <= 0) return 0;
+/* one launch over nseg event segments (ev[s], n[s] events each; at most
+ * C2D_EV_SHARDS): the transport's event shards binned together */
+extern "C" int c2d_launch_obs_segs(const c2d::ObsDev* O, const double* const* ev, const int64_t* n, int nseg,
+                                   int grid, hipStream_t stream) {
+  if (nseg < 1 || nseg > C2D_EV_SHARDS) return (int)hipErrorInvalidValue;
+  c2d::ObsSegs S;
+  int k = 0;
+  S.pre[0] = 0;
+  for (int s = 0; s < nseg; s++) {
+    if (n[s] <= 0) continue;
+    S.base[k] = ev[s];
+    S.pre[k + 1] = S.pre[k] + n[s];
+    k++;
+  }
+  if (k == 0) return 0;
+  S.nseg = k;
   const size_t lds = c2d_obs_lds_bytes(O->n_t, O->n_mu, O->n_e, O->lds_rows);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)c2d::c2d_obs_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL(c2d::c2d_obs_kernel, dim3(grid), dim3(c2d::OBS_BLOCK), lds, stream, *O, ev, n);
+  hipLaunchKernelGGL(c2d::c2d_obs_kernel, dim3(grid), dim3(c2d::OBS_BLOCK), lds, stream, *O, S);
   return (int)hipGetLastError();
+}
+
+extern "C" int c2d_launch_obs(const c2d::ObsDev* O, const double* ev, int64_t n, int grid,
+                              hipStream_t stream) {
+  return c2d_launch_obs_segs(O, &ev, &n, 1, grid, stream);
 }

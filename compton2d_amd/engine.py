@@ -70,6 +70,8 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
     lib.c2d_tally_device_ptr.argtypes = [vp]
     lib.c2d_tally_download.restype = C.c_int
     lib.c2d_tally_download.argtypes = [vp, C.POINTER(C.c_double), C.c_int64]
+    lib.c2d_tally_download_range.restype = C.c_int
+    lib.c2d_tally_download_range.argtypes = [vp, C.POINTER(C.c_double), C.c_int64, C.c_int64]
     lib.c2d_events.restype = C.c_int
     lib.c2d_events.argtypes = [vp, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_int64)]
     lib.c2d_census_count.restype = C.c_int
@@ -222,6 +224,13 @@ class Engine:
         out = np.zeros(self.layout.total, np.float64)
         self._check(self.lib.c2d_tally_download(
             self.ctx, out.ctypes.data_as(C.POINTER(C.c_double)), out.size))
+        return out
+
+    def tally_range(self, offset: int, n: int) -> np.ndarray:
+        """Tally words [offset, offset + n) of the fused buffer (c2d_tally_download_range)."""
+        out = np.zeros(n, np.float64)
+        self._check(self.lib.c2d_tally_download_range(
+            self.ctx, out.ctypes.data_as(C.POINTER(C.c_double)), int(offset), int(n)))
         return out
 
     def tallies(self) -> dict:

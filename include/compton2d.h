@@ -389,6 +389,9 @@ int  c2d_tally_layout_get(c2d_ctx* ctx, c2d_tally_layout* out);
 double* c2d_tally_device_ptr(c2d_ctx* ctx);
 /* Copy the fused tally buffer to host memory (total doubles). */
 int  c2d_tally_download(c2d_ctx* ctx, double* host, int64_t n);
+/* Copy tally words [offset, offset + n) of the fused buffer to host memory
+ * (e.g. one tally and the counters, instead of the whole buffer per step). */
+int  c2d_tally_download_range(c2d_ctx* ctx, double* host, int64_t offset, int64_t n);
 
 /* Escape events of the last step: copies min(cap, n) records. */
 int  c2d_events(c2d_ctx* ctx, double* buf, int64_t cap, int64_t* n);
