@@ -211,6 +211,14 @@ module compton2d
        integer(c_int64_t), value :: n
      end function c2d_tally_download
 
+     integer(c_int) function c2d_tally_download_range(ctx, host, offset, n) &
+         bind(C, name='c2d_tally_download_range')
+       import :: c_int, c_ptr, c_double, c_int64_t
+       type(c_ptr), value :: ctx
+       real(c_double), intent(out) :: host(*)
+       integer(c_int64_t), value :: offset, n
+     end function c2d_tally_download_range
+
      integer(c_int) function c2d_events(ctx, buf, cap, n) bind(C, name='c2d_events')
        import :: c_int, c_ptr, c_double, c_int64_t
        type(c_ptr), value :: ctx
